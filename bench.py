@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""Benchmark of the path-tracing hot path on MI355X.
+
+Metric (BASELINE.json): "Mrays/sec + wall-clock render time, CBdragon 1024x1024
+@ 64 spp".  A "step" is one full-frame render (every 32x32 tile of the
+reference's FIFO) of the C3 workload: 1024x1024, 64 spp, max_ray_depth 4,
+ns_area_light 1 (readme.txt:1 settings) on the CBdragon proxy CBbunny_sub1
+(114,316 triangles; CBdragon.dae is absent).
+Mrays/s = W*H*spp*frames / seconds / 1e6 (primary path samples, the unit of the
+reference's "Primary (M ray/s)" column); scene load / BVH build / upload are
+outside the timed region, as in the reference's timers.
+
+N > 1 (one process per GPU, torchrun): ranks render interleaved 32x32 tiles
+(tile_id mod N) into a zeroed device frame and the frames are summed onto rank 0
+with an RCCL reduce over xGMI (non-owners add +0.0, so the image is bit-identical
+to the 1-GPU image); per-GPU work is fixed per frame => "scaling": "strong" is
+NOT what happens here: total work per step is fixed, so scaling is "strong".
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+W, H, SPP, DEPTH, NSL, SEED = 1024, 1024, 64, 4, 1, 1
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes(st: dict) -> float:
+    """SURVEY.md §8(d) reference-layout cost model: 64 B per BVH node visit,
+    48 B per triangle test, 16 B per sphere test, 4 B per leaf primitive index,
+    36 B per hit (vertex normals), 12 B per pixel written."""
+    prim = st["tri_tests"] + st["sphere_tests"]
+    return (64.0 * st["node_visits"] + 48.0 * st["tri_tests"] + 16.0 * st["sphere_tests"] + 4.0 * prim
+            + 36.0 * st["ext_hits"] + 12.0 * st["pixels"])
+
+
+def cpu_baseline(scene_dump: str, budget_s: float = 12.0) -> dict:
+    """Reference CPU algorithm (oracle/restate.cpp, bit-identical to the
+    reference binary at -t 1: glibc rand, one thread) timed on this host on a
+    bounded sample of the same workload: every k-th tile of the 1024x1024 FIFO
+    at the full 64 spp."""
+    from tests.oracle_helpers import Restatement
+    rs = Restatement()
+    ntiles = (W // 32) * (H // 32)
+    # calibrate on one tile, then size the sample to ~budget_s
+    t0 = time.perf_counter()
+    rs.render(scene_dump, W, H, SPP, DEPTH, NSL, SEED, rng_mode=0, tile_begin=ntiles // 2, tile_end=ntiles // 2 + 1)
+    one = max(time.perf_counter() - t0, 1e-3)
+    step = max(1, int(ntiles * one / budget_s))
+    total_t, total_px = 0.0, 0
+    for ti in range(0, ntiles, step):
+        t0 = time.perf_counter()
+        rs.render(scene_dump, W, H, SPP, DEPTH, NSL, SEED, rng_mode=0, tile_begin=ti, tile_end=ti + 1)
+        total_t += time.perf_counter() - t0
+        total_px += 32 * 32
+    return {"value": total_px * SPP / total_t / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
+            "sample": f"every {step}th 32x32 tile of the 1024x1024 frame ({total_px} px) at 64 spp, -m 4 -l 1, "
+                      f"oracle/restate.cpp glibc-rand mode (== reference -t 1), {total_t:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scene-dump", default=None, help="PTDUMP scene instead of the native .dae loader")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(local)
+
+    from dsgpuraytracing_amd import scenes
+    from dsgpuraytracing_amd.pathtracer import Device, Scene, tile_fifo
+
+    t_load = time.perf_counter()
+    if args.scene_dump:
+        scene = Scene.from_dump(args.scene_dump)
+        dump_path = args.scene_dump
+    else:
+        dae = scenes.proxy_path(1)
+        scene = Scene.from_dae(dae, W, H)
+        dump_path = None
+    dev = Device(local)
+    dev.upload_scene(scene)
+    dev.set_camera(scene.camera)
+    dev.set_params(W, H, SPP, DEPTH, NSL, SEED)
+    t_load = time.perf_counter() - t_load
+
+    tiles = tile_fifo(W, H)[rank::world]
+    frame = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{local}")
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step(stats=False):
+        dev.render_tiles_device(tiles, frame.data_ptr(), stream, stats=stats)
+        if world > 1:
+            dist.reduce(frame, dst=0)
+        return dev.stats()
+
+    # counters for the roofline's algorithmic bytes (deterministic: same work as every step)
+    st_counts = step(stats=True)
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        if world > 1:
+            frame.zero_()
+        s = step()
+        kernel_ms.append(s["last_ms"])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        counts = torch.tensor([st_counts[k] for k in ("node_visits", "tri_tests", "sphere_tests", "ext_hits",
+                                                      "pixels")], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(counts)
+
+    if rank == 0:
+        frames = args.steps
+        value = W * H * SPP * frames / elapsed / 1e6
+        bytes_launch = algorithmic_bytes(st_counts)
+        avg_ms = float(np.mean(kernel_ms))
+        achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
+        img = frame.float().cpu().numpy()
+        out = {
+            "metric": "Mrays/sec + wall-clock render time, CBdragon 1024x1024 @ 64 spp",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / frames * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic: deterministic CBbunny_sub1 proxy for the missing CBdragon.dae (SURVEY §8(d))",
+            "config": {"workload": "C3 CBbunny_sub1 (114,316 tris) 1024x1024 64spp -m 4 -l 1, default camera",
+                       "width": W, "height": H, "spp": SPP, "max_ray_depth": DEPTH, "ns_area_light": NSL,
+                       "parallelism": f"tiles{world}" if world > 1 else "single",
+                       "render_time_s": round(elapsed / frames, 4), "scene_load_s": round(t_load, 3)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "render_kernel<false>", "kernel_ms": round(avg_ms, 3),
+                         "algorithmic_bytes_per_launch": bytes_launch},
+            "counters": {k: st_counts[k] for k in ("camera_rays", "bounce_rays", "shadow_rays", "node_visits",
+                                                   "tri_tests", "sphere_tests", "ext_hits")},
+            "image_mean": float(img.mean()),
+        }
+        rays = st_counts["camera_rays"] + st_counts["bounce_rays"] + st_counts["shadow_rays"]
+        out["ray_casts_per_s_M"] = round(rays * frames / elapsed / 1e6 if world == 1 else float("nan"), 1)
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                dp = dump_path
+                if dp is None:
+                    from dsgpuraytracing_amd import scene_loader
+                    dp = os.path.join(ROOT, "_scenes", "bench_sub1_1024.ptd")
+                    scene_loader.dump_dae(scenes.proxy_path(1), W, H, dp)
+                out["cpu_baseline"] = cpu_baseline(dp)
+            except Exception as e:  # reported, never silently replaced
+                out["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

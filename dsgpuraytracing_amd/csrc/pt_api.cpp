@@ -1,0 +1,481 @@
+// pt_api.cpp — C ABI of the HIP path (include/ptgpu.h): device context, scene
+// upload (reference BVH -> 64-B two-child-box nodes, primitives -> 48-B float
+// records), tile rendering, batched ray queries, counters.
+//
+// Replaces CUDAPathTracer (cuda_src/setup.h:90-148, setup.cu:92-843): instead of
+// one cudaMalloc+cudaMemcpy per BVH node (setup.cu:429-476), constant-memory
+// tables capped at 20 entries (kernel.cu:3-20) and exit() on error, the scene is
+// flattened on the host into four contiguous arrays, uploaded once, and every
+// failure is returned as a PT_E_* code with a message in pt_last_error().
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ptgpu.h"
+#include "pt_device.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                            \
+  do {                                                                                          \
+    hipError_t _e = (expr);                                                                     \
+    if (_e != hipSuccess) return fail(PT_E_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t reserve(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T));
+    if (e == hipSuccess) n = std::max<size_t>(count, 1);
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+float round_down(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = std::nextafter(f, -INFINITY);
+  return f;
+}
+float round_up(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = std::nextafter(f, INFINITY);
+  return f;
+}
+
+}  // namespace
+
+struct pt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  DevBuf<DNode> nodes;
+  DevBuf<DPrim> prims;
+  DevBuf<float> norms;
+  DevBuf<DBsdf> bsdfs;
+  DevBuf<DLight> lights;
+  DevBuf<int4> tiles;
+  DevBuf<float> frame;  // device framebuffer for host-output renders
+  DevBuf<uint32_t> counter;
+  DevBuf<unsigned long long> stats;
+  DevBuf<float> q_f;    // ray-query scratch
+  DevBuf<int32_t> q_i;
+  int n_lights = 0;
+  int64_t n_prims = 0;
+  bool have_scene = false, have_cam = false, have_params = false;
+  pt_camera cam{};
+  pt_params params{};
+  pt_stats last{};
+  int grid_plain = 0, grid_stats = 0;
+};
+
+extern "C" {
+
+const char* pt_last_error(void) { return g_err.c_str(); }
+
+int pt_create(int device, pt_ctx** out) {
+  if (!out) return fail(PT_E_INVALID, "pt_create: out is NULL");
+  *out = nullptr;
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(PT_E_INVALID, "pt_create: no such HIP device");
+  HIPCHK(hipSetDevice(device));
+  pt_ctx* c = new pt_ctx();
+  c->device = device;
+  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreate(&c->ev0));
+  HIPCHK(hipEventCreate(&c->ev1));
+  HIPCHK(c->counter.reserve(1));
+  HIPCHK(c->stats.reserve(8));
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  int bpc = 0;
+  HIPCHK(ptk_render_occupancy(&bpc, false));
+  c->grid_plain = std::max(1, bpc) * prop.multiProcessorCount;
+  HIPCHK(ptk_render_occupancy(&bpc, true));
+  c->grid_stats = std::max(1, bpc) * prop.multiProcessorCount;
+  *out = c;
+  return PT_OK;
+}
+
+int pt_destroy(pt_ctx* c) {
+  if (!c) return PT_OK;
+  (void)hipSetDevice(c->device);
+  c->nodes.release();
+  c->prims.release();
+  c->norms.release();
+  c->bsdfs.release();
+  c->lights.release();
+  c->tiles.release();
+  c->frame.release();
+  c->counter.release();
+  c->stats.release();
+  c->q_f.release();
+  c->q_i.release();
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return PT_OK;
+}
+
+int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
+  if (!c || !s) return fail(PT_E_INVALID, "pt_upload_scene: NULL argument");
+  if (s->n_prims <= 0 || s->n_nodes <= 0 || !s->prim_type || !s->prim_bsdf || !s->prim_geom || !s->prim_norm ||
+      !s->nodes)
+    return fail(PT_E_INVALID, "pt_upload_scene: empty scene");
+  if (s->n_bsdfs <= 0 || !s->bsdfs) return fail(PT_E_INVALID, "pt_upload_scene: no BSDFs");
+  if (s->n_lights < 0 || (s->n_lights > 0 && !s->lights)) return fail(PT_E_INVALID, "pt_upload_scene: bad lights");
+  if (s->n_prims > (int64_t)0x3fffffff) return fail(PT_E_INVALID, "pt_upload_scene: too many primitives");
+  HIPCHK(hipSetDevice(c->device));
+
+  // ---- primitives (already in BVH order)
+  std::vector<DPrim> prims((size_t)s->n_prims);
+  std::vector<float> norms((size_t)s->n_prims * 9);
+  for (int64_t i = 0; i < s->n_prims; ++i) {
+    const double* g = s->prim_geom + 9 * i;
+    const double* n = s->prim_norm + 9 * i;
+    int b = s->prim_bsdf[i];
+    if (b < 0 || b >= s->n_bsdfs) return fail(PT_E_INVALID, "pt_upload_scene: primitive BSDF index out of range");
+    DPrim& P = prims[(size_t)i];
+    if (s->prim_type[i] == PT_PRIM_TRIANGLE) {
+      int meta = (b << 1) | 1;
+      float mf;
+      std::memcpy(&mf, &meta, 4);
+      P.v0 = make_float4((float)g[0], (float)g[1], (float)g[2], mf);
+      P.e1 = make_float4((float)(g[3] - g[0]), (float)(g[4] - g[1]), (float)(g[5] - g[2]), 0.f);
+      P.e2 = make_float4((float)(g[6] - g[0]), (float)(g[7] - g[1]), (float)(g[8] - g[2]), 0.f);
+      for (int k = 0; k < 9; ++k) norms[9 * i + k] = (float)n[k];
+    } else if (s->prim_type[i] == PT_PRIM_SPHERE) {
+      int meta = (b << 1);
+      float mf;
+      std::memcpy(&mf, &meta, 4);
+      P.v0 = make_float4((float)g[0], (float)g[1], (float)g[2], mf);
+      P.e1 = make_float4((float)g[3], (float)(g[3] * g[3]), 0.f, 0.f);
+      P.e2 = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      return fail(PT_E_INVALID, "pt_upload_scene: unknown primitive type");
+    }
+  }
+
+  // ---- BVH: internal nodes only, pre-order, child boxes rounded outward.
+  const pt_bvh_node* N = s->nodes;
+  const int64_t nn = s->n_nodes;
+  auto is_leaf = [&](int64_t i) { return N[i].left < 0 && N[i].right < 0; };
+  for (int64_t i = 0; i < nn; ++i) {
+    if ((N[i].left < 0) != (N[i].right < 0)) return fail(PT_E_INVALID, "pt_upload_scene: half-empty BVH node");
+    if (N[i].left >= nn || N[i].right >= nn) return fail(PT_E_INVALID, "pt_upload_scene: BVH child out of range");
+    if (is_leaf(i) && (N[i].start < 0 || N[i].range <= 0 || N[i].start + N[i].range > s->n_prims))
+      return fail(PT_E_INVALID, "pt_upload_scene: bad leaf range");
+  }
+  std::vector<DNode> dn;
+  std::vector<int64_t> map(nn, -1);
+  int max_depth = 0;
+  auto set_child = [&](DNode& d, int side, int64_t ci) {
+    const pt_bvh_node& C = N[ci];
+    float lx = round_down(C.bb_min[0]), hx = round_up(C.bb_max[0]);
+    float ly = round_down(C.bb_min[1]), hy = round_up(C.bb_max[1]);
+    float lz = round_down(C.bb_min[2]), hz = round_up(C.bb_max[2]);
+    if (side == 0) {
+      d.a = make_float4(lx, hx, ly, hy);
+      d.c.x = lz;
+      d.c.y = hz;
+    } else {
+      d.b = make_float4(lx, hx, ly, hy);
+      d.c.z = lz;
+      d.c.w = hz;
+    }
+  };
+  if (is_leaf(0)) {
+    DNode d{};
+    set_child(d, 0, 0);
+    d.b = make_float4(1.f, -1.f, 1.f, -1.f);
+    d.c.z = 1.f;
+    d.c.w = -1.f;
+    d.e = make_int4((int)N[0].start, 0, (int)N[0].range, -1);
+    dn.push_back(d);
+    max_depth = 1;
+  } else {
+    // explicit DFS: (ref node, parent dnode, side, depth)
+    struct Item { int64_t ref; int64_t parent; int side; int depth; };
+    std::vector<Item> st = {{0, -1, 0, 1}};
+    while (!st.empty()) {
+      Item it = st.back();
+      st.pop_back();
+      int64_t me = (int64_t)dn.size();
+      dn.push_back(DNode{});
+      map[it.ref] = me;
+      max_depth = std::max(max_depth, it.depth);
+      if (it.parent >= 0) {
+        if (it.side == 0) dn[it.parent].e.x = (int)me;
+        else dn[it.parent].e.y = (int)me;
+      }
+      const pt_bvh_node& R = N[it.ref];
+      int64_t ch[2] = {R.left, R.right};
+      for (int side = 0; side < 2; ++side) {
+        set_child(dn[me], side, ch[side]);
+        if (is_leaf(ch[side])) {
+          if (side == 0) { dn[me].e.x = (int)N[ch[0]].start; dn[me].e.z = (int)N[ch[0]].range; }
+          else { dn[me].e.y = (int)N[ch[1]].start; dn[me].e.w = (int)N[ch[1]].range; }
+        }
+      }
+      // push right first so the left subtree follows its parent in memory
+      for (int side = 1; side >= 0; --side)
+        if (!is_leaf(ch[side])) st.push_back({ch[side], me, side, it.depth + 1});
+    }
+  }
+  if (max_depth > PT_STACK)
+    return fail(PT_E_INVALID, "pt_upload_scene: BVH deeper than the traversal stack (" + std::to_string(max_depth) +
+                                  " > " + std::to_string(PT_STACK) + ")");
+
+  std::vector<DBsdf> bs((size_t)s->n_bsdfs);
+  for (int i = 0; i < s->n_bsdfs; ++i) {
+    const pt_bsdf& B = s->bsdfs[i];
+    if (B.type < 0 || B.type > 4) return fail(PT_E_INVALID, "pt_upload_scene: unknown BSDF type");
+    DBsdf& d = bs[(size_t)i];
+    d.type = B.type;
+    for (int k = 0; k < 3; ++k) {
+      d.a[k] = B.albedo[k];
+      d.t[k] = B.transmittance[k];
+      d.e[k] = B.emission[k];
+    }
+    d.ior = B.ior;
+    d.pad = 0.f;
+  }
+  std::vector<DLight> ls((size_t)std::max(0, s->n_lights));
+  for (int i = 0; i < s->n_lights; ++i) {
+    const pt_light& L = s->lights[i];
+    if (L.type < 0 || L.type > 3) return fail(PT_E_INVALID, "pt_upload_scene: unsupported light type");
+    DLight& d = ls[(size_t)i];
+    std::memset(&d, 0, sizeof(d));
+    d.type = L.type;
+    for (int k = 0; k < 3; ++k) {
+      d.rad[k] = L.radiance[k];
+      d.pos[k] = (float)L.position[k];
+      d.dir[k] = (float)L.direction[k];
+      d.dimx[k] = (float)L.dim_x[k];
+      d.dimy[k] = (float)L.dim_y[k];
+    }
+    d.area = L.area;
+  }
+
+  HIPCHK(c->nodes.reserve(dn.size()));
+  HIPCHK(c->prims.reserve(prims.size()));
+  HIPCHK(c->norms.reserve(norms.size()));
+  HIPCHK(c->bsdfs.reserve(bs.size()));
+  HIPCHK(c->lights.reserve(std::max<size_t>(1, ls.size())));
+  HIPCHK(hipMemcpy(c->nodes.p, dn.data(), dn.size() * sizeof(DNode), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c->prims.p, prims.data(), prims.size() * sizeof(DPrim), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c->norms.p, norms.data(), norms.size() * sizeof(float), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c->bsdfs.p, bs.data(), bs.size() * sizeof(DBsdf), hipMemcpyHostToDevice));
+  if (!ls.empty()) HIPCHK(hipMemcpy(c->lights.p, ls.data(), ls.size() * sizeof(DLight), hipMemcpyHostToDevice));
+  c->n_lights = (int)ls.size();
+  c->n_prims = s->n_prims;
+  c->have_scene = true;
+  return PT_OK;
+}
+
+int pt_set_camera(pt_ctx* c, const pt_camera* cam) {
+  if (!c || !cam) return fail(PT_E_INVALID, "pt_set_camera: NULL argument");
+  if (!(cam->screen_dist > 0) || !(cam->screen_w > 0) || !(cam->screen_h > 0))
+    return fail(PT_E_INVALID, "pt_set_camera: non-positive screen size/distance");
+  c->cam = *cam;
+  c->have_cam = true;
+  return PT_OK;
+}
+
+int pt_set_params(pt_ctx* c, const pt_params* p) {
+  if (!c || !p) return fail(PT_E_INVALID, "pt_set_params: NULL argument");
+  if (p->width <= 0 || p->height <= 0 || p->spp <= 0 || p->max_depth < 0 || p->ns_area_light <= 0)
+    return fail(PT_E_INVALID, "pt_set_params: width/height/spp/ns_area_light must be positive, max_depth >= 0");
+  if ((int64_t)p->width * p->height > (int64_t)1 << 30) return fail(PT_E_INVALID, "pt_set_params: frame too large");
+  c->params = *p;
+  c->have_params = true;
+  return PT_OK;
+}
+
+static int build_tiles(pt_ctx* c, const pt_tile* tiles, int32_t n, std::vector<int4>& out) {
+  const int W = c->params.width, H = c->params.height;
+  for (int32_t i = 0; i < n; ++i) {
+    const pt_tile& t = tiles[i];
+    if (t.w < 0 || t.h < 0) return fail(PT_E_INVALID, "pt_render_tiles: negative tile size");
+    int x0 = std::max(0, t.x), y0 = std::max(0, t.y);
+    int x1 = std::min(W, t.x + t.w), y1 = std::min(H, t.y + t.h);  // raytrace_tile clamps (pathtracer.cpp:594-595)
+    for (int y = y0; y < y1; y += 32)
+      for (int x = x0; x < x1; x += 32) out.push_back(make_int4(x, y, std::min(32, x1 - x), std::min(32, y1 - y)));
+  }
+  return PT_OK;
+}
+
+static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStream_t s, uint32_t flags) {
+  const bool stats = (flags & PT_FLAG_STATS) != 0;
+  std::memset(&c->last, 0, sizeof(c->last));
+  if (tl.empty()) return PT_OK;
+  HIPCHK(c->tiles.reserve(tl.size()));
+  HIPCHK(hipMemcpyAsync(c->tiles.p, tl.data(), tl.size() * sizeof(int4), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(c->counter.p, 0, sizeof(uint32_t), s));
+  if (stats) HIPCHK(hipMemsetAsync(c->stats.p, 0, 8 * sizeof(unsigned long long), s));
+  KParams P;
+  std::memset(&P, 0, sizeof(P));
+  for (int k = 0; k < 3; ++k) {
+    P.cam_pos[k] = (float)c->cam.pos[k];
+    P.c2w_col0[k] = (float)c->cam.c2w[3 * k + 0];
+    P.c2w_col1[k] = (float)c->cam.c2w[3 * k + 1];
+    P.c2w_col2[k] = (float)c->cam.c2w[3 * k + 2];
+  }
+  P.cam_ax = (float)(c->cam.screen_w / c->cam.screen_dist);
+  P.cam_ay = (float)(c->cam.screen_h / c->cam.screen_dist);
+  P.W = c->params.width;
+  P.H = c->params.height;
+  P.spp = c->params.spp;
+  P.max_depth = c->params.max_depth;
+  P.ns_area = c->params.ns_area_light;
+  P.seed = c->params.seed;
+  P.n_lights = c->n_lights;
+  P.n_tiles = (int)tl.size();
+  P.nodes = c->nodes.p;
+  P.prims = c->prims.p;
+  P.norms = c->norms.p;
+  P.bsdfs = c->bsdfs.p;
+  P.lights = c->lights.p;
+  P.tiles = c->tiles.p;
+  P.out = out_dev;
+  P.work_counter = c->counter.p;
+  P.stats = c->stats.p;
+  int64_t slots = (int64_t)tl.size() * 1024;
+  int64_t max_grid = (slots + PT_BLOCK - 1) / PT_BLOCK;
+  int grid = (int)std::min<int64_t>(stats ? c->grid_stats : c->grid_plain, max_grid);
+  HIPCHK(hipEventRecord(c->ev0, s));
+  HIPCHK(ptk_launch_render(&P, grid, stats, s));
+  HIPCHK(hipEventRecord(c->ev1, s));
+  int64_t px = 0;
+  for (const int4& t : tl) px += (int64_t)t.z * t.w;
+  c->last.pixels = px;
+  c->last.samples = px * c->params.spp;
+  return PT_OK;
+}
+
+static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags) {
+  HIPCHK(hipStreamSynchronize(s));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  c->last.last_ms = ms;
+  if (flags & PT_FLAG_STATS) {
+    unsigned long long v[8] = {0};
+    HIPCHK(hipMemcpy(v, c->stats.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    c->last.camera_rays = (int64_t)v[0];
+    c->last.bounce_rays = (int64_t)v[1];
+    c->last.shadow_rays = (int64_t)v[2];
+    c->last.node_visits = (int64_t)v[3];
+    c->last.tri_tests = (int64_t)v[4];
+    c->last.sphere_tests = (int64_t)v[5];
+    c->last.ext_hits = (int64_t)v[6];
+    c->last.counters_valid = 1;
+  }
+  return PT_OK;
+}
+
+static int check_ready(pt_ctx* c) {
+  if (!c) return fail(PT_E_INVALID, "NULL context");
+  if (!c->have_scene || !c->have_cam || !c->have_params)
+    return fail(PT_E_NOSCENE, "render before pt_upload_scene / pt_set_camera / pt_set_params");
+  return PT_OK;
+}
+
+int pt_render_tiles(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, float* hdr_out_host, uint32_t flags) {
+  int rc = check_ready(c);
+  if (rc) return rc;
+  if (n_tiles < 0 || (n_tiles > 0 && (!tiles || !hdr_out_host))) return fail(PT_E_INVALID, "pt_render_tiles: bad args");
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<int4> tl;
+  if ((rc = build_tiles(c, tiles, n_tiles, tl))) return rc;
+  const size_t W = (size_t)c->params.width, H = (size_t)c->params.height;
+  HIPCHK(c->frame.reserve(W * H * 3));
+  if ((rc = launch(c, tl, c->frame.p, c->stream, flags))) return rc;
+  for (const int4& t : tl) {
+    size_t off = ((size_t)t.y * W + (size_t)t.x) * 3;
+    HIPCHK(hipMemcpy2DAsync(hdr_out_host + off, W * 3 * sizeof(float), c->frame.p + off, W * 3 * sizeof(float),
+                            (size_t)t.z * 3 * sizeof(float), (size_t)t.w, hipMemcpyDeviceToHost, c->stream));
+  }
+  return finish_stats(c, c->stream, flags);
+}
+
+int pt_render_tiles_device(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, float* hdr_out_dev, void* stream,
+                           uint32_t flags) {
+  int rc = check_ready(c);
+  if (rc) return rc;
+  if (n_tiles < 0 || (n_tiles > 0 && (!tiles || !hdr_out_dev)))
+    return fail(PT_E_INVALID, "pt_render_tiles_device: bad args");
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<int4> tl;
+  if ((rc = build_tiles(c, tiles, n_tiles, tl))) return rc;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if ((rc = launch(c, tl, hdr_out_dev, s, flags))) return rc;
+  return finish_stats(c, s, flags);
+}
+
+int pt_intersect(pt_ctx* c, int64_t n, const double* o, const double* d, const double* max_t, int32_t* hit, float* t,
+                 int32_t* prim, int32_t* any_hit) {
+  if (!c) return fail(PT_E_INVALID, "NULL context");
+  if (!c->have_scene) return fail(PT_E_NOSCENE, "pt_intersect before pt_upload_scene");
+  if (n < 0 || (n > 0 && (!o || !d || !max_t))) return fail(PT_E_INVALID, "pt_intersect: bad args");
+  if (n == 0) return PT_OK;
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<float> f((size_t)n * 7);
+  for (int64_t i = 0; i < 3 * n; ++i) {
+    f[(size_t)i] = (float)o[i];
+    f[(size_t)(3 * n + i)] = (float)d[i];
+  }
+  for (int64_t i = 0; i < n; ++i) f[(size_t)(6 * n + i)] = (float)max_t[i];
+  HIPCHK(c->q_f.reserve((size_t)n * 8));
+  HIPCHK(c->q_i.reserve((size_t)n * 3));
+  HIPCHK(hipMemcpyAsync(c->q_f.p, f.data(), f.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  float* dt = c->q_f.p + 7 * n;
+  int32_t* dh = c->q_i.p;
+  int32_t* dp = c->q_i.p + n;
+  int32_t* da = c->q_i.p + 2 * n;
+  HIPCHK(ptk_launch_intersect(c->nodes.p, c->prims.p, c->q_f.p, c->q_f.p + 3 * n, c->q_f.p + 6 * n, n, dh, dt, dp, da,
+                              c->stream));
+  std::vector<int32_t> ib((size_t)n * 3);
+  std::vector<float> tb((size_t)n);
+  HIPCHK(hipMemcpyAsync(ib.data(), c->q_i.p, ib.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(tb.data(), dt, tb.size() * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (int64_t i = 0; i < n; ++i) {
+    if (hit) hit[i] = ib[(size_t)i];
+    if (prim) prim[i] = ib[(size_t)(n + i)];
+    if (any_hit) any_hit[i] = ib[(size_t)(2 * n + i)];
+    if (t) t[i] = tb[(size_t)i];
+  }
+  return PT_OK;
+}
+
+int pt_get_stats(pt_ctx* c, pt_stats* out) {
+  if (!c || !out) return fail(PT_E_INVALID, "pt_get_stats: NULL argument");
+  *out = c->last;
+  return PT_OK;
+}
+
+}  // extern "C"

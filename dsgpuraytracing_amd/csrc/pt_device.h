@@ -1,0 +1,74 @@
+// pt_device.h — device-side data layout of the HIP path (shared by the kernels
+// and the host conversion in pt_api.cpp).  See DESIGN.md "Data layout in HBM".
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifndef PT_BLOCK
+#define PT_BLOCK 64  // one wave64 per workgroup: the persistent queue is per wave
+#endif
+#ifndef PT_STACK
+#define PT_STACK 64  // traversal stack entries per lane (LDS, lane-contiguous)
+#endif
+
+// BVH2 node, 64 B: both child boxes + child references.
+//  a = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
+//  b = (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
+//  c = (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
+//  e = (c0 ref, c1 ref, c0 count, c1 count): count 0 => ref is a node index,
+//      count > 0 => leaf primitives [ref, ref+count) in BVH order.
+struct alignas(16) DNode {
+  float4 a, b, c;
+  int4 e;
+};
+
+// Primitive, 48 B.  Triangle: v0 = (p1, meta), e1 = p2-p1, e2 = p3-p1.
+// Sphere: v0 = (o, meta), e1 = (r, r*r, 0, 0).  meta = (bsdf << 1) | is_triangle.
+struct alignas(16) DPrim {
+  float4 v0, e1, e2;
+};
+
+struct DBsdf {
+  int type;
+  float a[3];  // albedo / reflectance
+  float t[3];  // transmittance
+  float e[3];  // emission
+  float ior;
+  float pad;
+};
+
+struct DLight {
+  int type;
+  float rad[3];
+  float pos[3];
+  float dir[3];
+  float dimx[3];
+  float dimy[3];
+  float area;
+  float pad[2];
+};
+
+struct KParams {
+  float cam_pos[3];
+  float c2w_col0[3], c2w_col1[3], c2w_col2[3];
+  float cam_ax, cam_ay;  // screenW/screenDist, screenH/screenDist
+  int W, H, spp, max_depth, ns_area;
+  uint32_t seed;
+  int n_lights;
+  int n_tiles;  // 32x32 (or smaller) tiles: 1024 work slots each
+  const DNode* nodes;
+  const DPrim* prims;
+  const float* norms;  // 9 floats per primitive (vertex normals n1,n2,n3)
+  const DBsdf* bsdfs;
+  const DLight* lights;
+  const int4* tiles;  // (x, y, w, h)
+  float* out;         // W*H*3
+  uint32_t* work_counter;
+  unsigned long long* stats;  // 7 counters (PT_FLAG_STATS)
+};
+
+extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, hipStream_t s);
+extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prims, const float* o, const float* d,
+                                           const float* maxt, int64_t n, int32_t* hit, float* t, int32_t* prim,
+                                           int32_t* anyhit, hipStream_t s);
+extern "C" hipError_t ptk_render_occupancy(int* blocks_per_cu, bool stats);

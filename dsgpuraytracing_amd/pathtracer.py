@@ -1,0 +1,261 @@
+"""Host-side mirror of the reference's PathTracer interface over the HIP path.
+
+Reference: class PathTracer (src/pathtracer.h:55-272, src/pathtracer.cpp).
+Same names, argument meaning and state machine for the part of the interface
+that drives the hot path:
+
+  PathTracer(ns_aa, max_ray_depth, ns_area_light, ns_diff, ns_glsy, ns_refr,
+             num_threads, envmap)                       pathtracer.cpp:30-66
+  set_scene / set_camera / set_frame_size               pathtracer.cpp:76-122
+  start_raytracing  (all tiles of the 32x32 FIFO)       pathtracer.cpp:192-221
+  raytrace_tile(tile_x, tile_y, tile_w, tile_h)         pathtracer.cpp:585-611
+  raytrace_pixel(x, y)                                  pathtracer.cpp:555-583
+  sampleBuffer (HDR, float32 HxWx3, row 0 = bottom)     image.h:79-205
+  frameBuffer  (RGBA8 after toColor)                    image.h:174-189
+  save_image(path)                                      pathtracer.cpp:649-674
+
+Every pixel is computed by libptgpu.so on the GPU; nothing here falls back to
+the CPU.  `num_threads` is accepted for interface parity and ignored (the GPU
+schedules itself).  Randomness comes from the counter stream keyed by
+(seed, pixel, sample) instead of std::rand() (see csrc/pt_rng.h).
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import native, ptdump
+from .native import check, lib
+
+TILE = 32  # imageTileSize (pathtracer.cpp:57)
+
+
+class Device:
+    """One pt_ctx on one GPU (CUDAPathTracer's device state, setup.h:90-148)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = lib()
+        h = ctypes.c_void_p()
+        check(self._lib.pt_create(device, ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+        self._scene_keepalive = None
+
+    def close(self):
+        if self.handle:
+            self._lib.pt_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover - interpreter teardown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload_scene(self, scene: "Scene"):
+        check(self._lib.pt_upload_scene(self.handle, ctypes.byref(scene.arrays.scene)))
+        self._scene_keepalive = scene
+
+    def set_camera(self, cam: native.pt_camera):
+        check(self._lib.pt_set_camera(self.handle, ctypes.byref(cam)))
+
+    def set_params(self, width, height, spp, max_depth, ns_area_light, seed):
+        p = native.pt_params(width=width, height=height, spp=spp, max_depth=max_depth,
+                             ns_area_light=ns_area_light, seed=seed & 0xFFFFFFFF)
+        check(self._lib.pt_set_params(self.handle, ctypes.byref(p)))
+
+    @staticmethod
+    def _tiles(tiles: Sequence[Tuple[int, int, int, int]]):
+        arr = (native.pt_tile * max(1, len(tiles)))()
+        for i, (x, y, w, h) in enumerate(tiles):
+            arr[i] = native.pt_tile(x, y, w, h)
+        return arr
+
+    def render_tiles(self, tiles, out: np.ndarray, stats: bool = False):
+        assert out.dtype == np.float32 and out.flags.c_contiguous
+        arr = self._tiles(tiles)
+        flags = native.PT_FLAG_STATS if stats else 0
+        check(self._lib.pt_render_tiles(self.handle, arr, len(tiles), out.ctypes.data, flags))
+
+    def render_tiles_device(self, tiles, out_ptr: int, stream: int = 0, stats: bool = False):
+        arr = self._tiles(tiles)
+        flags = native.PT_FLAG_STATS if stats else 0
+        check(self._lib.pt_render_tiles_device(self.handle, arr, len(tiles), ctypes.c_void_p(out_ptr),
+                                               ctypes.c_void_p(stream or None), flags))
+
+    def intersect(self, o, d, max_t):
+        o = np.ascontiguousarray(o, np.float64)
+        d = np.ascontiguousarray(d, np.float64)
+        max_t = np.ascontiguousarray(max_t, np.float64)
+        n = len(max_t)
+        hit = np.zeros(n, np.int32)
+        t = np.zeros(n, np.float32)
+        prim = np.zeros(n, np.int32)
+        anyh = np.zeros(n, np.int32)
+        check(self._lib.pt_intersect(self.handle, n, o.ctypes.data, d.ctypes.data, max_t.ctypes.data,
+                                     hit.ctypes.data, t.ctypes.data, prim.ctypes.data, anyh.ctypes.data))
+        return hit, t, prim, anyh
+
+    def stats(self) -> dict:
+        s = native.pt_stats()
+        check(self._lib.pt_get_stats(self.handle, ctypes.byref(s)))
+        return {k: getattr(s, k) for k, _ in native.pt_stats._fields_}
+
+
+class Scene:
+    """A flattened scene (what BVHAccel + the lights hand to the GPU seam)."""
+
+    def __init__(self, arrays: native.SceneArrays):
+        self.arrays = arrays
+
+    @classmethod
+    def from_dump(cls, path: str) -> "Scene":
+        return cls(native.SceneArrays(ptdump.read(path)))
+
+    @classmethod
+    def from_dae(cls, path: str, width: int, height: int, cam_info: Optional[str] = None) -> "Scene":
+        from . import scene_loader
+        return cls(native.SceneArrays(scene_loader.load_dae(path, width, height, cam_info)))
+
+    @property
+    def camera(self) -> native.pt_camera:
+        return self.arrays.camera
+
+
+class State(enum.IntEnum):
+    INIT = 0
+    READY = 1
+    VISUALIZE = 2
+    RENDERING = 3
+    DONE = 4
+
+
+def tile_fifo(w: int, h: int, tile: int = TILE) -> List[Tuple[int, int, int, int]]:
+    """The reference's row-major tile work queue (pathtracer.cpp:209-214)."""
+    return [(x, y, tile, tile) for y in range(0, h, tile) for x in range(0, w, tile)]
+
+
+def to_color(hdr: np.ndarray) -> np.ndarray:
+    """HDRImageBuffer::toColor (image.h:174-189) + Color -> RGBA8
+    (ImageBuffer::update_pixel, image.h:49-58): c = (s*sqrt(2))^(1/2.2),
+    clamped to [0,1], times 255, truncated."""
+    gamma = np.float32(2.2)
+    one_over_gamma = np.float32(1.0) / gamma
+    exposure = np.float32(np.sqrt(np.float32(2.0)))
+    with np.errstate(invalid="ignore"):
+        c = np.power(hdr.astype(np.float32) * exposure, one_over_gamma)
+    c = np.nan_to_num(c, nan=0.0)
+    c = np.clip(c, 0.0, 1.0)
+    rgb = (c * 255).astype(np.uint8)
+    a = np.full(hdr.shape[:2] + (1,), 255, np.uint8)
+    return np.concatenate([rgb, a], axis=2)
+
+
+class PathTracer:
+    def __init__(self, ns_aa: int = 1, max_ray_depth: int = 4, ns_area_light: int = 1, ns_diff: int = 1,
+                 ns_glsy: int = 1, ns_refr: int = 1, num_threads: int = 1, envmap=None, device: int = 0,
+                 seed: int = 1):
+        if envmap is not None:
+            raise NotImplementedError("environment lights are not on the HIP path yet (SURVEY §8(f) rank 3)")
+        self.state = State.INIT
+        self.ns_aa = int(ns_aa)
+        self.max_ray_depth = int(max_ray_depth)
+        self.ns_area_light = int(ns_area_light)
+        self.ns_diff, self.ns_glsy, self.ns_refr = ns_diff, ns_diff, ns_refr  # pathtracer.cpp:38-40 (sic)
+        self.numWorkerThreads = int(num_threads)
+        self.imageTileSize = TILE
+        self.seed = int(seed)
+        self.scene: Optional[Scene] = None
+        self.camera: Optional[native.pt_camera] = None
+        self.sampleBuffer = np.zeros((0, 0, 3), np.float32)
+        self.frameBuffer = np.zeros((0, 0, 4), np.uint8)
+        self._device_index = device
+        self._dev: Optional[Device] = None
+        self.last_stats: dict = {}
+
+    # ---- configuration (pathtracer.cpp:76-127)
+    def _device(self) -> Device:
+        if self._dev is None:
+            self._dev = Device(self._device_index)
+        return self._dev
+
+    def has_valid_configuration(self) -> bool:
+        return self.scene is not None and self.camera is not None and self.sampleBuffer.size > 0
+
+    def set_scene(self, scene: Scene):
+        if self.state != State.INIT:
+            return
+        self.scene = scene
+        self._device().upload_scene(scene)
+        if self.has_valid_configuration():
+            self.state = State.READY
+
+    def set_camera(self, camera: native.pt_camera):
+        self.camera = camera
+        self._device().set_camera(camera)
+        if self.has_valid_configuration():
+            self.state = State.READY
+
+    def set_frame_size(self, width: int, height: int):
+        self.sampleBuffer = np.zeros((height, width, 3), np.float32)
+        self.frameBuffer = np.zeros((height, width, 4), np.uint8)
+        if self.has_valid_configuration():
+            self.state = State.READY
+
+    def clear(self):
+        if self.state != State.READY:
+            return
+        self.scene = None
+        self.camera = None
+        self.sampleBuffer = np.zeros((0, 0, 3), np.float32)
+        self.frameBuffer = np.zeros((0, 0, 4), np.uint8)
+        self.state = State.INIT
+
+    # ---- rendering
+    def _params(self):
+        h, w = self.sampleBuffer.shape[:2]
+        self._device().set_params(w, h, self.ns_aa, self.max_ray_depth, self.ns_area_light, self.seed)
+
+    def raytrace_tile(self, tile_x: int, tile_y: int, tile_w: int, tile_h: int, stats: bool = False):
+        """Drop-in for PathTracer::raytrace_tile: HDR for the tile, then toColor."""
+        self.render_tiles([(tile_x, tile_y, tile_w, tile_h)], stats=stats)
+
+    def render_tiles(self, tiles: Iterable[Tuple[int, int, int, int]], stats: bool = False):
+        if not self.has_valid_configuration():
+            raise RuntimeError("PathTracer is not configured (scene, camera, frame size)")
+        tiles = list(tiles)
+        self._params()
+        dev = self._device()
+        dev.render_tiles(tiles, self.sampleBuffer, stats=stats)
+        self.last_stats = dev.stats()
+        h, w = self.sampleBuffer.shape[:2]
+        for (x, y, tw, th) in tiles:
+            x1, y1 = min(x + tw, w), min(y + th, h)
+            self.frameBuffer[y:y1, x:x1] = to_color(self.sampleBuffer[y:y1, x:x1])
+
+    def raytrace_pixel(self, x: int, y: int) -> np.ndarray:
+        self.raytrace_tile(x, y, 1, 1)
+        return self.sampleBuffer[y, x].copy()
+
+    def start_raytracing(self, stats: bool = False):
+        """Whole frame: every tile of the FIFO in one batched launch."""
+        if self.state != State.READY:
+            return
+        self.state = State.RENDERING
+        self.sampleBuffer[...] = 0
+        self.frameBuffer[...] = 0
+        h, w = self.sampleBuffer.shape[:2]
+        self.render_tiles(tile_fifo(w, h), stats=stats)
+        self.state = State.DONE
+
+    def stop(self):
+        if self.state in (State.RENDERING, State.DONE):
+            self.state = State.READY
+
+    def save_image(self, path: str):
+        """Writes frameBuffer flipped vertically (pathtracer.cpp:662-672) as PNG."""
+        from .image_io import write_png
+        write_png(path, self.frameBuffer[::-1])

@@ -1,0 +1,108 @@
+"""Deterministic benchmark scenes.
+
+CBdragon.dae (BASELINE configs C3/C4, 100,012 tris) and CBlucy.dae (C5) are
+listed in the reference's .MISSING_LARGE_BLOBS and absent here, so the
+benchmarks use the proxies SURVEY.md §8(d) specifies: dae/sky/CBbunny.dae with
+its bunny geometry ("Mesh-mesh", 28,576 tris) midpoint-subdivided 4:1 per level
+(sub1 = 114,304 + 12 box/light tris; sub2 = 457,216 + 12).
+
+Recipe: each triangle (a, b, c) -> (a, ab, ca), (ab, b, bc), (ca, bc, c),
+(ab, bc, ca); the edge midpoints are shared through an undirected edge map and
+appended after the original vertices in first-use order (ab, bc, ca per
+triangle).  The rewritten polylist keeps only the VERTEX input (normals are
+recomputed by the halfedge build anyway, src/halfEdgeMesh.h:492-515).
+Original vertices keep their exact text; new ones are written with %.7g.
+The output is an ordinary .dae that the reference and this package both load.
+"""
+from __future__ import annotations
+
+import os
+import re
+from typing import Optional
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ASSETS = os.path.join(ROOT, "assets")
+C1_DAE = os.path.join(ASSETS, "CBspheres_lambertian.dae")
+BUNNY_DAE = os.path.join(ASSETS, "CBbunny.dae")
+
+
+def _subdivide_once(pos_tokens, tris):
+    """pos_tokens: list of 3-tuples of text tokens; tris: (n,3) int array."""
+    pos = np.array([[np.float32(t) for t in p] for p in pos_tokens], dtype=np.float32)
+    edge = {}
+    new_pos = []
+    base = len(pos_tokens)
+
+    def mid(a, b):
+        key = (a, b) if a < b else (b, a)
+        idx = edge.get(key)
+        if idx is None:
+            idx = base + len(new_pos)
+            edge[key] = idx
+            m = (pos[a].astype(np.float64) + pos[b].astype(np.float64)) * 0.5
+            new_pos.append(tuple("%.7g" % v for v in m))
+        return idx
+
+    out = np.empty((len(tris) * 4, 3), np.int64)
+    for i, (a, b, c) in enumerate(tris.tolist()):
+        ab, bc, ca = mid(a, b), mid(b, c), mid(c, a)
+        out[4 * i + 0] = (a, ab, ca)
+        out[4 * i + 1] = (ab, b, bc)
+        out[4 * i + 2] = (ca, bc, c)
+        out[4 * i + 3] = (ab, bc, ca)
+    return pos_tokens + new_pos, out
+
+
+def make_subdivided(src: str, dst: str, levels: int = 1, geometry_id: str = "Mesh-mesh") -> str:
+    txt = open(src).read()
+    g0 = txt.index(f'<geometry id="{geometry_id}"')
+    g1 = txt.index("</geometry>", g0)
+    geo = txt[g0:g1]
+    m = re.search(r'(<float_array id="[^"]*positions-array" count=")(\d+)(">)([^<]*)(</float_array>)', geo)
+    toks = m.group(4).split()
+    pos_tokens = [tuple(toks[i:i + 3]) for i in range(0, len(toks), 3)]
+    pl = re.search(r"<polylist[^>]*>.*?</polylist>", geo, flags=re.S).group(0)
+    inputs = re.findall(r'<input semantic="(\w+)" source="([^"]*)" offset="(\d+)"', pl)
+    stride = max(int(o) for _, _, o in inputs) + 1
+    voff = [int(o) for s, _, o in inputs if s == "VERTEX"][0]
+    vsrc = [src_ for s, src_, _ in inputs if s == "VERTEX"][0]
+    vcount = np.array(re.search(r"<vcount>([^<]*)</vcount>", pl).group(1).split(), np.int64)
+    if not (vcount == 3).all():
+        raise ValueError("subdivision proxy expects a triangle polylist")
+    p = np.array(re.search(r"<p>([^<]*)</p>", pl).group(1).split(), np.int64)
+    tris = p.reshape(-1, stride)[:, voff].reshape(-1, 3)
+    for _ in range(levels):
+        pos_tokens, tris = _subdivide_once(pos_tokens, tris)
+    mat = re.search(r'material="([^"]*)"', pl).group(1)
+    new_pl = (f'<polylist material="{mat}" count="{len(tris)}">\n'
+              f'          <input semantic="VERTEX" source="{vsrc}" offset="0"/>\n'
+              f'          <vcount>{" ".join(["3"] * len(tris))} </vcount>\n'
+              f'          <p>{" ".join(map(str, tris.reshape(-1).tolist()))}</p>\n'
+              f'        </polylist>')
+    flat = " ".join(" ".join(t) for t in pos_tokens)
+    geo2 = geo[:m.start()] + m.group(1) + str(3 * len(pos_tokens)) + m.group(3) + flat + m.group(5) + geo[m.end():]
+    geo2 = re.sub(r"<polylist[^>]*>.*?</polylist>", lambda _: new_pl, geo2, count=1, flags=re.S)
+    out = txt[:g0] + geo2 + txt[g1:]
+    os.makedirs(os.path.dirname(os.path.abspath(dst)), exist_ok=True)
+    tmp = dst + ".tmp"
+    with open(tmp, "w") as f:
+        f.write(out)
+    os.replace(tmp, dst)
+    return dst
+
+
+def proxy_path(levels: int, cache_dir: Optional[str] = None) -> str:
+    """Path of CBbunny_sub<levels>.dae, generated on first use."""
+    cache_dir = cache_dir or os.path.join(ROOT, "_scenes")
+    dst = os.path.join(cache_dir, f"CBbunny_sub{levels}.dae")
+    if not os.path.exists(dst) or os.path.getmtime(dst) < os.path.getmtime(__file__):
+        make_subdivided(BUNNY_DAE, dst, levels)
+    return dst
+
+
+if __name__ == "__main__":
+    import sys
+    for lv in (int(a) for a in sys.argv[1:] or ["1"]):
+        print(proxy_path(lv))

@@ -1,0 +1,187 @@
+/* ptgpu.h — C ABI of the MI355X-native path-tracing hot path.
+ *
+ * This is the drop-in boundary for the reference's per-pixel radiance loop.
+ * Every entry point names the reference interface it replaces:
+ *
+ *   pt_create / pt_destroy      CUDAPathTracer::CUDAPathTracer / ~CUDAPathTracer
+ *                               (cuda_src/setup.h:90-148, setup.cu:92-115)
+ *   pt_upload_scene             CUDAPathTracer::init -> loadPrimitives/loadLights/
+ *                               loadBVH (setup.cu:181-201, 249-476, 689-774)
+ *   pt_set_camera               CUDAPathTracer::loadCamera (setup.cu:221-247);
+ *                               camera semantics of Camera::generate_ray
+ *                               (src/camera.cpp:113-129)
+ *   pt_set_params               CUDAPathTracer::loadParameters (setup.cu:777-811);
+ *                               PathTracer::ns_aa/max_ray_depth/ns_area_light
+ *                               (src/pathtracer.h:222-227)
+ *   pt_render_tiles             PathTracer::raytrace_tile(tile_x,tile_y,tile_w,tile_h)
+ *                               (src/pathtracer.h:181, src/pathtracer.cpp:585-611) for
+ *                               one tile; whole-frame batches replace
+ *                               CUDAPathTracer::startRayTracingPT + updateHostSampleBuffer
+ *                               + PathTracer::updateBufferFromGPU (setup.cu:147-179,813-843)
+ *   pt_render_tiles_device      same, output left in device memory on a caller stream
+ *                               (used for the multi-GPU framebuffer reduction)
+ *   pt_intersect                BVHAccel::intersect(ray, isect) and BVHAccel::intersect(ray)
+ *                               (src/bvh.cpp:331-362) as a batched query
+ *   pt_get_stats                timers/counters (pathtracer.cpp:615-632, setup.cu:546-685)
+ *   pt_last_error               replaces fprintf+exit(EXIT_FAILURE) (setup.cu:139-143, ...)
+ *
+ * Conventions: plain C types and host pointers only; the caller owns every host
+ * input and output; the library owns device memory until pt_destroy.  Calls on
+ * one pt_ctx are serialised by the caller; different contexts (one per GPU) may
+ * be driven from different host threads or processes.  Every function returns
+ * PT_OK (0) or a negative PT_E_* code and never exits the process.
+ * Image layout: float32 RGB, row-major, index (x + y*W)*3, y = 0 is the BOTTOM
+ * row (HDRImageBuffer::update_pixel, src/image.h:113-117).
+ */
+#ifndef PTGPU_H
+#define PTGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_OK 0
+#define PT_E_INVALID (-1)  /* bad argument / unsupported scene content */
+#define PT_E_HIP (-2)      /* HIP runtime error (message in pt_last_error) */
+#define PT_E_NOSCENE (-3)  /* render/intersect before pt_upload_scene/pt_set_camera */
+#define PT_E_ALLOC (-4)    /* device or host allocation failed */
+#define PT_E_IO (-5)       /* file could not be read/written */
+
+/* Primitive types follow Primitive::getType(): Sphere 0, Triangle 1. */
+#define PT_PRIM_SPHERE 0
+#define PT_PRIM_TRIANGLE 1
+/* BSDF types follow BSDF::getType(): Diffuse 0, Mirror 1, Refraction 2, Glass 3, Emission 4. */
+#define PT_BSDF_DIFFUSE 0
+#define PT_BSDF_MIRROR 1
+#define PT_BSDF_REFRACTION 2
+#define PT_BSDF_GLASS 3
+#define PT_BSDF_EMISSION 4
+/* Light types follow SceneLight::getType(): Directional 0, Hemisphere 1, Point 2, Area 3. */
+#define PT_LIGHT_DIRECTIONAL 0
+#define PT_LIGHT_HEMISPHERE 1
+#define PT_LIGHT_POINT 2
+#define PT_LIGHT_AREA 3
+
+typedef struct pt_ctx pt_ctx;
+
+/* One BSDF (src/bsdf.h).  albedo holds Diffuse::albedo, Mirror::reflectance and
+ * Glass::reflectance; transmittance holds Refraction/Glass::transmittance;
+ * emission holds EmissionBSDF::radiance. */
+typedef struct pt_bsdf {
+  int32_t type;
+  float albedo[3];
+  float transmittance[3];
+  float emission[3];
+  float ior;
+  float roughness;
+} pt_bsdf;
+
+/* One light (src/static_scene/light.h).  Directional: direction = dirToLight.
+ * Point: position.  Area: position, direction, dim_x, dim_y, area. */
+typedef struct pt_light {
+  int32_t type;
+  float radiance[3];
+  double position[3];
+  double direction[3];
+  double dim_x[3];
+  double dim_y[3];
+  float area;
+} pt_light;
+
+/* Camera (src/camera.h): pos, c2w(i,j) row-major, screenW/H/screenDist. */
+typedef struct pt_camera {
+  double pos[3];
+  double c2w[9];
+  double screen_w;
+  double screen_h;
+  double screen_dist;
+} pt_camera;
+
+/* One node of the reference BVH (src/bvh.h BVHNode), flattened: children by
+ * index (-1 = NULL), primitives [start, start+range) of the BVH-ordered list. */
+typedef struct pt_bvh_node {
+  double bb_min[3];
+  double bb_max[3];
+  int64_t start;
+  int64_t range;
+  int64_t left;
+  int64_t right;
+} pt_bvh_node;
+
+/* Flattened scene exactly as BVHAccel holds it: primitives in BVH order.
+ * prim_geom: triangle p1,p2,p3 (9 doubles); sphere o.xyz, r (rest 0).
+ * prim_norm: triangle vertex normals n1,n2,n3 (9 doubles); sphere ignored.
+ * nodes[0] is the root. */
+typedef struct pt_scene {
+  int64_t n_prims;
+  const int32_t* prim_type;
+  const int32_t* prim_bsdf;
+  const double* prim_geom;
+  const double* prim_norm;
+  int64_t n_nodes;
+  const pt_bvh_node* nodes;
+  int32_t n_bsdfs;
+  const pt_bsdf* bsdfs;
+  int32_t n_lights;
+  const pt_light* lights;
+} pt_scene;
+
+/* Integrator settings (PathTracer members) and frame size. */
+typedef struct pt_params {
+  int32_t width;
+  int32_t height;
+  int32_t spp;           /* ns_aa */
+  int32_t max_depth;     /* max_ray_depth */
+  int32_t ns_area_light; /* ns_area_light */
+  uint32_t seed;         /* counter-RNG key: (seed, pixel, sample) */
+} pt_params;
+
+typedef struct pt_tile {
+  int32_t x, y, w, h;
+} pt_tile;
+
+typedef struct pt_stats {
+  int64_t pixels;       /* pixels rendered by the last call */
+  int64_t samples;      /* pixels * spp */
+  int64_t camera_rays;
+  int64_t bounce_rays;
+  int64_t shadow_rays;
+  int64_t node_visits;  /* BVH2 internal-node fetches (64 B each in the reference layout) */
+  int64_t tri_tests;
+  int64_t sphere_tests;
+  int64_t ext_hits;     /* nearest-hit rays that hit (shading-normal fetch) */
+  double last_ms;       /* device time of the last render kernel (hipEvent) */
+  int32_t counters_valid; /* 1 if the last call ran with PT_FLAG_STATS */
+} pt_stats;
+
+#define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */
+
+int pt_create(int device, pt_ctx** out);
+int pt_destroy(pt_ctx* ctx);
+int pt_upload_scene(pt_ctx* ctx, const pt_scene* scene);
+int pt_set_camera(pt_ctx* ctx, const pt_camera* cam);
+int pt_set_params(pt_ctx* ctx, const pt_params* params);
+/* Renders the listed tiles into a host framebuffer of width*height*3 floats;
+ * only pixels inside the tiles are written.  flags: PT_FLAG_* */
+int pt_render_tiles(pt_ctx* ctx, const pt_tile* tiles, int32_t n_tiles, float* hdr_out_host,
+                    uint32_t flags);
+/* Same, into a device framebuffer (width*height*3 floats) on `stream`
+ * (hipStream_t, NULL = the context's stream).  Returns after the kernel is
+ * queued; synchronise on the stream before reading. */
+int pt_render_tiles_device(pt_ctx* ctx, const pt_tile* tiles, int32_t n_tiles, float* hdr_out_dev,
+                           void* stream, uint32_t flags);
+/* Batched BVHAccel::intersect.  Rays: origin o[3n], direction d[3n] (normalised),
+ * max_t[n] for the any-hit query.  Outputs (each nullable): nearest hit flag,
+ * t, primitive index (BVH order), and the any-hit flag within (0, max_t). */
+int pt_intersect(pt_ctx* ctx, int64_t n, const double* o, const double* d, const double* max_t,
+                 int32_t* hit, float* t, int32_t* prim, int32_t* any_hit);
+int pt_get_stats(pt_ctx* ctx, pt_stats* out);
+const char* pt_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PTGPU_H */

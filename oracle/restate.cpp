@@ -239,10 +239,28 @@ static bool sphere_test(const Prim& P, const Ray& r, double& t1, double& t2) {
   return true;
 }
 
+static bool sphere_test_alias(const Prim& P, const Ray& r, double& t) {
+  V3 m = P.o - r.o;
+  double b = dot(m, r.d);
+  double c = dot(m, m) - P.r2;
+  double delta = b * b - c;
+  if (delta < 0) return false;
+  t = b - std::sqrt(delta);
+  t = b + std::sqrt(delta);
+  if (t >= r.max_t || t <= r.min_t) return false;
+  return true;
+}
+
 static bool sphere_hit(const Prim& P, const Ray& r, Isect* is, Stats& st) {
   st.spheres++;
   double t1, t2;
-  if (!is) return sphere_test(P, r, t1, t2);
+  // Sphere::intersect(r) (sphere.cpp:37-45) calls test(r, tmp, tmp): both
+  // out-references alias one double, so the range check sees the far root twice.
+  if (!is) {
+    double tmp;
+    if (!sphere_test_alias(P, r, tmp)) return false;
+    return true;
+  }
   if (!sphere_test(P, r, t1, t2)) return false;
   double t = t1;
   if (t1 <= r.min_t) t = t2;

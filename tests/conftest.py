@@ -1,0 +1,25 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libptgpu.so on cuda:0)")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session")
+def restate():
+    from tests import oracle_helpers
+    return oracle_helpers.Restatement()
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx():
+    from dsgpuraytracing_amd import pathtracer
+    return pathtracer.Device(0)

@@ -1,0 +1,88 @@
+"""Regenerates the committed golden fixtures from the REFERENCE itself.
+
+Runs oracle/_ref/ref_driver (the reference's own CPU path tracer sources,
+compiled by oracle/ref/Makefile in the build container; /root/reference is not
+available on the GPU box) and stores inputs + outputs as small PTDUMP files:
+
+  c1_<cam>_<W>x<H>.scene.ptd   flattened scene the GPU seam receives (prims in
+                               BVH order, BVH nodes, BSDFs, lights, camera)
+  c1_<cam>_<W>x<H>_s<spp>_m<depth>_l<ns>_seed<k>.hdr.ptd
+                               reference HDR sampleBuffer (float32, y=0 bottom),
+                               srand(seed) immediately before start_raytracing, -t 1
+  c1_rays.ptd / c1_rays_ref.ptd  ray-query KAT inputs / BVHAccel::intersect answers
+
+Usage: python tests/golden/make_golden.py   (needs oracle/_ref/ref_driver)
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+from dsgpuraytracing_amd import ptdump  # noqa: E402
+
+REF = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+C1 = os.path.join(ROOT, "assets", "CBspheres_lambertian.dae")
+CAMS = {"default": None, "sphcam": os.path.join(ROOT, "assets", "cam_sphere.info")}
+
+SCENES = [("default", 64, 64), ("sphcam", 96, 64), ("default", 128, 128), ("default", 256, 256)]
+RENDERS = [
+    # (cam, W, H, spp, depth, ns_area_light, seed)
+    ("default", 64, 64, 4, 4, 1, 1),      # exact-parity case (SURVEY §8(c) criterion 1)
+    ("sphcam", 96, 64, 3, 4, 2, 7),       # non-square, framed camera, 2 area samples
+    ("default", 256, 256, 1, 4, 1, 1),    # BASELINE config C1 (256x256, 1 spp)
+    ("default", 128, 128, 64, 4, 1, 1),   # statistical parity pair (noise floor)
+    ("default", 128, 128, 64, 4, 1, 2),
+]
+
+
+def scene_name(cam, w, h):
+    return f"c1_{cam}_{w}x{h}.scene.ptd"
+
+
+def hdr_name(cam, w, h, spp, m, l, seed):
+    return f"c1_{cam}_{w}x{h}_s{spp}_m{m}_l{l}_seed{seed}.hdr.ptd"
+
+
+def run(args):
+    subprocess.run([REF] + args, check=True, stdout=subprocess.DEVNULL)
+
+
+def main():
+    if not os.path.exists(REF):
+        sys.exit("oracle/_ref/ref_driver missing: run `make -C oracle/ref` in the build container")
+    for cam, w, h in SCENES:
+        args = [C1, "-w", str(w), "-h", str(h), "--mode", "dump", "--out", os.path.join(HERE, scene_name(cam, w, h))]
+        if CAMS[cam]:
+            args += ["--cam", CAMS[cam]]
+        run(args)
+    for cam, w, h, spp, m, l, seed in RENDERS:
+        out = os.path.join(HERE, hdr_name(cam, w, h, spp, m, l, seed))
+        args = [C1, "-w", str(w), "-h", str(h), "-s", str(spp), "-m", str(m), "-l", str(l), "--seed", str(seed),
+                "--out", out]
+        if CAMS[cam]:
+            args += ["--cam", CAMS[cam]]
+        run(args)
+        d = ptdump.read(out)
+        ptdump.write(out, {"hdr": d["hdr"], "shape": d["shape"]})  # drop the wall time: deterministic file
+    # Ray-query KATs on C1: rays from around the box towards random points inside it.
+    rng = np.random.default_rng(462)
+    n = 2048
+    o = rng.uniform(-1.2, 1.2, (n, 3)) + np.array([0.0, 0.75, 0.0])
+    tgt = rng.uniform(-1.0, 1.0, (n, 3)) * np.array([1.0, 0.75, 1.0]) + np.array([0.0, 0.75, 0.0])
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    maxt = rng.uniform(0.05, 3.0, n)
+    rays = os.path.join(HERE, "c1_rays.ptd")
+    ptdump.write(rays, {"ray_o": o.reshape(-1), "ray_d": d.reshape(-1), "ray_maxt": maxt})
+    run([C1, "-w", "64", "-h", "64", "--mode", "rays", "--rays", rays, "--out", os.path.join(HERE, "c1_rays_ref.ptd")])
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

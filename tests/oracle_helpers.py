@@ -1,0 +1,75 @@
+"""Test-side access to the oracle (oracle/restate.cpp, oracle/_ref).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this
+module; the product (dsgpuraytracing_amd) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE = os.path.join(ROOT, "oracle")
+RESTATE_SO = os.path.join(ORACLE, "_build", "librestate.so")
+REF_DRIVER = os.path.join(ORACLE, "_ref", "ref_driver")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def build_restatement() -> str:
+    src = os.path.join(ORACLE, "restate.cpp")
+    if not os.path.exists(RESTATE_SO) or os.path.getmtime(RESTATE_SO) < os.path.getmtime(src):
+        subprocess.run(["make", "-C", ORACLE, "-s"], check=True)
+    return RESTATE_SO
+
+
+class Restatement:
+    def __init__(self):
+        self.lib = ctypes.CDLL(build_restatement())
+        self.lib.rs_render.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 5 + [ctypes.c_uint32] + \
+            [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_void_p]
+        self.lib.rs_render.restype = ctypes.c_int
+        self.lib.rs_intersect.argtypes = [ctypes.c_char_p, ctypes.c_int64] + [ctypes.c_void_p] * 8
+        self.lib.rs_intersect.restype = ctypes.c_int
+        self.lib.rs_rng_draw.argtypes = [ctypes.c_uint32] * 4
+        self.lib.rs_rng_draw.restype = ctypes.c_double
+
+    def render(self, scene_path, w, h, spp, depth=4, ns_area_light=1, seed=1, rng_mode=0, threads=1,
+               tile_begin=0, tile_end=-1):
+        out = np.zeros((h, w, 3), np.float32)
+        st = np.zeros(5, np.int64)
+        rc = self.lib.rs_render(scene_path.encode(), w, h, spp, depth, ns_area_light, seed, rng_mode, threads,
+                                tile_begin, tile_end, out.ctypes.data, st.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"rs_render failed on {scene_path}")
+        return out, st
+
+    def intersect(self, scene_path, o, d, maxt):
+        n = len(maxt)
+        o = np.ascontiguousarray(o, np.float64)
+        d = np.ascontiguousarray(d, np.float64)
+        maxt = np.ascontiguousarray(maxt, np.float64)
+        hit = np.zeros(n, np.int32)
+        t = np.zeros(n, np.float64)
+        prim = np.zeros(n, np.int32)
+        nrm = np.zeros(3 * n, np.float64)
+        anyh = np.zeros(n, np.int32)
+        rc = self.lib.rs_intersect(scene_path.encode(), n, o.ctypes.data, d.ctypes.data, maxt.ctypes.data,
+                                   hit.ctypes.data, t.ctypes.data, prim.ctypes.data, nrm.ctypes.data,
+                                   anyh.ctypes.data)
+        if rc != 0:
+            raise RuntimeError("rs_intersect failed")
+        return hit, t, prim, nrm.reshape(-1, 3), anyh
+
+    def rng_draw(self, seed, pixel, sample, k):
+        return self.lib.rs_rng_draw(seed, pixel, sample, k)
+
+
+def golden(name: str) -> str:
+    return os.path.join(GOLDEN, name)
+
+
+def have_ref() -> bool:
+    return os.path.exists(REF_DRIVER) and os.path.isdir("/root/reference")
