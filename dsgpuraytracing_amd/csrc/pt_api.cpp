@@ -18,15 +18,20 @@
 
 #include "../../include/ptgpu.h"
 #include "pt_device.h"
+#include "pt_error.h"
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-int fail(int code, const std::string& msg) {
+int pt_fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+
+namespace {
+
+int fail(int code, const std::string& msg) { return pt_fail(code, msg); }
 
 #define HIPCHK(expr)                                                                            \
   do {                                                                                          \

@@ -96,6 +96,11 @@ _SIGS = {
                                c_void_p, c_void_p]),
     "pt_get_stats": (c_int32, [c_void_p, POINTER(pt_stats)]),
     "pt_last_error": (c_char_p, []),
+    # include/ptgpu_scene.h (bound with full types in scene_loader.py)
+    "pt_host_scene_load": (c_int32, [c_char_p, c_int32, c_int32, c_char_p, POINTER(c_void_p)]),
+    "pt_host_scene_view": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "pt_host_scene_dump": (c_int32, [c_void_p, c_char_p]),
+    "pt_host_scene_free": (None, [c_void_p]),
 }
 
 _lib = None

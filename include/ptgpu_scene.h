@@ -1,0 +1,53 @@
+/* ptgpu_scene.h — native host scene pipeline of the HIP path (C ABI).
+ *
+ * For callers that do not own a CMU462 PathTracer: restates the reference's
+ * host side that produces the flattened scene pt_upload_scene consumes.
+ *
+ *   pt_host_scene_load   Collada::ColladaParser::load (src/collada/collada.cpp:131-936)
+ *                        + Application::load / init_* (src/application.cpp:223-365)
+ *                        + DynamicScene -> StaticScene (src/dynamic_scene/{mesh,sphere,scene}.cpp,
+ *                          src/static_scene/object.cpp:16-80)
+ *                        + HalfedgeMesh::build / Vertex::computeNormal
+ *                          (src/halfEdgeMesh.cpp:29-397, src/halfEdgeMesh.h:492-515)
+ *                        + PathTracer::build_accel / BVHAccel::BVHAccel / buildBVH
+ *                          (src/pathtracer.cpp:224-248, src/bvh.cpp:21-202; with the
+ *                          bucket-index clamp of SURVEY.md §8(a) quirk 1)
+ *                        + Application::loadCamera for .info files
+ *                          (src/application.cpp:823-853)
+ *   pt_host_scene_view   borrowed pt_scene / pt_camera views of the result
+ *   pt_host_scene_dump   PTDUMP file (the oracle's scene interchange format)
+ *   pt_host_scene_free   release
+ *
+ * The result is bit-identical to what the reference's own host code builds
+ * (primitive order, vertex order, area-weighted normals, BVH topology and
+ * boxes, lights, BSDFs, camera); tests/test_scene_loader.py pins it against
+ * dumps written by the reference (oracle/_ref/ref_driver --mode dump).
+ */
+#ifndef PTGPU_SCENE_H
+#define PTGPU_SCENE_H
+
+#include <stdint.h>
+
+#include "ptgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pt_host_scene pt_host_scene;
+
+/* Loads a COLLADA .dae, builds the reference BVH and places the default camera
+ * for a width x height frame.  cam_info (nullable) is a .info camera file. */
+int pt_host_scene_load(const char* dae_path, int32_t width, int32_t height, const char* cam_info,
+                       pt_host_scene** out);
+/* Borrowed views, valid until pt_host_scene_free. Either pointer may be NULL. */
+int pt_host_scene_view(const pt_host_scene* hs, pt_scene* scene, pt_camera* cam);
+/* Writes the flattened scene as a PTDUMP file. */
+int pt_host_scene_dump(const pt_host_scene* hs, const char* path);
+void pt_host_scene_free(pt_host_scene* hs);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PTGPU_SCENE_H */

@@ -15,6 +15,8 @@ Usage: python tests/golden/make_golden.py   (needs oracle/_ref/ref_driver)
 """
 from __future__ import annotations
 
+import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -81,7 +83,24 @@ def main():
     rays = os.path.join(HERE, "c1_rays.ptd")
     ptdump.write(rays, {"ray_o": o.reshape(-1), "ray_d": d.reshape(-1), "ray_maxt": maxt})
     run([C1, "-w", "64", "-h", "64", "--mode", "rays", "--rays", rays, "--out", os.path.join(HERE, "c1_rays_ref.ptd")])
+    # Scene checksums of larger scenes (too big to commit as dumps): the
+    # reference's own flattened scene, hashed array by array.
+    sys.path.insert(0, ROOT)
+    from dsgpuraytracing_amd import scenes
+    hashes = {}
+    for dae, w, h in [(os.path.join(ROOT, "assets", "CBbunny.dae"), 1024, 1024), (scenes.proxy_path(1), 1024, 1024),
+                      (scenes.proxy_path(1), 1920, 1080)]:
+        tmp = os.path.join(HERE, "_tmp_scene.ptd")
+        run([dae, "-w", str(w), "-h", str(h), "--mode", "dump", "--out", tmp])
+        hashes[f"{os.path.basename(dae)}@{w}x{h}"] = scene_hashes(ptdump.read(tmp))
+        os.remove(tmp)
+    with open(os.path.join(HERE, "scene_hashes.json"), "w") as f:
+        json.dump(hashes, f, indent=1, sort_keys=True)
     print("golden fixtures written to", HERE)
+
+
+def scene_hashes(d):
+    return {k: {"n": int(v.size), "sha256": hashlib.sha256(v.tobytes()).hexdigest()} for k, v in sorted(d.items())}
 
 
 if __name__ == "__main__":
