@@ -170,6 +170,7 @@ def main():
                          "algorithmic_bytes_per_launch": bytes_launch},
             "counters": {k: st_counts[k] for k in ("camera_rays", "bounce_rays", "shadow_rays", "node_visits",
                                                    "tri_tests", "sphere_tests", "ext_hits")},
+            "launch": {"grid_blocks": s["grid_blocks"], "block": 64, "blocks_per_cu_query": s["blocks_per_cu"]},
             "image_mean": float(img.mean()),
         }
         rays = st_counts["camera_rays"] + st_counts["bounce_rays"] + st_counts["shadow_rays"]

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -94,6 +95,7 @@ struct pt_ctx {
   pt_params params{};
   pt_stats last{};
   int grid_plain = 0, grid_stats = 0;
+  int bpc_plain = 0, bpc_stats = 0, n_cu = 0;
 };
 
 extern "C" {
@@ -116,11 +118,14 @@ int pt_create(int device, pt_ctx** out) {
   HIPCHK(c->stats.reserve(8));
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, device));
-  int bpc = 0;
-  HIPCHK(ptk_render_occupancy(&bpc, false));
-  c->grid_plain = std::max(1, bpc) * prop.multiProcessorCount;
-  HIPCHK(ptk_render_occupancy(&bpc, true));
-  c->grid_stats = std::max(1, bpc) * prop.multiProcessorCount;
+  // Persistent grid: as many one-wave workgroups as can be resident.  The
+  // work queue needs no co-residency (no grid barrier), so a wrong occupancy
+  // answer only costs speed; never size below 8 waves per CU.
+  c->n_cu = prop.multiProcessorCount;
+  HIPCHK(ptk_render_occupancy(&c->bpc_plain, false));
+  HIPCHK(ptk_render_occupancy(&c->bpc_stats, true));
+  c->grid_plain = std::max(8, c->bpc_plain) * c->n_cu;
+  c->grid_stats = std::max(8, c->bpc_stats) * c->n_cu;
   *out = c;
   return PT_OK;
 }
@@ -369,12 +374,29 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.out = out_dev;
   P.work_counter = c->counter.p;
   P.stats = c->stats.p;
+  P.dbg_pix = -1;
+  P.shade_batch = 32;
+  if (const char* sb = std::getenv("PT_SHADE_BATCH")) {  // tuning knob
+    int v = std::atoi(sb);
+    if (v >= 1 && v <= 64) P.shade_batch = v;
+  }
+  if (const char* dp = std::getenv("PT_DEBUG_PIXEL")) {  // diagnostics only
+    int dx = -1, dy = -1;
+    if (std::sscanf(dp, "%d,%d", &dx, &dy) == 2 && dx >= 0 && dy >= 0 && dx < P.W && dy < P.H) P.dbg_pix = dx + dy * P.W;
+  }
   int64_t slots = (int64_t)tl.size() * 1024;
   int64_t max_grid = (slots + PT_BLOCK - 1) / PT_BLOCK;
-  int grid = (int)std::min<int64_t>(stats ? c->grid_stats : c->grid_plain, max_grid);
+  int64_t want = stats ? c->grid_stats : c->grid_plain;
+  if (const char* g = std::getenv("PT_WAVES_PER_CU")) {  // tuning knob
+    int w = std::atoi(g);
+    if (w > 0) want = (int64_t)w * c->n_cu;
+  }
+  int grid = (int)std::min<int64_t>(want, max_grid);
   HIPCHK(hipEventRecord(c->ev0, s));
   HIPCHK(ptk_launch_render(&P, grid, stats, s));
   HIPCHK(hipEventRecord(c->ev1, s));
+  c->last.grid_blocks = grid;
+  c->last.blocks_per_cu = stats ? c->bpc_stats : c->bpc_plain;
   int64_t px = 0;
   for (const int4& t : tl) px += (int64_t)t.z * t.w;
   c->last.pixels = px;

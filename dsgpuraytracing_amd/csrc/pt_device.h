@@ -8,7 +8,7 @@
 #define PT_BLOCK 64  // one wave64 per workgroup: the persistent queue is per wave
 #endif
 #ifndef PT_STACK
-#define PT_STACK 64  // traversal stack entries per lane (LDS, lane-contiguous)
+#define PT_STACK 32  // traversal stack entries per lane (LDS, lane-contiguous)
 #endif
 
 // BVH2 node, 64 B: both child boxes + child references.
@@ -65,6 +65,8 @@ struct KParams {
   float* out;         // W*H*3
   uint32_t* work_counter;
   unsigned long long* stats;  // 7 counters (PT_FLAG_STATS)
+  int dbg_pix;                // diagnostic printf trace of one pixel (-1: off)
+  int shade_batch;            // leave the traversal phase once this many lanes finished their ray
 };
 
 extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, hipStream_t s);

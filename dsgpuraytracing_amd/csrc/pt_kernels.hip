@@ -95,125 +95,149 @@ struct Counters {
   uint32_t nodes, tris, spheres;
 };
 
-// Stack-based BVH2 traversal.  ANY=true: occlusion query, exits on the first
-// hit in (0, tmax) (BVHAccel::intersect(ray), bvh.cpp:282-341).  Otherwise
-// nearest hit (bvh.cpp:227-279, 343-362): same closest hit, visit order by
-// child entry distance, boxes clipped to the current [0, tmax].
+// Resumable stack-based BVH2 traversal state of one lane.
+struct Trav {
+  float3 o, d, inv;
+  float tmax;
+  int node, sp;
+  bool any, found;
+  Hit hit;
+};
+
+__device__ __forceinline__ void trav_init(Trav& tr, float3 o, float3 d, float tmax, bool any) {
+  const float kTiny = 1e-20f;
+  float3 dd = f3(fabsf(d.x) < kTiny ? copysignf(kTiny, d.x) : d.x, fabsf(d.y) < kTiny ? copysignf(kTiny, d.y) : d.y,
+                 fabsf(d.z) < kTiny ? copysignf(kTiny, d.z) : d.z);
+  tr.o = o;
+  tr.d = d;
+  tr.inv = f3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
+  tr.tmax = tmax;
+  tr.node = 0;
+  tr.sp = 0;
+  tr.any = any;
+  tr.found = false;
+  tr.hit.t = 0.0f;
+  tr.hit.u = tr.hit.v = 0.0f;
+  tr.hit.prim = -1;
+}
+
+// One traversal step: fetch one node (both child boxes), intersect the
+// primitives of leaf children in place, then descend / push / pop.  Returns
+// true when the query is complete.  Semantics: nearest hit (bvh.cpp:227-279,
+// 343-362: the same closest hit, children visited near-first, boxes clipped to
+// the current [0, tmax]) or, with tr.any, occlusion within (0, tmax)
+// (bvh.cpp:282-341), leaving on the first hit.
+template <bool STATS>
+__device__ __forceinline__ bool trav_step(const DNode* __restrict__ nodes, const DPrim* __restrict__ prims,
+                                          int* __restrict__ stk, int stride, Trav& tr, Counters& ct) {
+  const float kRobust = 1.0000005f;
+  const float4 a = nodes[tr.node].a;
+  const float4 b = nodes[tr.node].b;
+  const float4 c = nodes[tr.node].c;
+  const int4 e = nodes[tr.node].e;
+  if (STATS) ct.nodes++;
+  const float3 o = tr.o, d = tr.d, inv = tr.inv;
+  const float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+  float l0x = fmaf(a.x, inv.x, -oi.x), h0x = fmaf(a.y, inv.x, -oi.x);
+  float l0y = fmaf(a.z, inv.y, -oi.y), h0y = fmaf(a.w, inv.y, -oi.y);
+  float l0z = fmaf(c.x, inv.z, -oi.z), h0z = fmaf(c.y, inv.z, -oi.z);
+  float l1x = fmaf(b.x, inv.x, -oi.x), h1x = fmaf(b.y, inv.x, -oi.x);
+  float l1y = fmaf(b.z, inv.y, -oi.y), h1y = fmaf(b.w, inv.y, -oi.y);
+  float l1z = fmaf(c.z, inv.z, -oi.z), h1z = fmaf(c.w, inv.z, -oi.z);
+  float tn0 = fmaxf(fmaxf(fminf(l0x, h0x), fminf(l0y, h0y)), fmaxf(fminf(l0z, h0z), 0.0f));
+  float tf0 = fminf(fminf(fmaxf(l0x, h0x), fmaxf(l0y, h0y)), fminf(fmaxf(l0z, h0z), tr.tmax)) * kRobust;
+  float tn1 = fmaxf(fmaxf(fminf(l1x, h1x), fminf(l1y, h1y)), fmaxf(fminf(l1z, h1z), 0.0f));
+  float tf1 = fminf(fminf(fmaxf(l1x, h1x), fmaxf(l1y, h1y)), fminf(fmaxf(l1z, h1z), tr.tmax)) * kRobust;
+  bool hit0 = tn0 <= tf0;
+  bool hit1 = tn1 <= tf1;
+  // Leaf children: intersect their primitives now.
+  for (int side = 0; side < 2; ++side) {
+    bool h = side == 0 ? hit0 : hit1;
+    int cnt = side == 0 ? e.z : e.w;
+    if (!(h && cnt > 0)) continue;
+    int start = side == 0 ? e.x : e.y;
+    for (int k = 0; k < cnt; ++k) {
+      const int pi = start + k;
+      const float4 v0 = prims[pi].v0;
+      const float4 e1 = prims[pi].e1;
+      const int meta = __float_as_int(v0.w);
+      float t, u = 0.0f, v = 0.0f;
+      if (meta & 1) {  // triangle: Moller-Trumbore; u,v >= 0, u+v <= 1, 0 < t < tmax
+        if (STATS) ct.tris++;
+        const float4 e2 = prims[pi].e2;
+        float3 E1 = f3(e1.x, e1.y, e1.z), E2 = f3(e2.x, e2.y, e2.z);
+        float3 pv = cross(d, E2);
+        float det = dot(E1, pv);
+        if (det == 0.0f) continue;
+        float id = 1.0f / det;
+        float3 tv = o - f3(v0.x, v0.y, v0.z);
+        u = dot(tv, pv) * id;
+        float3 qv = cross(tv, E1);
+        v = dot(d, qv) * id;
+        t = dot(E2, qv) * id;
+        if (!(u >= 0.0f && v >= 0.0f && u + v <= 1.0f)) continue;
+      } else {  // sphere, cancellation-free roots (Haines et al., Ray Tracing Gems ch.7)
+        if (STATS) ct.spheres++;
+        float3 fo = o - f3(v0.x, v0.y, v0.z);
+        float bq = dot(fo, d);
+        float3 lp = fo - d * bq;
+        float disc = e1.y - dot(lp, lp);
+        if (disc < 0.0f) continue;
+        float q = -bq - copysignf(sqrtf(disc), bq);
+        if (q == 0.0f) continue;
+        float ta = (dot(fo, fo) - e1.y) / q, tb = q;
+        float t1 = fminf(ta, tb), t2 = fmaxf(ta, tb);
+        // nearest: nearer root unless behind the origin (sphere.cpp:47-77);
+        // occlusion: the far root, as Sphere::intersect(r)'s aliased test (sphere.cpp:37-45)
+        t = (t1 > 0.0f && !tr.any) ? t1 : t2;
+      }
+      if (t > 0.0f && t < tr.tmax) {
+        tr.tmax = t;
+        tr.hit.t = t;
+        tr.hit.u = u;
+        tr.hit.v = v;
+        tr.hit.prim = pi;
+        tr.found = true;
+        if (tr.any) return true;
+      }
+    }
+  }
+  bool in0 = hit0 && e.z == 0 && tn0 <= tr.tmax;
+  bool in1 = hit1 && e.w == 0 && tn1 <= tr.tmax;
+  if (in0 && in1) {
+    bool first0 = tn0 <= tn1;
+    stk[tr.sp * stride] = first0 ? e.y : e.x;
+    ++tr.sp;
+    tr.node = first0 ? e.x : e.y;
+  } else if (in0) {
+    tr.node = e.x;
+  } else if (in1) {
+    tr.node = e.y;
+  } else {
+    if (tr.sp == 0) return true;
+    --tr.sp;
+    tr.node = stk[tr.sp * stride];
+  }
+  return false;
+}
+
 template <bool STATS>
 __device__ __forceinline__ bool traverse(const DNode* __restrict__ nodes, const DPrim* __restrict__ prims,
                                          int* __restrict__ stk, int stride, float3 o, float3 d, float tmax,
                                          bool any, Hit& hit, Counters& ct) {
-  const float kTiny = 1e-20f;
-  float3 dd = f3(fabsf(d.x) < kTiny ? copysignf(kTiny, d.x) : d.x, fabsf(d.y) < kTiny ? copysignf(kTiny, d.y) : d.y,
-                 fabsf(d.z) < kTiny ? copysignf(kTiny, d.z) : d.z);
-  float3 inv = f3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
-  float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
-  const float kRobust = 1.0000005f;
-  int node = 0, sp = 0;
-  bool found = false;
-  hit.prim = -1;
-  for (;;) {
-    const float4 a = nodes[node].a;
-    const float4 b = nodes[node].b;
-    const float4 c = nodes[node].c;
-    const int4 e = nodes[node].e;
-    if (STATS) ct.nodes++;
-    // child 0: a = (lo.x, hi.x, lo.y, hi.y), c.xy = (lo.z, hi.z)
-    float l0x = fmaf(a.x, inv.x, -oi.x), h0x = fmaf(a.y, inv.x, -oi.x);
-    float l0y = fmaf(a.z, inv.y, -oi.y), h0y = fmaf(a.w, inv.y, -oi.y);
-    float l0z = fmaf(c.x, inv.z, -oi.z), h0z = fmaf(c.y, inv.z, -oi.z);
-    float l1x = fmaf(b.x, inv.x, -oi.x), h1x = fmaf(b.y, inv.x, -oi.x);
-    float l1y = fmaf(b.z, inv.y, -oi.y), h1y = fmaf(b.w, inv.y, -oi.y);
-    float l1z = fmaf(c.z, inv.z, -oi.z), h1z = fmaf(c.w, inv.z, -oi.z);
-    float tn0 = fmaxf(fmaxf(fminf(l0x, h0x), fminf(l0y, h0y)), fmaxf(fminf(l0z, h0z), 0.0f));
-    float tf0 = fminf(fminf(fmaxf(l0x, h0x), fmaxf(l0y, h0y)), fminf(fmaxf(l0z, h0z), tmax)) * kRobust;
-    float tn1 = fmaxf(fmaxf(fminf(l1x, h1x), fminf(l1y, h1y)), fmaxf(fminf(l1z, h1z), 0.0f));
-    float tf1 = fminf(fminf(fmaxf(l1x, h1x), fmaxf(l1y, h1y)), fminf(fmaxf(l1z, h1z), tmax)) * kRobust;
-    bool hit0 = tn0 <= tf0;
-    bool hit1 = tn1 <= tf1;
-    // Leaf children are intersected in place.
-    for (int side = 0; side < 2; ++side) {
-      bool h = side == 0 ? hit0 : hit1;
-      int cnt = side == 0 ? e.z : e.w;
-      if (!(h && cnt > 0)) continue;
-      int start = side == 0 ? e.x : e.y;
-      for (int k = 0; k < cnt; ++k) {
-        const int pi = start + k;
-        const float4 v0 = prims[pi].v0;
-        const float4 e1 = prims[pi].e1;
-        const int meta = __float_as_int(v0.w);
-        if (meta & 1) {  // triangle: Moller-Trumbore; accept u,v >= 0, u+v <= 1, 0 < t < tmax
-          if (STATS) ct.tris++;
-          const float4 e2 = prims[pi].e2;
-          float3 E1 = f3(e1.x, e1.y, e1.z), E2 = f3(e2.x, e2.y, e2.z);
-          float3 pv = cross(d, E2);
-          float det = dot(E1, pv);
-          if (det == 0.0f) continue;
-          float id = 1.0f / det;
-          float3 tv = o - f3(v0.x, v0.y, v0.z);
-          float u = dot(tv, pv) * id;
-          float3 qv = cross(tv, E1);
-          float v = dot(d, qv) * id;
-          float t = dot(E2, qv) * id;
-          if (u >= 0.0f && v >= 0.0f && u + v <= 1.0f && t > 0.0f && t < tmax) {
-            tmax = t;
-            hit.t = t;
-            hit.u = u;
-            hit.v = v;
-            hit.prim = pi;
-            found = true;
-            if (any) break;
-          }
-        } else {  // sphere (Sphere::test, sphere.cpp:10-31): nearer root if > 0 else farther
-          if (STATS) ct.spheres++;
-          float3 m = f3(v0.x, v0.y, v0.z) - o;
-          float bb = dot(m, d);
-          float cc = dot(m, m) - e1.y;
-          float disc = bb * bb - cc;
-          if (disc < 0.0f) continue;
-          float sq = sqrtf(disc);
-          float t1 = bb - sq, t2 = bb + sq;
-          // nearest: nearer root unless behind the origin (sphere.cpp:47-77);
-          // occlusion: the far root, as Sphere::intersect(r)'s aliased test (sphere.cpp:37-45)
-          float t = (t1 > 0.0f && !any) ? t1 : t2;
-          if (t > 0.0f && t < tmax) {
-            tmax = t;
-            hit.t = t;
-            hit.u = 0.0f;
-            hit.v = 0.0f;
-            hit.prim = pi;
-            found = true;
-            if (any) break;
-          }
-        }
-      }
-      if (any && found) break;
-    }
-    if (any && found) break;
-    bool in0 = hit0 && e.z == 0 && tn0 <= tmax;
-    bool in1 = hit1 && e.w == 0 && tn1 <= tmax;
-    if (in0 && in1) {
-      int nearN = tn0 <= tn1 ? e.x : e.y;
-      int farN = tn0 <= tn1 ? e.y : e.x;
-      stk[sp * stride] = farN;
-      ++sp;
-      node = nearN;
-    } else if (in0) {
-      node = e.x;
-    } else if (in1) {
-      node = e.y;
-    } else {
-      if (sp == 0) break;
-      --sp;
-      node = stk[sp * stride];
-    }
+  Trav tr;
+  trav_init(tr, o, d, tmax, any);
+  while (!trav_step<STATS>(nodes, prims, stk, stride, tr, ct)) {
   }
-  return found;
+  hit = tr.hit;
+  return tr.found;
 }
 
-enum : int { M_IDLE = 0, M_EXT = 1, M_SHADOW = 2, M_FETCH = 3, M_DONE = 4 };
+// Lane modes of the persistent kernel.
+enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 
-template <bool STATS>
+// DBG: diagnostic build that printf-traces the pixel P.dbg_pix (PT_DEBUG_PIXEL=x,y)
+template <bool STATS, bool DBG>
 __global__ __launch_bounds__(PT_BLOCK) void render_kernel(KParams P) {
   __shared__ int s_stack[PT_STACK * PT_BLOCK];
   int* stk = s_stack + threadIdx.x;
@@ -221,143 +245,78 @@ __global__ __launch_bounds__(PT_BLOCK) void render_kernel(KParams P) {
 
   // ---- per-lane state
   int mode = M_FETCH;
+  bool shadow = false;  // the ray in flight is a shadow ray
   int pix = 0, px = 0, py = 0, sample = 0;
   uint32_t rbase = 0, rdim = 0;
-  float3 acc = f3(0, 0, 0);      // pixel sum over samples (sample order)
-  float3 L = f3(0, 0, 0);        // radiance of the current sample
-  float3 T = f3(1, 1, 1);        // path throughput
+  float3 acc = f3(0, 0, 0);  // pixel sum over samples, in sample order
+  float3 L = f3(0, 0, 0);    // radiance of the current sample
+  float3 T = f3(1, 1, 1);    // path throughput
   int depth = 0;
   bool includeLe = true;
-  RayState ray;
-  ray.o = f3(0, 0, 0);
-  ray.d = f3(0, 0, 1);
-  ray.tmax = 0.0f;
-  // shading record of the current hit
+  // shading record of the current path vertex
   float3 hp = f3(0, 0, 0), ns = f3(0, 0, 1), ng = f3(0, 0, 1), wo = f3(0, 0, 1);
-  Frame fr;
-  fr.x = f3(1, 0, 0);
-  fr.y = f3(0, 1, 0);
-  fr.z = f3(0, 0, 1);
   int bsdf = 0;
-  int li = 0, ls = 0;           // NEE cursor: light index, light sample index
-  float3 pend = f3(0, 0, 0);    // NEE contribution awaiting its shadow ray
+  int li = 0, ls = 0;         // NEE cursor: light index, light sample index
+  float3 pend = f3(0, 0, 0);  // NEE contribution awaiting its shadow ray
+  Trav tr;
+  trav_init(tr, f3(0, 0, 0), f3(0, 0, 1), 0.0f, false);
   Counters ct = {0, 0, 0};
   uint32_t n_cam = 0, n_bounce = 0, n_shadow = 0, n_hits = 0;
 
   const uint32_t total_slots = (uint32_t)P.n_tiles * 1024u;
   const float inv_spp = (float)(1.0 / (double)P.spp);
+  const int batch = P.shade_batch;
 
   for (;;) {
-    // ---- wave-aggregated pixel fetch
-    for (;;) {
-      bool need = mode == M_FETCH;
-      unsigned long long m = __ballot(need);
-      if (m == 0ull) break;
-      int cnt = __popcll(m);
-      int leader = __ffsll((long long)m) - 1;
-      uint32_t base = 0;
-      if (lane == leader) base = atomicAdd(P.work_counter, (uint32_t)cnt);
-      base = __shfl(base, leader);
-      if (need) {
-        int rank = __popcll(m & ((1ull << lane) - 1ull));
-        uint32_t slot = base + (uint32_t)rank;
-        if (slot >= total_slots) {
-          mode = M_DONE;
-        } else {
-          int4 tile = P.tiles[slot >> 10];
-          uint32_t off = slot & 1023u;
-          uint32_t blk = off >> 6, w = off & 63u;
-          int x = tile.x + (int)((blk & 3u) * 8u + (w & 7u));
-          int y = tile.y + (int)((blk >> 2) * 8u + (w >> 3));
-          if (x < tile.x + tile.z && y < tile.y + tile.w) {
-            px = x;
-            py = y;
-            pix = x + y * P.W;
-            sample = 0;
-            acc = f3(0, 0, 0);
-            mode = M_IDLE;  // camera ray below
-          }
-        }
-      }
-    }
-    // ---- camera ray: Camera::generate_ray (camera.cpp:113-129) at the jittered
-    // pixel position of raytrace_pixel (pathtracer.cpp:571-575)
-    if (mode == M_IDLE) {
-      rbase = ptrng::stream_base(P.seed, (uint32_t)pix, (uint32_t)sample);
-      rdim = 0;
-      float ry = ptrng::draw(rbase, rdim++);  // UniformGridSampler2D draws y first
-      float rx = ptrng::draw(rbase, rdim++);
-      float fx = ((float)px + rx) / (float)P.W;
-      float fy = ((float)py + ry) / (float)P.H;
-      float3 sp = f3((0.5f - fx) * P.cam_ax, (0.5f - fy) * P.cam_ay, 1.0f);
-      float3 c0 = ld3(P.c2w_col0), c1 = ld3(P.c2w_col1), c2 = ld3(P.c2w_col2);
-      float3 wsp = c0 * sp.x + c1 * sp.y + c2 * sp.z;
-      ray.o = wsp + ld3(P.cam_pos);
-      ray.d = normalize(f3(0, 0, 0) - wsp);
-      ray.tmax = 3.0e38f;
-      L = f3(0, 0, 0);
-      T = f3(1, 1, 1);
-      depth = 0;
-      includeLe = true;
-      mode = M_EXT;
-      if (STATS) n_cam++;
-    }
-    if (__ballot(mode == M_EXT || mode == M_SHADOW) == 0ull) break;
-
-    // ---- one traversal per lane
-    Hit h;
-    h.t = 0.0f;
-    h.u = h.v = 0.0f;
-    h.prim = -1;
-    bool active = mode == M_EXT || mode == M_SHADOW;
-    bool found = false;
-    if (active)
-      found = traverse<STATS>(P.nodes, P.prims, stk, PT_BLOCK, ray.o, ray.d, ray.tmax, mode == M_SHADOW, h, ct);
-
-    // ---- shading state machine: runs until this lane has its next ray
-    if (!active) continue;
-    bool finish = false;  // sample finished
-    int stage;            // 0: NEE loop, 1: BSDF step
-    if (mode == M_SHADOW) {
-      if (!found) L = L + pend;  // unoccluded: the sample was already counted in ls
-      stage = 0;
-    } else {
-      if (!found) {
+    // ================= shading phase: lanes whose ray finished =================
+    if (mode == M_SHADE) {
+      const bool found = tr.found;
+      bool finish = false;  // the sample is complete
+      int stage;            // 0: NEE loop, 1: BSDF step, 2: none
+      if (shadow) {
+        if (!found) L = L + pend;  // unoccluded (the light sample was already counted)
+        if (DBG && pix == P.dbg_pix) printf("    shadow %s (pend %.6g) prim %d t %.9g\n", found ? "occluded" : "clear", pend.x, tr.hit.prim, tr.hit.t);
+        stage = 0;
+      } else if (!found) {
         finish = true;  // miss: no environment light (pathtracer.cpp:421-426)
         stage = 2;
       } else {
         if (STATS) n_hits++;
-        // ---- hit record (Intersection + trace_ray lines 435-456)
+        // ---- hit record (Intersection, trace_ray lines 435-456).  Hit points
+        // are rebuilt from the primitive (barycentrics / sphere reprojection),
+        // not o + t*d, so their error is relative to the primitive and the
+        // 256-ulp origin offset always clears the surface.
+        const Hit h = tr.hit;
         const DPrim pr = P.prims[h.prim];
         const int meta = __float_as_int(pr.v0.w);
         bsdf = meta >> 1;
-        hp = ray.o + ray.d * h.t;
         if (meta & 1) {
           const float* nn = P.norms + 9 * (size_t)h.prim;
           float w0 = 1.0f - h.u - h.v;
+          float3 E1 = f3(pr.e1.x, pr.e1.y, pr.e1.z), E2 = f3(pr.e2.x, pr.e2.y, pr.e2.z);
+          hp = f3(pr.v0.x, pr.v0.y, pr.v0.z) + E1 * h.u + E2 * h.v;
           ns = ld3(nn) * w0 + ld3(nn + 3) * h.u + ld3(nn + 6) * h.v;
-          ng = cross(f3(pr.e1.x, pr.e1.y, pr.e1.z), f3(pr.e2.x, pr.e2.y, pr.e2.z));
+          ng = cross(E1, E2);
         } else {
-          ns = normalize(hp - f3(pr.v0.x, pr.v0.y, pr.v0.z));
+          float3 C = f3(pr.v0.x, pr.v0.y, pr.v0.z);
+          ns = normalize(tr.o + tr.d * h.t - C);
+          hp = C + ns * pr.e1.x;
           ng = ns;
         }
-        if (dot(ray.d, ns) > 0.0f) ns = f3(0, 0, 0) - ns;
+        if (dot(tr.d, ns) > 0.0f) ns = f3(0, 0, 0) - ns;
         ng = normalize(ng);
-        fr = make_frame(ns);
-        wo = normalize(fr.to_local(f3(0, 0, 0) - ray.d));
-        const DBsdf B = P.bsdfs[bsdf];
-        if (includeLe) L = L + mul(T, ld3(B.e));
+        wo = normalize(make_frame(ns).to_local(f3(0, 0, 0) - tr.d));
+        if (includeLe) L = L + mul(T, ld3(P.bsdfs[bsdf].e));
+        if (DBG && pix == P.dbg_pix) printf("  depth %d hit prim %d bsdf %d t=%.9g n=(%.6g %.6g %.6g) T=(%.5g)\n", depth, h.prim, bsdf, h.t, ns.x, ns.y, ns.z, T.x);
         li = 0;
         ls = 0;
         stage = 0;
       }
-    }
-    mode = M_IDLE;
-    while (stage < 2) {
-      const DBsdf B = P.bsdfs[bsdf];
-      if (stage == 0) {
-        // ---- next-event estimation over all lights (pathtracer.cpp:469-523)
+      if (stage < 2) {
+        const DBsdf B = P.bsdfs[bsdf];
+        const Frame fr = make_frame(ns);
         bool emitted = false;
+        // ---- next-event estimation over all lights (pathtracer.cpp:469-523)
         while (li < P.n_lights) {
           const DLight Lt = P.lights[li];
           const bool delta = Lt.type == 0 || Lt.type == 2;
@@ -369,9 +328,8 @@ __global__ __launch_bounds__(PT_BLOCK) void render_kernel(KParams P) {
           }
           float3 wi;
           float dist, pdf;
-          float3 rad = ld3(Lt.rad);
           bool lit = true;
-          if (Lt.type == 3) {  // AreaLight::sample_L (light.cpp:80-92)
+          if (Lt.type == 3) {  // AreaLight::sample_L (light.cpp:80-92); grid sampler draws y first
             float u0 = ptrng::draw(rbase, rdim++);
             float u1 = ptrng::draw(rbase, rdim++);
             float sx = u1 - 0.5f, sy = u0 - 0.5f;
@@ -380,7 +338,7 @@ __global__ __launch_bounds__(PT_BLOCK) void render_kernel(KParams P) {
             float sq = dot(dv, dv);
             dist = sqrtf(sq);
             wi = dv * (1.0f / dist);
-            pdf = sq / (Lt.area * fabsf(cosL));
+            pdf = sq / (Lt.area * fabsf(cosL));  // unnormalised d.dir, as the reference
             lit = cosL < 0.0f;
           } else if (Lt.type == 1) {  // InfiniteHemisphereLight (light.cpp:34-42)
             float r1 = ptrng::draw(rbase, rdim++);
@@ -404,120 +362,168 @@ __global__ __launch_bounds__(PT_BLOCK) void render_kernel(KParams P) {
           ++ls;
           // f() is zero for every BSDF but Diffuse (bsdf.cpp:34-202): nothing to add.
           if (B.type != 0 || !lit) continue;
-          float3 wl = fr.to_local(wi);
-          float cos_t = fmaxf(0.0f, wl.z);
+          float cos_t = fmaxf(0.0f, fr.to_local(wi).z);
           if (!(cos_t > 0.0f)) continue;
           float3 f = ld3(B.a) * 0.31830988618379067f;
-          float3 contrib = mul(mul(T, rad * (cos_t / pdf)), f) * scale;
+          pend = mul(mul(T, ld3(Lt.rad) * (cos_t / pdf)), f) * scale;
           // shadow ray (pathtracer.cpp:497-504): delta lights offset EPS_N along n
-          float3 so;
-          if (delta) so = hp + ns * 5e-3f;
-          else so = offset_ray(hp, dot(wi, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng);
-          ray.o = so;
-          ray.d = wi;
-          ray.tmax = dist * 0.999f;
-          pend = contrib;
+          float3 so = delta ? hp + ns * 5e-3f : offset_ray(hp, dot(wi, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng);
+          trav_init(tr, so, wi, dist * 0.999f, true);
+          if (DBG && pix == P.dbg_pix) printf("    shadow o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) maxt=%.9g cos %.4g pdf %.4g\n", so.x, so.y, so.z, wi.x, wi.y, wi.z, tr.tmax, cos_t, pdf);
           emitted = true;
           if (STATS) n_shadow++;
           break;
         }
         if (emitted) {
-          mode = M_SHADOW;
-          break;
-        }
-        stage = 1;
-      }
-      if (stage == 1) {
-        // ---- indirect bounce (pathtracer.cpp:527-552)
-        if (depth >= P.max_depth) {
+          shadow = true;
+          mode = M_TRAV;
+        } else if (depth >= P.max_depth) {
           finish = true;
-          break;
-        }
-        float3 wi;
-        float pdf = 1.0f;
-        float3 f;
-        bool reached = true;
-        if (B.type == 0 || B.type == 4) {  // cosine hemisphere (sampler.cpp:44-55)
-          float r1 = ptrng::draw(rbase, rdim++);
-          float r2 = ptrng::draw(rbase, rdim++);
-          float ct = sqrtf(1.0f - r1);  // cos(acos(1-2 r1)/2)
-          float stt = sqrtf(r1);
-          float ph = 6.28318530717958647f * r2;
-          wi = f3(stt * cosf(ph), stt * sinf(ph), ct);
-          pdf = ct * 0.31830988618379067f;
-          f = B.type == 0 ? ld3(B.a) * 0.31830988618379067f : f3(0, 0, 0);
-        } else if (B.type == 1) {  // MirrorBSDF::sample_f (bsdf.cpp:60-69)
-          wi = f3(-wo.x, -wo.y, wo.z);
-          f = ld3(B.a) * (1.0f / fmaxf(wo.z, 1e-8f));
-        } else {  // Refraction (bsdf.cpp:90-111) / Glass (bsdf.cpp:120-158)
-          float ratio = B.ior;
-          float sgn = 1.0f;
-          if (wo.z > 0.0f) {
-            sgn = -1.0f;
-            ratio = 1.0f / ratio;
-          }
-          float cos2 = 1.0f - ratio * ratio * (1.0f - wo.z * wo.z);
-          bool tir = cos2 < 0.0f;
-          if (tir) {
+        } else {
+          // ---- indirect bounce (pathtracer.cpp:527-552)
+          float3 wi;
+          float pdf = 1.0f;
+          float3 f;
+          if (B.type == 0 || B.type == 4) {  // cosine hemisphere (sampler.cpp:44-55)
+            float r1 = ptrng::draw(rbase, rdim++);
+            float r2 = ptrng::draw(rbase, rdim++);
+            float ct = sqrtf(1.0f - r1);  // cos(acos(1 - 2 r1) / 2)
+            float stt = sqrtf(r1);
+            float ph = 6.28318530717958647f * r2;
+            wi = f3(stt * cosf(ph), stt * sinf(ph), ct);
+            pdf = ct * 0.31830988618379067f;
+            f = B.type == 0 ? ld3(B.a) * 0.31830988618379067f : f3(0, 0, 0);
+          } else if (B.type == 1) {  // MirrorBSDF::sample_f (bsdf.cpp:60-69)
             wi = f3(-wo.x, -wo.y, wo.z);
-          } else {
-            wi = normalize(f3(-wo.x * ratio, -wo.y * ratio, sgn * sqrtf(cos2)));
-          }
-          float ni = B.ior, no = 1.0f;
-          if (wo.z < 0.0f) {
-            ni = 1.0f;
-            no = B.ior;
-          }
-          float inv_cos = 1.0f / fmaxf(fabsf(wi.z), 1e-8f);
-          if (B.type == 2) {
-            f = tir ? f3(0, 0, 0) : ld3(B.t) * ((no / ni) * (no / ni) * inv_cos);
-          } else if (tir) {
-            f = ld3(B.t) * inv_cos;  // quirk kept: TIR returns transmittance (bsdf.cpp:129-131)
-          } else {
-            float ci = fabsf(wi.z), co = fabsf(wo.z);
-            float r1 = (no * ci - ni * co) / (no * ci + ni * co);
-            float r2 = (ni * ci - no * co) / (ni * ci + no * co);
-            float Fr = 0.5f * (r1 * r1 + r2 * r2);
-            if (ptrng::draw(rbase, rdim++) <= Fr) {
-              wi = f3(-wo.x, -wo.y, wo.z);
-              f = ld3(B.a) * (1.0f / fmaxf(fabsf(wi.z), 1e-8f));
+            f = ld3(B.a) * (1.0f / fmaxf(wo.z, 1e-8f));
+          } else {  // Refraction (bsdf.cpp:90-111) / Glass (bsdf.cpp:120-158)
+            float ratio = B.ior;
+            float sgn = 1.0f;
+            if (wo.z > 0.0f) {
+              sgn = -1.0f;
+              ratio = 1.0f / ratio;
+            }
+            float cos2 = 1.0f - ratio * ratio * (1.0f - wo.z * wo.z);
+            bool tir = cos2 < 0.0f;
+            wi = tir ? f3(-wo.x, -wo.y, wo.z) : normalize(f3(-wo.x * ratio, -wo.y * ratio, sgn * sqrtf(cos2)));
+            float ni = B.ior, no = 1.0f;
+            if (wo.z < 0.0f) {
+              ni = 1.0f;
+              no = B.ior;
+            }
+            float inv_cos = 1.0f / fmaxf(fabsf(wi.z), 1e-8f);
+            if (B.type == 2) {
+              f = tir ? f3(0, 0, 0) : ld3(B.t) * ((no / ni) * (no / ni) * inv_cos);
+            } else if (tir) {
+              f = ld3(B.t) * inv_cos;  // quirk kept: TIR returns transmittance (bsdf.cpp:129-131)
             } else {
-              f = ld3(B.t) * ((no / ni) * (no / ni) * inv_cos);
+              float ci = fabsf(wi.z), co = fabsf(wo.z);
+              float r1 = (no * ci - ni * co) / (no * ci + ni * co);
+              float r2 = (ni * ci - no * co) / (ni * ci + no * co);
+              float Fr = 0.5f * (r1 * r1 + r2 * r2);
+              if (ptrng::draw(rbase, rdim++) <= Fr) {
+                wi = f3(-wo.x, -wo.y, wo.z);
+                f = ld3(B.a) * (1.0f / fmaxf(fabsf(wi.z), 1e-8f));
+              } else {
+                f = ld3(B.t) * ((no / ni) * (no / ni) * inv_cos);
+              }
             }
           }
+          // Russian roulette (pathtracer.cpp:534-541)
+          float pterm = fmaxf(1.0f - illum(f), 0.0f);
+          if (ptrng::draw(rbase, rdim++) < pterm) {
+            if (DBG && pix == P.dbg_pix) printf("    RR terminate (p=%.4g)\n", pterm);
+            finish = true;
+          } else {
+            if (DBG && pix == P.dbg_pix) printf("    bounce wi=(%.6g %.6g %.6g) pdf %.5g p %.4g dim %u\n", wi.x, wi.y, wi.z, pdf, pterm, rdim);
+            T = mul(T, f * (fabsf(wi.z) / (pdf * (1.0f - pterm))));
+            float3 v = normalize(fr.to_world(wi));
+            trav_init(tr, offset_ray(hp, dot(v, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng), v, 3.0e38f, false);
+            includeLe = B.type == 1 || B.type == 2 || B.type == 3;
+            ++depth;
+            shadow = false;
+            mode = M_TRAV;
+            if (STATS) n_bounce++;
+          }
         }
-        (void)reached;
-        // Russian roulette (pathtracer.cpp:534-541)
-        float pterm = fmaxf(1.0f - illum(f), 0.0f);
-        if (ptrng::draw(rbase, rdim++) < pterm) {
-          finish = true;
-          break;
+      }
+      if (finish) {
+        acc = acc + L;
+        ++sample;
+        if (sample < P.spp) {
+          mode = M_CAMERA;
+        } else {
+          float* o = P.out + 3 * (size_t)pix;
+          o[0] = acc.x * inv_spp;
+          o[1] = acc.y * inv_spp;
+          o[2] = acc.z * inv_spp;
+          mode = M_FETCH;
         }
-        float w = fabsf(wi.z) / (pdf * (1.0f - pterm));
-        T = mul(T, f * w);
-        float3 v = normalize(fr.to_world(wi));
-        ray.o = offset_ray(hp, dot(v, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng);
-        ray.d = v;
-        ray.tmax = 3.0e38f;
-        includeLe = B.type == 1 || B.type == 2 || B.type == 3;
-        ++depth;
-        mode = M_EXT;
-        if (STATS) n_bounce++;
-        break;
       }
     }
-    if (finish) {
-      acc = acc + L;
-      ++sample;
-      if (sample < P.spp) {
-        mode = M_IDLE;
-      } else {
-        float* o = P.out + 3 * (size_t)pix;
-        o[0] = acc.x * inv_spp;
-        o[1] = acc.y * inv_spp;
-        o[2] = acc.z * inv_spp;
-        mode = M_FETCH;
+    // ---- wave-aggregated pixel fetch (one atomic per wave per refill)
+    for (;;) {
+      bool need = mode == M_FETCH;
+      unsigned long long m = __ballot(need);
+      if (m == 0ull) break;
+      int cnt = __popcll(m);
+      int leader = __ffsll((long long)m) - 1;
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(P.work_counter, (uint32_t)cnt);
+      base = __shfl(base, leader);
+      if (need) {
+        uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (slot >= total_slots) {
+          mode = M_DONE;
+        } else {
+          int4 tile = P.tiles[slot >> 10];
+          uint32_t off = slot & 1023u;
+          uint32_t blk = off >> 6, w = off & 63u;
+          int x = tile.x + (int)((blk & 3u) * 8u + (w & 7u));
+          int y = tile.y + (int)((blk >> 2) * 8u + (w >> 3));
+          if (x < tile.x + tile.z && y < tile.y + tile.w) {
+            px = x;
+            py = y;
+            pix = x + y * P.W;
+            sample = 0;
+            acc = f3(0, 0, 0);
+            mode = M_CAMERA;
+          }
+        }
       }
+    }
+    // ---- camera ray: Camera::generate_ray (camera.cpp:113-129) at the jittered
+    // pixel position of raytrace_pixel (pathtracer.cpp:571-575)
+    if (mode == M_CAMERA) {
+      rbase = ptrng::stream_base(P.seed, (uint32_t)pix, (uint32_t)sample);
+      rdim = 0;
+      float ry = ptrng::draw(rbase, rdim++);  // UniformGridSampler2D draws y first
+      float rx = ptrng::draw(rbase, rdim++);
+      float fx = ((float)px + rx) / (float)P.W;
+      float fy = ((float)py + ry) / (float)P.H;
+      float3 sp = f3((0.5f - fx) * P.cam_ax, (0.5f - fy) * P.cam_ay, 1.0f);
+      float3 wsp = ld3(P.c2w_col0) * sp.x + ld3(P.c2w_col1) * sp.y + ld3(P.c2w_col2) * sp.z;
+      float3 d = normalize(f3(0, 0, 0) - wsp);
+      trav_init(tr, wsp + ld3(P.cam_pos), d, 3.0e38f, false);
+      L = f3(0, 0, 0);
+      T = f3(1, 1, 1);
+      depth = 0;
+      includeLe = true;
+      shadow = false;
+      mode = M_TRAV;
+      if (STATS) n_cam++;
+      if (DBG && pix == P.dbg_pix) printf("pixel (%d,%d) sample %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g)\n", px, py, sample, tr.o.x, tr.o.y, tr.o.z, d.x, d.y, d.z);
+    }
+    // ================= traversal phase =================
+    // Step every in-flight ray one node at a time; leave as soon as `batch`
+    // lanes have finished their ray, so finished lanes are refilled together
+    // (coherent shading) while the others keep their traversal state.
+    if (__ballot(mode == M_TRAV) == 0ull) break;  // every lane is M_DONE
+    for (;;) {
+      if (mode == M_TRAV && trav_step<STATS>(P.nodes, P.prims, stk, PT_BLOCK, tr, ct)) mode = M_SHADE;
+      unsigned long long ready = __ballot(mode == M_SHADE);
+      unsigned long long busy = __ballot(mode == M_TRAV);
+      if (busy == 0ull || __popcll(ready) >= batch) break;
     }
   }
 
@@ -561,10 +567,12 @@ __global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __rest
 
 // ------------------------------------------------------------------ launchers
 extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, hipStream_t s) {
-  if (stats)
-    hipLaunchKernelGGL(ptk::render_kernel<true>, dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+  if (P->dbg_pix >= 0)
+    hipLaunchKernelGGL((ptk::render_kernel<false, true>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+  else if (stats)
+    hipLaunchKernelGGL((ptk::render_kernel<true, false>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
   else
-    hipLaunchKernelGGL(ptk::render_kernel<false>, dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+    hipLaunchKernelGGL((ptk::render_kernel<false, false>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
   return hipGetLastError();
 }
 
@@ -580,6 +588,6 @@ extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prim
 
 extern "C" hipError_t ptk_render_occupancy(int* blocks_per_cu, bool stats) {
   if (stats)
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ptk::render_kernel<true>, PT_BLOCK, 0);
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ptk::render_kernel<false>, PT_BLOCK, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ptk::render_kernel<true, false>, PT_BLOCK, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ptk::render_kernel<false, false>, PT_BLOCK, 0);
 }

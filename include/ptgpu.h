@@ -154,6 +154,8 @@ typedef struct pt_stats {
   int64_t ext_hits;     /* nearest-hit rays that hit (shading-normal fetch) */
   double last_ms;       /* device time of the last render kernel (hipEvent) */
   int32_t counters_valid; /* 1 if the last call ran with PT_FLAG_STATS */
+  int32_t grid_blocks;    /* persistent workgroups launched (PT_BLOCK lanes each) */
+  int32_t blocks_per_cu;  /* resident workgroups per CU the occupancy query allows */
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */

@@ -40,6 +40,14 @@
 
 namespace rs {
 
+// Diagnostic trace of one pixel (RS_DEBUG_PIXEL=x,y): prints every hit/NEE/bounce.
+static int g_dbg_x = -1, g_dbg_y = -1;
+static thread_local bool t_dbg = false;
+#define RS_DBG(...) \
+  do {              \
+    if (t_dbg) std::fprintf(stderr, __VA_ARGS__); \
+  } while (0)
+
 static const double PI_D = 3.14159265358979323;
 static const double EPS_D = 0.00000000001;
 static const double EPS_N = 5e-3;
@@ -453,6 +461,8 @@ struct Tracer {
     if (!intersect(r, &isect)) return Spec(0, 0, 0);
     const Prim& P = S.prims[isect.prim];
     const Bsdf& B = S.bsdfs[P.bsdf];
+    RS_DBG("  depth %zu hit prim %d (type %d bsdf %d) t=%.9g n=(%.6g %.6g %.6g)\n", r.depth, isect.prim, P.type,
+           P.bsdf, isect.t, isect.n.x, isect.n.y, isect.n.z);
     Spec L_out = includeLe ? B.e : Spec();
     V3 hit_p = r.o + r.d * isect.t;
     M3 o2w;
@@ -474,12 +484,19 @@ struct Tracer {
         Ray sR(hit_p + eps * isect.n + EPS_D * dir_to_light, dir_to_light);
         sR.max_t = dist_to_light * 0.999;
         st.shadow++;
-        if (intersect(sR, nullptr)) continue;
+        if (intersect(sR, nullptr)) {
+          RS_DBG("    shadow ray occluded (Li %.4g pdf %.4g dist %.6g)\n", light_L.r, pdf, dist_to_light);
+          continue;
+        }
         V3 w_in = w2o.mul(dir_to_light);
         w_in.normalize();
         double cos_theta = std::max(0.0, w_in[2]);
         Spec fv = f(B);
         L += (float)(cos_theta / pdf) * light_L * fv;
+        RS_DBG("    shadow o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) maxt=%.9g\n", sR.o.x, sR.o.y, sR.o.z, sR.d.x, sR.d.y,
+               sR.d.z, sR.max_t);
+        RS_DBG("    NEE + %.6g (cos %.4g pdf %.4g Li %.4g)\n", (float)(cos_theta / pdf) * light_L.r * fv.r, cos_theta,
+               pdf, light_L.r);
       }
       L_out += L * (float)scale;
     }
@@ -488,7 +505,11 @@ struct Tracer {
     Spec fs = sample_f(B, w_out, &w_in, &pdf, rng);
     double cos_theta = std::fabs(w_in[2]);
     double terminateProbability = std::max(1 - fs.illum(), 0.f);
-    if (rng.next() < terminateProbability) return L_out;
+    if (rng.next() < terminateProbability) {
+      RS_DBG("    RR terminate (p=%.4g)\n", terminateProbability);
+      return L_out;
+    }
+    RS_DBG("    bounce wi=(%.6g %.6g %.6g) pdf %.5g p %.4g\n", w_in.x, w_in.y, w_in.z, pdf, terminateProbability);
     V3 v = o2w.mul(w_in);
     v.normalize();
     Ray refR(hit_p + EPS_D * v, v);
@@ -603,6 +624,7 @@ int rs_render(const char* scene_path, int w, int h, int spp, int max_depth, int 
     for (int x = 0; x < w; x += T) tiles.push_back({x, y});
   if (tile_end < 0 || tile_end > (int)tiles.size()) tile_end = (int)tiles.size();
   if (tile_begin < 0) tile_begin = 0;
+  if (const char* dp = std::getenv("RS_DEBUG_PIXEL")) std::sscanf(dp, "%d,%d", &rs::g_dbg_x, &rs::g_dbg_y);
   std::atomic<int> next(tile_begin);
   std::vector<rs::Stats> stats(std::max(1, threads));
   auto worker = [&](int wid) {
@@ -620,8 +642,10 @@ int rs_render(const char* scene_path, int w, int h, int spp, int max_depth, int 
         for (int x = x0; x < x1; x++) {
           rs::Spec s(0, 0, 0);
           uint32_t pix = (uint32_t)(x + y * w);
+          rs::t_dbg = (x == rs::g_dbg_x && y == rs::g_dbg_y);
           for (int i = 0; i < spp; i++) {
             if (rng_mode == 1) rng.start(seed, pix, (uint32_t)i);
+            if (rs::t_dbg) std::fprintf(stderr, "pixel (%d,%d) sample %d\n", x, y, i);
             double ry = rng.next();  // UniformGridSampler2D: right-to-left
             double rx = rng.next();
             double px = (x + rx) / w;
