@@ -90,6 +90,7 @@ struct pt_ctx {
   DevBuf<int32_t> q_i;
   int n_lights = 0;
   int64_t n_prims = 0;
+  float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
   bool have_scene = false, have_cam = false, have_params = false;
   pt_camera cam{};
   pt_params params{};
@@ -303,6 +304,10 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
   if (!ls.empty()) HIPCHK(hipMemcpy(c->lights.p, ls.data(), ls.size() * sizeof(DLight), hipMemcpyHostToDevice));
   c->n_lights = (int)ls.size();
   c->n_prims = s->n_prims;
+  for (int k = 0; k < 3; ++k) {
+    c->root_lo[k] = round_down(N[0].bb_min[k]);
+    c->root_hi[k] = round_up(N[0].bb_max[k]);
+  }
   c->have_scene = true;
   return PT_OK;
 }
@@ -375,7 +380,11 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.work_counter = c->counter.p;
   P.stats = c->stats.p;
   P.dbg_pix = -1;
-  P.shade_batch = 32;
+  for (int k = 0; k < 3; ++k) {
+    P.root_lo[k] = c->root_lo[k];
+    P.root_hi[k] = c->root_hi[k];
+  }
+  P.shade_batch = 64;
   if (const char* sb = std::getenv("PT_SHADE_BATCH")) {  // tuning knob
     int v = std::atoi(sb);
     if (v >= 1 && v <= 64) P.shade_batch = v;

@@ -67,6 +67,7 @@ struct KParams {
   unsigned long long* stats;  // 7 counters (PT_FLAG_STATS)
   int dbg_pix;                // diagnostic printf trace of one pixel (-1: off)
   int shade_batch;            // leave the traversal phase once this many lanes finished their ray
+  float root_lo[3], root_hi[3];  // scene bounds (root box, rounded outward)
 };
 
 extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, hipStream_t s);

@@ -233,6 +233,17 @@ __device__ __forceinline__ bool traverse(const DNode* __restrict__ nodes, const 
   return tr.found;
 }
 
+// Robust slab test of the ray in `tr` against one box (lo, hi), clipped to [0, tmax].
+__device__ __forceinline__ bool box_hit(const Trav& tr, const float* lo, const float* hi) {
+  const float3 oi = f3(tr.o.x * tr.inv.x, tr.o.y * tr.inv.y, tr.o.z * tr.inv.z);
+  float lx = fmaf(lo[0], tr.inv.x, -oi.x), hx = fmaf(hi[0], tr.inv.x, -oi.x);
+  float ly = fmaf(lo[1], tr.inv.y, -oi.y), hy = fmaf(hi[1], tr.inv.y, -oi.y);
+  float lz = fmaf(lo[2], tr.inv.z, -oi.z), hz = fmaf(hi[2], tr.inv.z, -oi.z);
+  float tn = fmaxf(fmaxf(fminf(lx, hx), fminf(ly, hy)), fmaxf(fminf(lz, hz), 0.0f));
+  float tf = fminf(fminf(fmaxf(lx, hx), fmaxf(ly, hy)), fminf(fmaxf(lz, hz), tr.tmax)) * 1.0000005f;
+  return tn <= tf;
+}
+
 // Lane modes of the persistent kernel.
 enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 
@@ -461,58 +472,75 @@ __global__ __launch_bounds__(PT_BLOCK) void render_kernel(KParams P) {
         }
       }
     }
-    // ---- wave-aggregated pixel fetch (one atomic per wave per refill)
+    // ---- refill: wave-aggregated pixel fetch (one atomic per wave per round)
+    // and camera rays.  Camera rays that miss the scene's root box carry zero
+    // radiance (no environment light, pathtracer.cpp:421-426): they are
+    // completed here without touching memory, so background pixels never
+    // occupy a traversal slot.
     for (;;) {
       bool need = mode == M_FETCH;
       unsigned long long m = __ballot(need);
-      if (m == 0ull) break;
-      int cnt = __popcll(m);
-      int leader = __ffsll((long long)m) - 1;
-      uint32_t base = 0;
-      if (lane == leader) base = atomicAdd(P.work_counter, (uint32_t)cnt);
-      base = __shfl(base, leader);
-      if (need) {
-        uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        if (slot >= total_slots) {
-          mode = M_DONE;
-        } else {
-          int4 tile = P.tiles[slot >> 10];
-          uint32_t off = slot & 1023u;
-          uint32_t blk = off >> 6, w = off & 63u;
-          int x = tile.x + (int)((blk & 3u) * 8u + (w & 7u));
-          int y = tile.y + (int)((blk >> 2) * 8u + (w >> 3));
-          if (x < tile.x + tile.z && y < tile.y + tile.w) {
-            px = x;
-            py = y;
-            pix = x + y * P.W;
-            sample = 0;
-            acc = f3(0, 0, 0);
-            mode = M_CAMERA;
+      if (m != 0ull) {
+        int cnt = __popcll(m);
+        int leader = __ffsll((long long)m) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(P.work_counter, (uint32_t)cnt);
+        base = __shfl(base, leader);
+        if (need) {
+          uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+          if (slot >= total_slots) {
+            mode = M_DONE;
+          } else {
+            int4 tile = P.tiles[slot >> 10];
+            uint32_t off = slot & 1023u;
+            uint32_t blk = off >> 6, w = off & 63u;
+            int x = tile.x + (int)((blk & 3u) * 8u + (w & 7u));
+            int y = tile.y + (int)((blk >> 2) * 8u + (w >> 3));
+            if (x < tile.x + tile.z && y < tile.y + tile.w) {
+              px = x;
+              py = y;
+              pix = x + y * P.W;
+              sample = 0;
+              acc = f3(0, 0, 0);
+              mode = M_CAMERA;
+            }
           }
         }
       }
-    }
-    // ---- camera ray: Camera::generate_ray (camera.cpp:113-129) at the jittered
-    // pixel position of raytrace_pixel (pathtracer.cpp:571-575)
-    if (mode == M_CAMERA) {
-      rbase = ptrng::stream_base(P.seed, (uint32_t)pix, (uint32_t)sample);
-      rdim = 0;
-      float ry = ptrng::draw(rbase, rdim++);  // UniformGridSampler2D draws y first
-      float rx = ptrng::draw(rbase, rdim++);
-      float fx = ((float)px + rx) / (float)P.W;
-      float fy = ((float)py + ry) / (float)P.H;
-      float3 sp = f3((0.5f - fx) * P.cam_ax, (0.5f - fy) * P.cam_ay, 1.0f);
-      float3 wsp = ld3(P.c2w_col0) * sp.x + ld3(P.c2w_col1) * sp.y + ld3(P.c2w_col2) * sp.z;
-      float3 d = normalize(f3(0, 0, 0) - wsp);
-      trav_init(tr, wsp + ld3(P.cam_pos), d, 3.0e38f, false);
-      L = f3(0, 0, 0);
-      T = f3(1, 1, 1);
-      depth = 0;
-      includeLe = true;
-      shadow = false;
-      mode = M_TRAV;
-      if (STATS) n_cam++;
-      if (DBG && pix == P.dbg_pix) printf("pixel (%d,%d) sample %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g)\n", px, py, sample, tr.o.x, tr.o.y, tr.o.z, d.x, d.y, d.z);
+      // ---- camera rays: Camera::generate_ray (camera.cpp:113-129) at the
+      // jittered pixel position of raytrace_pixel (pathtracer.cpp:571-575)
+      while (mode == M_CAMERA) {
+        rbase = ptrng::stream_base(P.seed, (uint32_t)pix, (uint32_t)sample);
+        rdim = 0;
+        float ry = ptrng::draw(rbase, rdim++);  // UniformGridSampler2D draws y first
+        float rx = ptrng::draw(rbase, rdim++);
+        float fx = ((float)px + rx) / (float)P.W;
+        float fy = ((float)py + ry) / (float)P.H;
+        float3 sp = f3((0.5f - fx) * P.cam_ax, (0.5f - fy) * P.cam_ay, 1.0f);
+        float3 wsp = ld3(P.c2w_col0) * sp.x + ld3(P.c2w_col1) * sp.y + ld3(P.c2w_col2) * sp.z;
+        float3 d = normalize(f3(0, 0, 0) - wsp);
+        trav_init(tr, wsp + ld3(P.cam_pos), d, 3.0e38f, false);
+        if (STATS) n_cam++;
+        if (DBG && pix == P.dbg_pix) printf("pixel (%d,%d) sample %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g)\n", px, py, sample, tr.o.x, tr.o.y, tr.o.z, d.x, d.y, d.z);
+        if (box_hit(tr, P.root_lo, P.root_hi)) {
+          L = f3(0, 0, 0);
+          T = f3(1, 1, 1);
+          depth = 0;
+          includeLe = true;
+          shadow = false;
+          mode = M_TRAV;
+          break;
+        }
+        // miss: the sample contributes 0
+        if (++sample >= P.spp) {
+          float* o = P.out + 3 * (size_t)pix;
+          o[0] = acc.x * inv_spp;
+          o[1] = acc.y * inv_spp;
+          o[2] = acc.z * inv_spp;
+          mode = M_FETCH;
+        }
+      }
+      if (__ballot(mode == M_FETCH) == 0ull) break;
     }
     // ================= traversal phase =================
     // Step every in-flight ray one node at a time; leave as soon as `batch`
