@@ -12,9 +12,10 @@ outside the timed region, as in the reference's timers.
 
 N > 1 (one process per GPU, torchrun): ranks render interleaved 32x32 tiles
 (tile_id mod N) into a zeroed device frame and the frames are summed onto rank 0
-with an RCCL reduce over xGMI (non-owners add +0.0, so the image is bit-identical
-to the 1-GPU image); per-GPU work is fixed per frame => "scaling": "strong" is
-NOT what happens here: total work per step is fixed, so scaling is "strong".
+with one RCCL reduce over xGMI (non-owners add +0.0, so the image is
+bit-identical to the 1-GPU image).  The frame is fixed and split across the
+GPUs, so "scaling" is "strong"; value = all pixels*spp of the frame / max-rank
+time.  The reduce is inside the timed region.
 """
 from __future__ import annotations
 
@@ -40,6 +41,20 @@ def algorithmic_bytes(st: dict) -> float:
     prim = st["tri_tests"] + st["sphere_tests"]
     return (64.0 * st["node_visits"] + 48.0 * st["tri_tests"] + 16.0 * st["sphere_tests"] + 4.0 * prim
             + 36.0 * st["ext_hits"] + 12.0 * st["pixels"])
+
+
+def measured_traffic():
+    """HBM bytes per launch of the render kernel on this workload, from the
+    rocprofv3 PMC passes committed under profiles/ (FETCH_SIZE doubled per the
+    gfx950 correction of MI355X_MICROARCH.md §HBM, + WRITE_SIZE; KB -> bytes).
+    None when no summary for this workload is committed."""
+    p = os.path.join(ROOT, "profiles", "latest_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_baseline(scene_dump: str, budget_s: float = 12.0) -> dict:
@@ -78,14 +93,10 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
+    from dsgpuraytracing_amd.dist import init_from_env, render_sharded
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(local)
+    torch.cuda.set_device(local)
+    rank, world, local = init_from_env("nccl")
 
     from dsgpuraytracing_amd import scenes
     from dsgpuraytracing_amd.pathtracer import Device, Scene, tile_fifo
@@ -104,19 +115,19 @@ def main():
     dev.set_params(W, H, SPP, DEPTH, NSL, SEED)
     t_load = time.perf_counter() - t_load
 
-    tiles = tile_fifo(W, H)[rank::world]
+    tiles = tile_fifo(W, H)
     frame = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{local}")
     stream = torch.cuda.current_stream().cuda_stream
 
     def step(stats=False):
-        dev.render_tiles_device(tiles, frame.data_ptr(), stream, stats=stats)
-        if world > 1:
-            dist.reduce(frame, dst=0)
+        render_sharded(lambda mine: dev.render_tiles_device(mine, frame.data_ptr(), stream, stats=stats),
+                       frame, tiles, rank, world)
         return dev.stats()
 
     # counters for the roofline's algorithmic bytes (deterministic: same work as every step)
     st_counts = step(stats=True)
     for _ in range(args.warmup):
+        frame.zero_()
         step()
     if world > 1:
         dist.barrier()
@@ -125,7 +136,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         if world > 1:
-            frame.zero_()
+            frame.zero_()  # the reduce sums whole frames: non-owned tiles must be +0.0
         s = step()
         kernel_ms.append(s["last_ms"])
     if world > 1:
@@ -136,9 +147,6 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        counts = torch.tensor([st_counts[k] for k in ("node_visits", "tri_tests", "sphere_tests", "ext_hits",
-                                                      "pixels")], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(counts)
 
     if rank == 0:
         frames = args.steps
@@ -165,7 +173,7 @@ def main():
                        "parallelism": f"tiles{world}" if world > 1 else "single",
                        "render_time_s": round(elapsed / frames, 4), "scene_load_s": round(t_load, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": measured_traffic(),
                          "kernel": "render_kernel<false>", "kernel_ms": round(avg_ms, 3),
                          "algorithmic_bytes_per_launch": bytes_launch},
             "counters": {k: st_counts[k] for k in ("camera_rays", "bounce_rays", "shadow_rays", "node_visits",
@@ -174,7 +182,8 @@ def main():
             "image_mean": float(img.mean()),
         }
         rays = st_counts["camera_rays"] + st_counts["bounce_rays"] + st_counts["shadow_rays"]
-        out["ray_casts_per_s_M"] = round(rays * frames / elapsed / 1e6 if world == 1 else float("nan"), 1)
+        if world == 1:
+            out["ray_casts_per_s_M"] = round(rays * frames / elapsed / 1e6, 1)
         if world == 1 and not args.no_cpu_baseline:
             try:
                 dp = dump_path

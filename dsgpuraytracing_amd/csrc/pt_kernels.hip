@@ -314,7 +314,10 @@ __global__ __launch_bounds__(PT_BLOCK) void render_kernel(KParams P) {
           hp = C + ns * pr.e1.x;
           ng = ns;
         }
-        if (dot(tr.d, ns) > 0.0f) ns = f3(0, 0, 0) - ns;
+        // Triangle::intersect flips the shading normal to face the ray
+        // (triangle.cpp:95-99); Sphere::intersect keeps it outward
+        // (sphere.cpp:66-70), which is what tells GlassBSDF a ray is leaving.
+        if ((meta & 1) && dot(tr.d, ns) > 0.0f) ns = f3(0, 0, 0) - ns;
         ng = normalize(ng);
         wo = normalize(make_frame(ns).to_local(f3(0, 0, 0) - tr.d));
         if (includeLe) L = L + mul(T, ld3(P.bsdfs[bsdf].e));

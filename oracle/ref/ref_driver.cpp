@@ -19,6 +19,7 @@
 #include "bsdf.h"
 #include "camera.h"
 #include "collada/collada.h"
+#include "dynamic_scene/ambient_light.h"
 #include "dynamic_scene/area_light.h"
 #include "dynamic_scene/directional_light.h"
 #include "dynamic_scene/point_light.h"
@@ -74,6 +75,7 @@ static void build_scene(const Opts& o, Camera& camera, DynamicScene::Scene*& dsc
         Collada::LightInfo& li = static_cast<Collada::LightInfo&>(*instance);
         DynamicScene::SceneLight* l = nullptr;
         switch (li.light_type) {
+          case Collada::LightType::AMBIENT: l = new DynamicScene::AmbientLight(li); break;
           case Collada::LightType::DIRECTIONAL: l = new DynamicScene::DirectionalLight(li, transform); break;
           case Collada::LightType::AREA: l = new DynamicScene::AreaLight(li, transform); break;
           case Collada::LightType::POINT: l = new DynamicScene::PointLight(li, transform); break;

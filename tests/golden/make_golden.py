@@ -32,6 +32,9 @@ REF = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
 C1 = os.path.join(ROOT, "assets", "CBspheres_lambertian.dae")
 CAMS = {"default": None, "sphcam": os.path.join(ROOT, "assets", "cam_sphere.info")}
 
+EXTRA_SCENES = ["CBspheres", "CBspheres_lambertian_pointlight", "CBspheres_lambertian_dirlight",
+                "CBspheres_lambertian_ambientlight"]
+
 SCENES = [("default", 64, 64), ("sphcam", 96, 64), ("default", 128, 128), ("default", 256, 256)]
 RENDERS = [
     # (cam, W, H, spp, depth, ns_area_light, seed)
@@ -72,6 +75,22 @@ def main():
         run(args)
         d = ptdump.read(out)
         ptdump.write(out, {"hdr": d["hdr"], "shape": d["shape"]})  # drop the wall time: deterministic file
+    # BSDF / light coverage: mirror + glass spheres (CBspheres.dae, the BSDFs of
+    # config C5) and point / directional / ambient (hemisphere) light variants.
+    for name in EXTRA_SCENES:
+        dae = os.path.join(ROOT, "assets", name + ".dae")
+        run([dae, "-w", "64", "-h", "64", "--mode", "dump", "--out", os.path.join(HERE, f"{name}_64x64.scene.ptd")])
+        renders = [(64, 64, 4, 4, 1, 3)]
+        if name == "CBspheres":
+            run([dae, "-w", "128", "-h", "128", "--mode", "dump", "--out",
+                 os.path.join(HERE, f"{name}_128x128.scene.ptd")])
+            renders += [(128, 128, 64, 4, 1, 1), (128, 128, 64, 4, 1, 2)]
+        for w, h, spp, m, l, seed in renders:
+            out = os.path.join(HERE, f"{name}_{w}x{h}_s{spp}_m{m}_l{l}_seed{seed}.hdr.ptd")
+            run([dae, "-w", str(w), "-h", str(h), "-s", str(spp), "-m", str(m), "-l", str(l), "--seed", str(seed),
+                 "--out", out])
+            d = ptdump.read(out)
+            ptdump.write(out, {"hdr": d["hdr"], "shape": d["shape"]})
     # Ray-query KATs on C1: rays from around the box towards random points inside it.
     rng = np.random.default_rng(462)
     n = 2048

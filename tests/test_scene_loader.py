@@ -28,6 +28,16 @@ def test_c1_scene_bit_identical_to_reference(fixture, w, h, cam):
         assert np.array_equal(got[k], ref[k]), k
 
 
+@pytest.mark.parametrize("name", ["CBspheres", "CBspheres_lambertian_pointlight", "CBspheres_lambertian_dirlight",
+                                  "CBspheres_lambertian_ambientlight"])
+def test_bsdf_and_light_variants_bit_identical(name):
+    got = scene_loader.load_dae(os.path.join(ROOT, "assets", name + ".dae"), 64, 64)
+    ref = ptdump.read(golden(f"{name}_64x64.scene.ptd"))
+    assert sorted(got) == sorted(ref)
+    for k in ref:
+        assert np.array_equal(got[k], ref[k]), k
+
+
 @pytest.mark.parametrize("key", ["CBbunny.dae@1024x1024", "CBbunny_sub1.dae@1024x1024", "CBbunny_sub1.dae@1920x1080"])
 def test_bunny_scenes_match_reference_checksums(key):
     want = json.load(open(golden("scene_hashes.json")))[key]
