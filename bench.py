@@ -177,7 +177,9 @@ def main():
                          "kernel": "render_kernel<false>", "kernel_ms": round(avg_ms, 3),
                          "algorithmic_bytes_per_launch": bytes_launch},
             "counters": {k: st_counts[k] for k in ("camera_rays", "bounce_rays", "shadow_rays", "node_visits",
-                                                   "tri_tests", "sphere_tests", "ext_hits")},
+                                                   "tri_tests", "sphere_tests", "ext_hits", "wave_trav_steps",
+                                                   "wave_rounds")},
+            "traversal_simd_efficiency": round(st_counts["node_visits"] / max(1, 64 * st_counts["wave_trav_steps"]), 4),
             "launch": {"grid_blocks": s["grid_blocks"], "block": 64, "blocks_per_cu_query": s["blocks_per_cu"]},
             "image_mean": float(img.mean()),
         }

@@ -31,6 +31,8 @@ def _headers():
 
 
 def up_to_date() -> bool:
+    if os.environ.get("PT_HIPCC_FLAGS"):
+        return False
     if not os.path.exists(LIB):
         return False
     t = os.path.getmtime(LIB)
@@ -55,6 +57,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
                "-Wno-unused-function", f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}", "-c", src, "-o", obj]
+        cmd[1:1] = os.environ.get("PT_HIPCC_FLAGS", "").split()  # experiments, e.g. -DPT_MIN_WAVES_PER_SIMD=5
         if src.endswith(".cpp") and "pt_api" not in src:
             cmd.insert(1, "-xc++")  # host-only translation units
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))

@@ -91,6 +91,7 @@ struct pt_ctx {
   int n_lights = 0;
   int64_t n_prims = 0;
   float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
+  double root_lo_d[3] = {0, 0, 0}, root_hi_d[3] = {0, 0, 0};
   bool have_scene = false, have_cam = false, have_params = false;
   pt_camera cam{};
   pt_params params{};
@@ -116,7 +117,7 @@ int pt_create(int device, pt_ctx** out) {
   HIPCHK(hipEventCreate(&c->ev0));
   HIPCHK(hipEventCreate(&c->ev1));
   HIPCHK(c->counter.reserve(1));
-  HIPCHK(c->stats.reserve(8));
+  HIPCHK(c->stats.reserve(16));
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, device));
   // Persistent grid: as many one-wave workgroups as can be resident.  The
@@ -307,6 +308,8 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
   for (int k = 0; k < 3; ++k) {
     c->root_lo[k] = round_down(N[0].bb_min[k]);
     c->root_hi[k] = round_up(N[0].bb_max[k]);
+    c->root_lo_d[k] = N[0].bb_min[k];
+    c->root_hi_d[k] = N[0].bb_max[k];
   }
   c->have_scene = true;
   return PT_OK;
@@ -344,6 +347,53 @@ static int build_tiles(pt_ctx* c, const pt_tile* tiles, int32_t n, std::vector<i
   return PT_OK;
 }
 
+// Conservative pixel rectangle covering the scene box as seen by the camera.
+// Camera::generate_ray (camera.cpp:113-129) sends every ray of every pixel
+// through the pinhole `pos` with direction c2w * ((fx-.5)W/d, (fy-.5)H/d, -1);
+// a box entirely in front of the pinhole projects inside the rectangle of its
+// 8 projected corners.  Rays start one unit BEHIND the pinhole, so the
+// rectangle is only used when the box lies in front of the pinhole plane;
+// otherwise culling is disabled.  One pixel of margin absorbs rounding.
+static void screen_footprint(const pt_ctx* c, KParams& P) {
+  P.cull_x0 = 0;
+  P.cull_y0 = 0;
+  P.cull_x1 = P.W - 1;
+  P.cull_y1 = P.H - 1;
+  if (std::getenv("PT_NO_FOOTPRINT_CULL")) return;
+  const pt_camera& cam = c->cam;
+  for (int i = 0; i < 3; ++i)  // coordinates by dot products need an orthonormal c2w
+    for (int j = 0; j < 3; ++j) {
+      double dp = 0;
+      for (int r = 0; r < 3; ++r) dp += cam.c2w[3 * r + i] * cam.c2w[3 * r + j];
+      if (std::fabs(dp - (i == j ? 1.0 : 0.0)) > 1e-9) return;
+    }
+  double ax = cam.screen_w / cam.screen_dist, ay = cam.screen_h / cam.screen_dist;
+  double x0 = 1e300, x1 = -1e300, y0 = 1e300, y1 = -1e300;
+  for (int k = 0; k < 8; ++k) {
+    double X[3] = {(k & 1) ? c->root_hi_d[0] : c->root_lo_d[0], (k & 2) ? c->root_hi_d[1] : c->root_lo_d[1],
+                   (k & 4) ? c->root_hi_d[2] : c->root_lo_d[2]};
+    double v[3] = {X[0] - cam.pos[0], X[1] - cam.pos[1], X[2] - cam.pos[2]};
+    double cx = 0, cy = 0, cz = 0;  // coordinates along the c2w columns
+    for (int i = 0; i < 3; ++i) {
+      cx += v[i] * cam.c2w[3 * i + 0];
+      cy += v[i] * cam.c2w[3 * i + 1];
+      cz += v[i] * cam.c2w[3 * i + 2];
+    }
+    double depth = -cz;  // the view direction is -column 2
+    if (!(depth > 1e-6 * (std::fabs(cx) + std::fabs(cy) + 1.0))) return;  // behind / at the pinhole plane
+    double fx = 0.5 + cx / depth / ax, fy = 0.5 + cy / depth / ay;
+    x0 = std::min(x0, fx * P.W);
+    x1 = std::max(x1, fx * P.W);
+    y0 = std::min(y0, fy * P.H);
+    y1 = std::max(y1, fy * P.H);
+  }
+  // pixel x covers [x, x+1) in fx*W
+  P.cull_x0 = (int)std::max(-1.0, std::floor(x0) - 1);
+  P.cull_x1 = (int)std::min((double)P.W, std::floor(x1) + 1);
+  P.cull_y0 = (int)std::max(-1.0, std::floor(y0) - 1);
+  P.cull_y1 = (int)std::min((double)P.H, std::floor(y1) + 1);
+}
+
 static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStream_t s, uint32_t flags) {
   const bool stats = (flags & PT_FLAG_STATS) != 0;
   std::memset(&c->last, 0, sizeof(c->last));
@@ -351,7 +401,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   HIPCHK(c->tiles.reserve(tl.size()));
   HIPCHK(hipMemcpyAsync(c->tiles.p, tl.data(), tl.size() * sizeof(int4), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(c->counter.p, 0, sizeof(uint32_t), s));
-  if (stats) HIPCHK(hipMemsetAsync(c->stats.p, 0, 8 * sizeof(unsigned long long), s));
+  if (stats) HIPCHK(hipMemsetAsync(c->stats.p, 0, 16 * sizeof(unsigned long long), s));
   KParams P;
   std::memset(&P, 0, sizeof(P));
   for (int k = 0; k < 3; ++k) {
@@ -384,6 +434,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     P.root_lo[k] = c->root_lo[k];
     P.root_hi[k] = c->root_hi[k];
   }
+  screen_footprint(c, P);
   P.shade_batch = 64;
   if (const char* sb = std::getenv("PT_SHADE_BATCH")) {  // tuning knob
     int v = std::atoi(sb);
@@ -419,8 +470,8 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags) {
   HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   c->last.last_ms = ms;
   if (flags & PT_FLAG_STATS) {
-    unsigned long long v[8] = {0};
-    HIPCHK(hipMemcpy(v, c->stats.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    unsigned long long v[16] = {0};
+    HIPCHK(hipMemcpy(v, c->stats.p, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     c->last.camera_rays = (int64_t)v[0];
     c->last.bounce_rays = (int64_t)v[1];
     c->last.shadow_rays = (int64_t)v[2];
@@ -428,6 +479,9 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags) {
     c->last.tri_tests = (int64_t)v[4];
     c->last.sphere_tests = (int64_t)v[5];
     c->last.ext_hits = (int64_t)v[6];
+    c->last.wave_trav_steps = (int64_t)v[7];
+    c->last.wave_rounds = (int64_t)v[8];
+    c->last.culled_samples = (int64_t)v[9];
     c->last.counters_valid = 1;
   }
   return PT_OK;

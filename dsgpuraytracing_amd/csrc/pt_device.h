@@ -68,6 +68,7 @@ struct KParams {
   int dbg_pix;                // diagnostic printf trace of one pixel (-1: off)
   int shade_batch;            // leave the traversal phase once this many lanes finished their ray
   float root_lo[3], root_hi[3];  // scene bounds (root box, rounded outward)
+  int cull_x0, cull_y0, cull_x1, cull_y1;  // pixels outside [x0,x1]x[y0,y1] see no geometry
 };
 
 extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, hipStream_t s);

@@ -121,6 +121,54 @@ __device__ __forceinline__ void trav_init(Trav& tr, float3 o, float3 d, float tm
   tr.hit.prim = -1;
 }
 
+// Intersection of one primitive; updates the closest hit in `tr`.  Returns
+// true when an occlusion query can stop.
+template <bool STATS>
+__device__ __forceinline__ bool prim_test(const float4 v0, const float4 e1, const float4 e2, int pi, Trav& tr,
+                                          Counters& ct) {
+  const float3 o = tr.o, d = tr.d;
+  const int meta = __float_as_int(v0.w);
+  float t, u = 0.0f, v = 0.0f;
+  if (meta & 1) {  // triangle: Moller-Trumbore; u,v >= 0, u+v <= 1, 0 < t < tmax
+    if (STATS) ct.tris++;
+    float3 E1 = f3(e1.x, e1.y, e1.z), E2 = f3(e2.x, e2.y, e2.z);
+    float3 pv = cross(d, E2);
+    float det = dot(E1, pv);
+    if (det == 0.0f) return false;
+    float id = 1.0f / det;
+    float3 tv = o - f3(v0.x, v0.y, v0.z);
+    u = dot(tv, pv) * id;
+    float3 qv = cross(tv, E1);
+    v = dot(d, qv) * id;
+    t = dot(E2, qv) * id;
+    if (!(u >= 0.0f && v >= 0.0f && u + v <= 1.0f)) return false;
+  } else {  // sphere, cancellation-free roots (Haines et al., Ray Tracing Gems ch.7)
+    if (STATS) ct.spheres++;
+    float3 fo = o - f3(v0.x, v0.y, v0.z);
+    float bq = dot(fo, d);
+    float3 lp = fo - d * bq;
+    float disc = e1.y - dot(lp, lp);
+    if (disc < 0.0f) return false;
+    float q = -bq - copysignf(sqrtf(disc), bq);
+    if (q == 0.0f) return false;
+    float ta = (dot(fo, fo) - e1.y) / q, tb = q;
+    float t1 = fminf(ta, tb), t2 = fmaxf(ta, tb);
+    // nearest: nearer root unless behind the origin (sphere.cpp:47-77);
+    // occlusion: the far root, as Sphere::intersect(r)'s aliased test (sphere.cpp:37-45)
+    t = (t1 > 0.0f && !tr.any) ? t1 : t2;
+  }
+  if (t > 0.0f && t < tr.tmax) {
+    tr.tmax = t;
+    tr.hit.t = t;
+    tr.hit.u = u;
+    tr.hit.v = v;
+    tr.hit.prim = pi;
+    tr.found = true;
+    return tr.any;
+  }
+  return false;
+}
+
 // One traversal step: fetch one node (both child boxes), intersect the
 // primitives of leaf children in place, then descend / push / pop.  Returns
 // true when the query is complete.  Semantics: nearest hit (bvh.cpp:227-279,
@@ -136,7 +184,7 @@ __device__ __forceinline__ bool trav_step(const DNode* __restrict__ nodes, const
   const float4 c = nodes[tr.node].c;
   const int4 e = nodes[tr.node].e;
   if (STATS) ct.nodes++;
-  const float3 o = tr.o, d = tr.d, inv = tr.inv;
+  const float3 o = tr.o, inv = tr.inv;
   const float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
   float l0x = fmaf(a.x, inv.x, -oi.x), h0x = fmaf(a.y, inv.x, -oi.x);
   float l0y = fmaf(a.z, inv.y, -oi.y), h0y = fmaf(a.w, inv.y, -oi.y);
@@ -150,57 +198,19 @@ __device__ __forceinline__ bool trav_step(const DNode* __restrict__ nodes, const
   float tf1 = fminf(fminf(fmaxf(l1x, h1x), fmaxf(l1y, h1y)), fminf(fmaxf(l1z, h1z), tr.tmax)) * kRobust;
   bool hit0 = tn0 <= tf0;
   bool hit1 = tn1 <= tf1;
-  // Leaf children: intersect their primitives now.
-  for (int side = 0; side < 2; ++side) {
-    bool h = side == 0 ? hit0 : hit1;
-    int cnt = side == 0 ? e.z : e.w;
-    if (!(h && cnt > 0)) continue;
-    int start = side == 0 ? e.x : e.y;
-    for (int k = 0; k < cnt; ++k) {
-      const int pi = start + k;
-      const float4 v0 = prims[pi].v0;
-      const float4 e1 = prims[pi].e1;
-      const int meta = __float_as_int(v0.w);
-      float t, u = 0.0f, v = 0.0f;
-      if (meta & 1) {  // triangle: Moller-Trumbore; u,v >= 0, u+v <= 1, 0 < t < tmax
-        if (STATS) ct.tris++;
-        const float4 e2 = prims[pi].e2;
-        float3 E1 = f3(e1.x, e1.y, e1.z), E2 = f3(e2.x, e2.y, e2.z);
-        float3 pv = cross(d, E2);
-        float det = dot(E1, pv);
-        if (det == 0.0f) continue;
-        float id = 1.0f / det;
-        float3 tv = o - f3(v0.x, v0.y, v0.z);
-        u = dot(tv, pv) * id;
-        float3 qv = cross(tv, E1);
-        v = dot(d, qv) * id;
-        t = dot(E2, qv) * id;
-        if (!(u >= 0.0f && v >= 0.0f && u + v <= 1.0f)) continue;
-      } else {  // sphere, cancellation-free roots (Haines et al., Ray Tracing Gems ch.7)
-        if (STATS) ct.spheres++;
-        float3 fo = o - f3(v0.x, v0.y, v0.z);
-        float bq = dot(fo, d);
-        float3 lp = fo - d * bq;
-        float disc = e1.y - dot(lp, lp);
-        if (disc < 0.0f) continue;
-        float q = -bq - copysignf(sqrtf(disc), bq);
-        if (q == 0.0f) continue;
-        float ta = (dot(fo, fo) - e1.y) / q, tb = q;
-        float t1 = fminf(ta, tb), t2 = fmaxf(ta, tb);
-        // nearest: nearer root unless behind the origin (sphere.cpp:47-77);
-        // occlusion: the far root, as Sphere::intersect(r)'s aliased test (sphere.cpp:37-45)
-        t = (t1 > 0.0f && !tr.any) ? t1 : t2;
-      }
-      if (t > 0.0f && t < tr.tmax) {
-        tr.tmax = t;
-        tr.hit.t = t;
-        tr.hit.u = u;
-        tr.hit.v = v;
-        tr.hit.prim = pi;
-        tr.found = true;
-        if (tr.any) return true;
-      }
-    }
+  // Leaf children: intersect their primitives now, two at a time with all six
+  // 16-B loads issued together (one memory round trip per pair).
+  const bool leaf0 = hit0 && e.z > 0, leaf1 = hit1 && e.w > 0;
+  const int c0 = leaf0 ? e.z : 0;
+  const int total = c0 + (leaf1 ? e.w : 0);
+  for (int k = 0; k < total; k += 2) {
+    const int pa = k < c0 ? e.x + k : e.y + (k - c0);
+    const bool two = k + 1 < total;
+    const int pb = !two ? pa : (k + 1 < c0 ? e.x + k + 1 : e.y + (k + 1 - c0));
+    const float4 a0 = prims[pa].v0, a1 = prims[pa].e1, a2 = prims[pa].e2;
+    const float4 b0 = prims[pb].v0, b1 = prims[pb].e1, b2 = prims[pb].e2;
+    if (prim_test<STATS>(a0, a1, a2, pa, tr, ct)) return true;
+    if (two && prim_test<STATS>(b0, b1, b2, pb, tr, ct)) return true;
   }
   bool in0 = hit0 && e.z == 0 && tn0 <= tr.tmax;
   bool in1 = hit1 && e.w == 0 && tn1 <= tr.tmax;
@@ -248,8 +258,11 @@ __device__ __forceinline__ bool box_hit(const Trav& tr, const float* lo, const f
 enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 
 // DBG: diagnostic build that printf-traces the pixel P.dbg_pix (PT_DEBUG_PIXEL=x,y)
+#ifndef PT_MIN_WAVES_PER_SIMD
+#define PT_MIN_WAVES_PER_SIMD 4
+#endif
 template <bool STATS, bool DBG>
-__global__ __launch_bounds__(PT_BLOCK) void render_kernel(KParams P) {
+__global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel(KParams P) {
   __shared__ int s_stack[PT_STACK * PT_BLOCK];
   int* stk = s_stack + threadIdx.x;
   const int lane = threadIdx.x & 63;
@@ -273,6 +286,8 @@ __global__ __launch_bounds__(PT_BLOCK) void render_kernel(KParams P) {
   trav_init(tr, f3(0, 0, 0), f3(0, 0, 1), 0.0f, false);
   Counters ct = {0, 0, 0};
   uint32_t n_cam = 0, n_bounce = 0, n_shadow = 0, n_hits = 0;
+  uint32_t n_titer = 0, n_rounds = 0;  // wave-level traversal steps / shading rounds (lane 0)
+  uint32_t n_culled = 0;               // samples of pixels outside the scene's screen footprint
 
   const uint32_t total_slots = (uint32_t)P.n_tiles * 1024u;
   const float inv_spp = (float)(1.0 / (double)P.spp);
@@ -506,6 +521,17 @@ __global__ __launch_bounds__(PT_BLOCK) void render_kernel(KParams P) {
               sample = 0;
               acc = f3(0, 0, 0);
               mode = M_CAMERA;
+              // Every ray of this pixel passes through the pinhole; if the
+              // pixel lies outside the scene box's conservative screen
+              // footprint, every sample misses the root box (zero radiance).
+              if (x < P.cull_x0 || x > P.cull_x1 || y < P.cull_y0 || y > P.cull_y1) {
+                float* o = P.out + 3 * (size_t)pix;
+                o[0] = 0.0f;
+                o[1] = 0.0f;
+                o[2] = 0.0f;
+                if (STATS) n_culled += P.spp;
+                mode = M_FETCH;
+              }
             }
           }
         }
@@ -550,7 +576,9 @@ __global__ __launch_bounds__(PT_BLOCK) void render_kernel(KParams P) {
     // lanes have finished their ray, so finished lanes are refilled together
     // (coherent shading) while the others keep their traversal state.
     if (__ballot(mode == M_TRAV) == 0ull) break;  // every lane is M_DONE
+    if (STATS) n_rounds += lane == 0;
     for (;;) {
+      if (STATS) n_titer += lane == 0;
       if (mode == M_TRAV && trav_step<STATS>(P.nodes, P.prims, stk, PT_BLOCK, tr, ct)) mode = M_SHADE;
       unsigned long long ready = __ballot(mode == M_SHADE);
       unsigned long long busy = __ballot(mode == M_TRAV);
@@ -559,8 +587,9 @@ __global__ __launch_bounds__(PT_BLOCK) void render_kernel(KParams P) {
   }
 
   if (STATS) {
-    unsigned long long v[7] = {n_cam, n_bounce, n_shadow, ct.nodes, ct.tris, ct.spheres, n_hits};
-    for (int k = 0; k < 7; ++k) {
+    unsigned long long v[10] = {n_cam, n_bounce, n_shadow, ct.nodes, ct.tris, ct.spheres, n_hits, n_titer, n_rounds,
+                                n_culled};
+    for (int k = 0; k < 10; ++k) {
       unsigned long long s = v[k];
       for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
       if (lane == 0) atomicAdd(P.stats + k, s);

@@ -81,7 +81,8 @@ class pt_stats(ctypes.Structure):
                 ("bounce_rays", c_int64), ("shadow_rays", c_int64), ("node_visits", c_int64),
                 ("tri_tests", c_int64), ("sphere_tests", c_int64), ("ext_hits", c_int64),
                 ("last_ms", c_double), ("counters_valid", c_int32), ("grid_blocks", c_int32),
-                ("blocks_per_cu", c_int32)]
+                ("blocks_per_cu", c_int32), ("wave_trav_steps", c_int64), ("wave_rounds", c_int64),
+                ("culled_samples", c_int64)]
 
 
 # Every symbol include/ptgpu.h and include/ptgpu_scene.h declare, with ctypes signatures.

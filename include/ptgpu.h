@@ -156,6 +156,9 @@ typedef struct pt_stats {
   int32_t counters_valid; /* 1 if the last call ran with PT_FLAG_STATS */
   int32_t grid_blocks;    /* persistent workgroups launched (PT_BLOCK lanes each) */
   int32_t blocks_per_cu;  /* resident workgroups per CU the occupancy query allows */
+  int64_t wave_trav_steps; /* wave-level traversal steps (SIMD efficiency = node_visits / (64 * this)) */
+  int64_t wave_rounds;     /* wave-level shading/refill rounds */
+  int64_t culled_samples;  /* samples of pixels outside the scene's screen footprint (radiance 0, not traced) */
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */

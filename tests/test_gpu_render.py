@@ -116,6 +116,20 @@ def test_hip_deterministic_and_tile_assignment_independent():
     assert (one[:64] == 0).all()
 
 
+@pytest.mark.parametrize("scene,w,h", [("c1_default_128x128", 128, 128), ("c1_sphcam_96x64", 96, 64),
+                                       ("CBspheres_64x64", 64, 64)])
+def test_screen_footprint_culling_is_exact(monkeypatch, scene, w, h):
+    """Pixels outside the scene box's projected footprint are written as 0
+    without tracing: identical to tracing every sample."""
+    a, st = gpu_render(scene, w, h, 4, seed=21, stats=True)
+    monkeypatch.setenv("PT_NO_FOOTPRINT_CULL", "1")
+    b, st2 = gpu_render(scene, w, h, 4, seed=21, stats=True)
+    assert np.array_equal(a, b)
+    assert st2["culled_samples"] == 0
+    if scene == "c1_default_128x128":
+        assert st["culled_samples"] > 0
+
+
 def test_hip_ray_queries_vs_reference_kat():
     rays = ptdump.read(golden("c1_rays.ptd"))
     ref = ptdump.read(golden("c1_rays_ref.ptd"))
@@ -135,7 +149,7 @@ def test_hip_ray_queries_vs_reference_kat():
 def test_hip_stats_counters():
     _, st = gpu_render("c1_default_64x64", 64, 64, 2, stats=True)
     assert st["counters_valid"] == 1
-    assert st["camera_rays"] == 64 * 64 * 2
+    assert st["camera_rays"] + st["culled_samples"] == 64 * 64 * 2
     assert st["pixels"] == 64 * 64 and st["samples"] == 64 * 64 * 2
     assert st["node_visits"] > st["camera_rays"]
     assert st["shadow_rays"] > 0 and st["bounce_rays"] > 0 and st["sphere_tests"] > 0
