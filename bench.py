@@ -30,6 +30,15 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
+# BASELINE.json configs; C3 is the headline (default).
+WORKLOADS = {
+    "c1": dict(scene="c1", w=256, h=256, spp=1, desc="C1 CBspheres_lambertian 256x256 1spp -m 4 -l 1"),
+    "c2": dict(scene="c1", w=512, h=512, spp=16, desc="C2 CBspheres_lambertian 512x512 16spp -m 4 -l 1"),
+    "c3": dict(scene="sub1", w=1024, h=1024, spp=64,
+               desc="C3 CBbunny_sub1 (114,316 tris; CBdragon proxy) 1024x1024 64spp -m 4 -l 1"),
+    "c4": dict(scene="sub1", w=1920, h=1080, spp=256,
+               desc="C4 CBbunny_sub1 (CBdragon proxy) 1920x1080 256spp -m 4 -l 1, tiles over N GPUs"),
+}
 W, H, SPP, DEPTH, NSL, SEED = 1024, 1024, 64, 4, 1, 1
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -64,7 +73,8 @@ def cpu_baseline(scene_dump: str, budget_s: float = 12.0) -> dict:
     at the full 64 spp."""
     from tests.oracle_helpers import Restatement
     rs = Restatement()
-    ntiles = (W // 32) * (H // 32)
+    ntx = (W + 31) // 32
+    ntiles = ntx * ((H + 31) // 32)
     # calibrate on one tile, then size the sample to ~budget_s
     t0 = time.perf_counter()
     rs.render(scene_dump, W, H, SPP, DEPTH, NSL, SEED, rng_mode=0, tile_begin=ntiles // 2, tile_end=ntiles // 2 + 1)
@@ -75,9 +85,10 @@ def cpu_baseline(scene_dump: str, budget_s: float = 12.0) -> dict:
         t0 = time.perf_counter()
         rs.render(scene_dump, W, H, SPP, DEPTH, NSL, SEED, rng_mode=0, tile_begin=ti, tile_end=ti + 1)
         total_t += time.perf_counter() - t0
-        total_px += 32 * 32
+        tx, ty = (ti % ntx) * 32, (ti // ntx) * 32
+        total_px += (min(W, tx + 32) - tx) * (min(H, ty + 32) - ty)
     return {"value": total_px * SPP / total_t / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": f"every {step}th 32x32 tile of the 1024x1024 frame ({total_px} px) at 64 spp, -m 4 -l 1, "
+            "sample": f"every {step}th 32x32 tile of the {W}x{H} frame ({total_px} px) at {SPP} spp, -m 4 -l 1, "
                       f"oracle/restate.cpp glibc-rand mode (== reference -t 1), {total_t:.1f} s"}
 
 
@@ -88,7 +99,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scene-dump", default=None, help="PTDUMP scene instead of the native .dae loader")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     args = ap.parse_args()
+    global W, H, SPP
+    wl = WORKLOADS[args.workload]
+    W, H, SPP = wl["w"], wl["h"], wl["spp"]
 
     import torch
     import torch.distributed as dist
@@ -106,7 +121,7 @@ def main():
         scene = Scene.from_dump(args.scene_dump)
         dump_path = args.scene_dump
     else:
-        dae = scenes.proxy_path(1)
+        dae = scenes.proxy_path(1) if wl["scene"] == "sub1" else scenes.C1_DAE
         scene = Scene.from_dae(dae, W, H)
         dump_path = None
     dev = Device(local)
@@ -156,7 +171,8 @@ def main():
         achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
         img = frame.float().cpu().numpy()
         out = {
-            "metric": "Mrays/sec + wall-clock render time, CBdragon 1024x1024 @ 64 spp",
+            "metric": "Mrays/sec + wall-clock render time, CBdragon 1024x1024 @ 64 spp"
+                      if args.workload == "c3" else f"Mrays/sec + wall-clock render time, {wl['desc']}",
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -168,7 +184,7 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic: deterministic CBbunny_sub1 proxy for the missing CBdragon.dae (SURVEY §8(d))",
-            "config": {"workload": "C3 CBbunny_sub1 (114,316 tris) 1024x1024 64spp -m 4 -l 1, default camera",
+            "config": {"workload": wl["desc"] + ", default camera",
                        "width": W, "height": H, "spp": SPP, "max_ray_depth": DEPTH, "ns_area_light": NSL,
                        "parallelism": f"tiles{world}" if world > 1 else "single",
                        "render_time_s": round(elapsed / frames, 4), "scene_load_s": round(t_load, 3)},
@@ -178,7 +194,9 @@ def main():
                          "algorithmic_bytes_per_launch": bytes_launch},
             "counters": {k: st_counts[k] for k in ("camera_rays", "bounce_rays", "shadow_rays", "node_visits",
                                                    "tri_tests", "sphere_tests", "ext_hits", "wave_trav_steps",
-                                                   "wave_rounds")},
+                                                   "wave_rounds", "culled_samples", "queue_atomics", "shade_clocks",
+                                                   "trav_clocks", "max_wave_clocks", "wave_wall_sum",
+                                                   "wave_wall_max")},
             "traversal_simd_efficiency": round(st_counts["node_visits"] / max(1, 64 * st_counts["wave_trav_steps"]), 4),
             "launch": {"grid_blocks": s["grid_blocks"], "block": 64, "blocks_per_cu_query": s["blocks_per_cu"]},
             "image_mean": float(img.mean()),
@@ -191,8 +209,8 @@ def main():
                 dp = dump_path
                 if dp is None:
                     from dsgpuraytracing_amd import scene_loader
-                    dp = os.path.join(ROOT, "_scenes", "bench_sub1_1024.ptd")
-                    scene_loader.dump_dae(scenes.proxy_path(1), W, H, dp)
+                    dp = os.path.join(ROOT, "_scenes", f"bench_{args.workload}.ptd")
+                    scene_loader.dump_dae(dae, W, H, dp)
                 out["cpu_baseline"] = cpu_baseline(dp)
             except Exception as e:  # reported, never silently replaced
                 out["cpu_baseline"] = {"error": repr(e)}

@@ -76,7 +76,7 @@ float round_up(double x) {
 struct pt_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   DevBuf<DNode> nodes;
   DevBuf<DPrim> prims;
   DevBuf<float> norms;
@@ -84,6 +84,7 @@ struct pt_ctx {
   DevBuf<DLight> lights;
   DevBuf<int4> tiles;
   DevBuf<float> frame;  // device framebuffer for host-output renders
+  DevBuf<float> partial;  // per-slot sample-group sums
   DevBuf<uint32_t> counter;
   DevBuf<unsigned long long> stats;
   DevBuf<float> q_f;    // ray-query scratch
@@ -116,6 +117,7 @@ int pt_create(int device, pt_ctx** out) {
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreate(&c->ev0));
   HIPCHK(hipEventCreate(&c->ev1));
+  HIPCHK(hipEventCreate(&c->ev2));
   HIPCHK(c->counter.reserve(1));
   HIPCHK(c->stats.reserve(16));
   hipDeviceProp_t prop;
@@ -148,6 +150,7 @@ int pt_destroy(pt_ctx* c) {
   c->q_i.release();
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ev2) (void)hipEventDestroy(c->ev2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return PT_OK;
@@ -444,17 +447,37 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     int dx = -1, dy = -1;
     if (std::sscanf(dp, "%d,%d", &dx, &dy) == 2 && dx >= 0 && dy >= 0 && dx < P.W && dy < P.H) P.dbg_pix = dx + dy * P.W;
   }
-  int64_t slots = (int64_t)tl.size() * 1024;
-  int64_t max_grid = (slots + PT_BLOCK - 1) / PT_BLOCK;
+  // Work slots are (pixel, group of group_spp samples): small enough that
+  // the dynamic queue balances the waves (a whole pixel per slot left the
+  // launch waiting on a few waves holding 64-sample pixels).
   int64_t want = stats ? c->grid_stats : c->grid_plain;
   if (const char* g = std::getenv("PT_WAVES_PER_CU")) {  // tuning knob
     int w = std::atoi(g);
     if (w > 0) want = (int64_t)w * c->n_cu;
   }
+  P.group_spp = PT_GROUP_SPP;
+  if (const char* g = std::getenv("PT_SAMPLE_GROUP")) {  // tuning knob
+    int v = std::atoi(g);
+    if (v > 0) P.group_spp = v;
+  }
+  P.group_spp = std::min(P.group_spp, P.spp);
+  for (;;) {  // the 32-bit queue head may overshoot by one chunk per wave
+    P.n_groups = (P.spp + P.group_spp - 1) / P.group_spp;
+    int64_t slots = (int64_t)tl.size() * 1024 * P.n_groups;
+    if (slots + want * PT_CHUNK < (int64_t)UINT32_MAX || P.n_groups == 1) break;
+    P.group_spp *= 2;
+  }
+  int64_t slots = (int64_t)tl.size() * 1024 * P.n_groups;
+  if (slots + want * PT_CHUNK >= (int64_t)UINT32_MAX) return fail(PT_E_INVALID, "too many tiles for one launch");
+  HIPCHK(c->partial.reserve((size_t)slots * 3));
+  P.partial = c->partial.p;
+  int64_t max_grid = (slots + PT_BLOCK - 1) / PT_BLOCK;
   int grid = (int)std::min<int64_t>(want, max_grid);
   HIPCHK(hipEventRecord(c->ev0, s));
   HIPCHK(ptk_launch_render(&P, grid, stats, s));
   HIPCHK(hipEventRecord(c->ev1, s));
+  HIPCHK(ptk_launch_resolve(&P, s));
+  HIPCHK(hipEventRecord(c->ev2, s));
   c->last.grid_blocks = grid;
   c->last.blocks_per_cu = stats ? c->bpc_stats : c->bpc_plain;
   int64_t px = 0;
@@ -469,6 +492,8 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags) {
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   c->last.last_ms = ms;
+  HIPCHK(hipEventElapsedTime(&ms, c->ev1, c->ev2));
+  c->last.resolve_ms = ms;
   if (flags & PT_FLAG_STATS) {
     unsigned long long v[16] = {0};
     HIPCHK(hipMemcpy(v, c->stats.p, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
@@ -482,6 +507,12 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags) {
     c->last.wave_trav_steps = (int64_t)v[7];
     c->last.wave_rounds = (int64_t)v[8];
     c->last.culled_samples = (int64_t)v[9];
+    c->last.queue_atomics = (int64_t)v[10];
+    c->last.shade_clocks = (int64_t)v[11];
+    c->last.trav_clocks = (int64_t)v[12];
+    c->last.max_wave_clocks = (int64_t)v[13];
+    c->last.wave_wall_sum = (int64_t)v[14];
+    c->last.wave_wall_max = (int64_t)v[15];
     c->last.counters_valid = 1;
   }
   return PT_OK;

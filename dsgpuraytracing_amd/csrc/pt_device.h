@@ -7,6 +7,13 @@
 #ifndef PT_BLOCK
 #define PT_BLOCK 64  // one wave64 per workgroup: the persistent queue is per wave
 #endif
+#ifndef PT_CHUNK
+#define PT_CHUNK 64  // work slots (pixels) a wave takes from the queue per atomic
+#endif
+static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand");
+#ifndef PT_GROUP_SPP
+#define PT_GROUP_SPP 8  // default samples per work slot
+#endif
 #ifndef PT_STACK
 #define PT_STACK 32  // traversal stack entries per lane (LDS, lane-contiguous)
 #endif
@@ -55,7 +62,9 @@ struct KParams {
   int W, H, spp, max_depth, ns_area;
   uint32_t seed;
   int n_lights;
-  int n_tiles;  // 32x32 (or smaller) tiles: 1024 work slots each
+  int n_tiles;     // 32x32 (or smaller) tiles: 1024 pixels each
+  int group_spp;   // samples per work slot (a slot is one pixel's sample group)
+  int n_groups;    // ceil(spp / group_spp): slots per pixel
   const DNode* nodes;
   const DPrim* prims;
   const float* norms;  // 9 floats per primitive (vertex normals n1,n2,n3)
@@ -63,6 +72,7 @@ struct KParams {
   const DLight* lights;
   const int4* tiles;  // (x, y, w, h)
   float* out;         // W*H*3
+  float* partial;     // 3 floats per slot: the slot's sample sum, resolved into `out` in group order
   uint32_t* work_counter;
   unsigned long long* stats;  // 7 counters (PT_FLAG_STATS)
   int dbg_pix;                // diagnostic printf trace of one pixel (-1: off)
@@ -72,6 +82,7 @@ struct KParams {
 };
 
 extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, hipStream_t s);
+extern "C" hipError_t ptk_launch_resolve(const KParams* P, hipStream_t s);
 extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prims, const float* o, const float* d,
                                            const float* maxt, int64_t n, int32_t* hit, float* t, int32_t* prim,
                                            int32_t* anyhit, hipStream_t s);

@@ -46,6 +46,26 @@ __device__ __forceinline__ float3 cross(float3 u, float3 v) {
 __device__ __forceinline__ float3 normalize(float3 v) { return v * (1.0f / sqrtf(dot(v, v))); }
 __device__ __forceinline__ float illum(float3 s) { return 0.2126f * s.x + 0.7152f * s.y + 0.0722f * s.z; }
 __device__ __forceinline__ float3 ld3(const float* p) { return f3(p[0], p[1], p[2]); }
+__device__ __forceinline__ void store3(float* p, float3 v) {
+  p[0] = v.x;
+  p[1] = v.y;
+  p[2] = v.z;
+}
+
+// Pixel q (0..1023) of a tile in 8x8 blocks (4 blocks per row); (-1,-1) when
+// it lies outside a ragged tile.
+__device__ __forceinline__ int2 tile_pixel(int4 tile, uint32_t q) {
+  uint32_t blk = q >> 6, w = q & 63u;
+  int x = tile.x + (int)((blk & 3u) * 8u + (w & 7u));
+  int y = tile.y + (int)((blk >> 2) * 8u + (w >> 3));
+  if (x >= tile.x + tile.z || y >= tile.y + tile.w) return make_int2(-1, -1);
+  return make_int2(x, y);
+}
+
+// The pixel lies outside the scene box's conservative screen footprint.
+__device__ __forceinline__ bool culled(const KParams& P, int x, int y) {
+  return x < P.cull_x0 || x > P.cull_x1 || y < P.cull_y0 || y > P.cull_y1;
+}
 
 // Integer-ulp offset of p along n (n points to the side the new ray leaves on).
 __device__ __forceinline__ float3 offset_ray(float3 p, float3 n) {
@@ -270,7 +290,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // ---- per-lane state
   int mode = M_FETCH;
   bool shadow = false;  // the ray in flight is a shadow ray
-  int pix = 0, px = 0, py = 0, sample = 0;
+  int pix = 0, px = 0, py = 0, sample = 0, s_end = 0;
+  uint32_t wslot = 0;  // the work slot (pixel, sample group) this lane renders
   uint32_t rbase = 0, rdim = 0;
   float3 acc = f3(0, 0, 0);  // pixel sum over samples, in sample order
   float3 L = f3(0, 0, 0);    // radiance of the current sample
@@ -288,9 +309,14 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   uint32_t n_cam = 0, n_bounce = 0, n_shadow = 0, n_hits = 0;
   uint32_t n_titer = 0, n_rounds = 0;  // wave-level traversal steps / shading rounds (lane 0)
   uint32_t n_culled = 0;               // samples of pixels outside the scene's screen footprint
+  uint32_t n_atomics = 0;              // work-queue atomics (lane 0)
+  uint32_t chunk_next = 0, chunk_end = 0;  // the wave's private range of work slots
+  unsigned long long cyc_shade = 0, cyc_trav = 0;  // shader clocks per phase (lane 0)
+  unsigned long long t_mark = STATS ? clock64() : 0ull;
+  const unsigned long long w_start = STATS ? wall_clock64() : 0ull;
 
-  const uint32_t total_slots = (uint32_t)P.n_tiles * 1024u;
-  const float inv_spp = (float)(1.0 / (double)P.spp);
+  const uint32_t n_groups = (uint32_t)P.n_groups;
+  const uint32_t total_slots = (uint32_t)P.n_tiles * 1024u * n_groups;
   const int batch = P.shade_batch;
 
   for (;;) {
@@ -479,13 +505,10 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       if (finish) {
         acc = acc + L;
         ++sample;
-        if (sample < P.spp) {
+        if (sample < s_end) {
           mode = M_CAMERA;
         } else {
-          float* o = P.out + 3 * (size_t)pix;
-          o[0] = acc.x * inv_spp;
-          o[1] = acc.y * inv_spp;
-          o[2] = acc.z * inv_spp;
+          store3(P.partial + 3 * (size_t)wslot, acc);
           mode = M_FETCH;
         }
       }
@@ -499,41 +522,53 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       bool need = mode == M_FETCH;
       unsigned long long m = __ballot(need);
       if (m != 0ull) {
-        int cnt = __popcll(m);
-        int leader = __ffsll((long long)m) - 1;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(P.work_counter, (uint32_t)cnt);
-        base = __shfl(base, leader);
+        // Lanes are served from the wave's private chunk of consecutive slots;
+        // one atomic refills it with PT_CHUNK slots (keeps the queue head off
+        // the critical path: ~1 atomic per PT_CHUNK pixels).
+        uint32_t cnt = (uint32_t)__popcll(m);
+        uint32_t avail = chunk_end - chunk_next;
+        uint32_t nbase = 0;
+        if (cnt > avail) {
+          if (lane == 0) nbase = atomicAdd(P.work_counter, (uint32_t)PT_CHUNK);
+          nbase = __shfl(nbase, 0);
+          if (STATS) n_atomics += lane == 0;
+        }
         if (need) {
-          uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+          uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+          uint32_t slot = rank < avail ? chunk_next + rank : nbase + (rank - avail);
           if (slot >= total_slots) {
             mode = M_DONE;
           } else {
-            int4 tile = P.tiles[slot >> 10];
-            uint32_t off = slot & 1023u;
-            uint32_t blk = off >> 6, w = off & 63u;
-            int x = tile.x + (int)((blk & 3u) * 8u + (w & 7u));
-            int y = tile.y + (int)((blk >> 2) * 8u + (w >> 3));
-            if (x < tile.x + tile.z && y < tile.y + tile.w) {
-              px = x;
-              py = y;
-              pix = x + y * P.W;
-              sample = 0;
+            // slot = (tile * 1024 + pixel-in-tile) * n_groups + group: the
+            // groups of one pixel sit on neighbouring lanes (coherent rays)
+            uint32_t tq = slot / n_groups;
+            uint32_t g = slot - tq * n_groups;
+            int2 xy = tile_pixel(P.tiles[tq >> 10], tq & 1023u);
+            if (xy.x >= 0) {
+              px = xy.x;
+              py = xy.y;
+              pix = px + py * P.W;
+              sample = (int)g * P.group_spp;
+              s_end = min(P.spp, sample + P.group_spp);
+              wslot = slot;
               acc = f3(0, 0, 0);
               mode = M_CAMERA;
               // Every ray of this pixel passes through the pinhole; if the
               // pixel lies outside the scene box's conservative screen
-              // footprint, every sample misses the root box (zero radiance).
-              if (x < P.cull_x0 || x > P.cull_x1 || y < P.cull_y0 || y > P.cull_y1) {
-                float* o = P.out + 3 * (size_t)pix;
-                o[0] = 0.0f;
-                o[1] = 0.0f;
-                o[2] = 0.0f;
-                if (STATS) n_culled += P.spp;
+              // footprint, every sample misses the root box (zero radiance,
+              // written by resolve_kernel).
+              if (culled(P, px, py)) {
+                if (STATS) n_culled += s_end - sample;
                 mode = M_FETCH;
               }
             }
           }
+        }
+        if (cnt > avail) {  // wave-uniform
+          chunk_next = nbase + (cnt - avail);
+          chunk_end = nbase + PT_CHUNK;
+        } else {
+          chunk_next += cnt;
         }
       }
       // ---- camera rays: Camera::generate_ray (camera.cpp:113-129) at the
@@ -561,11 +596,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           break;
         }
         // miss: the sample contributes 0
-        if (++sample >= P.spp) {
-          float* o = P.out + 3 * (size_t)pix;
-          o[0] = acc.x * inv_spp;
-          o[1] = acc.y * inv_spp;
-          o[2] = acc.z * inv_spp;
+        if (++sample >= s_end) {
+          store3(P.partial + 3 * (size_t)wslot, acc);
           mode = M_FETCH;
         }
       }
@@ -576,7 +608,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     // lanes have finished their ray, so finished lanes are refilled together
     // (coherent shading) while the others keep their traversal state.
     if (__ballot(mode == M_TRAV) == 0ull) break;  // every lane is M_DONE
-    if (STATS) n_rounds += lane == 0;
+    if (STATS) {
+      n_rounds += lane == 0;
+      unsigned long long t = clock64();
+      cyc_shade += lane == 0 ? t - t_mark : 0ull;
+      t_mark = t;
+    }
     for (;;) {
       if (STATS) n_titer += lane == 0;
       if (mode == M_TRAV && trav_step<STATS>(P.nodes, P.prims, stk, PT_BLOCK, tr, ct)) mode = M_SHADE;
@@ -584,17 +621,46 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       unsigned long long busy = __ballot(mode == M_TRAV);
       if (busy == 0ull || __popcll(ready) >= batch) break;
     }
+    if (STATS) {
+      unsigned long long t = clock64();
+      cyc_trav += lane == 0 ? t - t_mark : 0ull;
+      t_mark = t;
+    }
   }
 
   if (STATS) {
-    unsigned long long v[10] = {n_cam, n_bounce, n_shadow, ct.nodes, ct.tris, ct.spheres, n_hits, n_titer, n_rounds,
-                                n_culled};
-    for (int k = 0; k < 10; ++k) {
+    unsigned long long v[13] = {n_cam,   n_bounce, n_shadow,  ct.nodes,  ct.tris,  ct.spheres, n_hits,
+                                n_titer, n_rounds, n_culled, n_atomics, cyc_shade, cyc_trav};
+    for (int k = 0; k < 13; ++k) {
       unsigned long long s = v[k];
       for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
       if (lane == 0) atomicAdd(P.stats + k, s);
     }
+    // load balance: the slowest wave bounds the launch
+    if (lane == 0) {
+      unsigned long long w = wall_clock64() - w_start;
+      atomicMax(P.stats + 13, cyc_shade + cyc_trav);
+      atomicAdd(P.stats + 14, w);
+      atomicMax(P.stats + 15, w);
+    }
   }
+}
+
+// Sums each pixel's sample groups in group order (so the sum is a fixed
+// function of the pixel, independent of scheduling) and writes the pixel's
+// average, SampleBuffer-style (pathtracer.cpp:577-581).  One lane per pixel.
+__global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
+  const uint32_t tq = blockIdx.x * 256u + threadIdx.x;
+  if (tq >= (uint32_t)P.n_tiles * 1024u) return;
+  int2 xy = tile_pixel(P.tiles[tq >> 10], tq & 1023u);
+  if (xy.x < 0) return;
+  float3 acc = f3(0, 0, 0);
+  if (!culled(P, xy.x, xy.y)) {
+    const float* p = P.partial + 3 * (size_t)tq * (size_t)P.n_groups;
+    for (int g = 0; g < P.n_groups; ++g) acc = acc + ld3(p + 3 * g);
+  }
+  const float inv_spp = (float)(1.0 / (double)P.spp);
+  store3(P.out + 3 * ((size_t)xy.x + (size_t)xy.y * (size_t)P.W), acc * inv_spp);
 }
 
 // Batched BVHAccel::intersect queries, one lane per ray.
@@ -633,6 +699,12 @@ extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, 
     hipLaunchKernelGGL((ptk::render_kernel<true, false>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
   else
     hipLaunchKernelGGL((ptk::render_kernel<false, false>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ptk_launch_resolve(const KParams* P, hipStream_t s) {
+  int grid = (int)(((int64_t)P->n_tiles * 1024 + 255) / 256);
+  hipLaunchKernelGGL(ptk::resolve_kernel, dim3(grid), dim3(256), 0, s, *P);
   return hipGetLastError();
 }
 

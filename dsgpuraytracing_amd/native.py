@@ -82,7 +82,10 @@ class pt_stats(ctypes.Structure):
                 ("tri_tests", c_int64), ("sphere_tests", c_int64), ("ext_hits", c_int64),
                 ("last_ms", c_double), ("counters_valid", c_int32), ("grid_blocks", c_int32),
                 ("blocks_per_cu", c_int32), ("wave_trav_steps", c_int64), ("wave_rounds", c_int64),
-                ("culled_samples", c_int64)]
+                ("culled_samples", c_int64), ("queue_atomics", c_int64),
+                ("shade_clocks", c_int64), ("trav_clocks", c_int64),
+                ("max_wave_clocks", c_int64), ("wave_wall_sum", c_int64), ("wave_wall_max", c_int64),
+                ("resolve_ms", c_double)]
 
 
 # Every symbol include/ptgpu.h and include/ptgpu_scene.h declare, with ctypes signatures.

@@ -159,6 +159,13 @@ typedef struct pt_stats {
   int64_t wave_trav_steps; /* wave-level traversal steps (SIMD efficiency = node_visits / (64 * this)) */
   int64_t wave_rounds;     /* wave-level shading/refill rounds */
   int64_t culled_samples;  /* samples of pixels outside the scene's screen footprint (radiance 0, not traced) */
+  int64_t queue_atomics;   /* work-queue atomics issued */
+  int64_t shade_clocks;    /* shader clocks summed over waves: refill + shading phases */
+  int64_t trav_clocks;     /* shader clocks summed over waves: traversal phases */
+  int64_t max_wave_clocks; /* shader clocks of the slowest wave */
+  int64_t wave_wall_sum;   /* wave lifetimes summed, device wall-clock ticks */
+  int64_t wave_wall_max;   /* longest wave lifetime, device wall-clock ticks */
+  double resolve_ms;       /* device time of the sample-group resolve kernel */
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */
