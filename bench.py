@@ -108,7 +108,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from dsgpuraytracing_amd.dist import init_from_env, render_sharded
+    from dsgpuraytracing_amd.dist import init_from_env, render_sharded, shard_tiles
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     rank, world, local = init_from_env("nccl")
@@ -134,8 +134,10 @@ def main():
     frame = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{local}")
     stream = torch.cuda.current_stream().cuda_stream
 
-    def step(stats=False):
-        render_sharded(lambda mine: dev.render_tiles_device(mine, frame.data_ptr(), stream, stats=stats),
+    mine_arr = np.asarray(shard_tiles(tiles, rank, world), dtype=np.int32).reshape(-1, 4)
+
+    def step(stats=False):  # render_sharded deals the same tiles to this rank every step
+        render_sharded(lambda mine: dev.render_tiles_device(mine_arr, frame.data_ptr(), stream, stats=stats),
                        frame, tiles, rank, world)
         return dev.stats()
 
@@ -147,13 +149,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms = []
+    kernel_ms, resolve_ms = [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         if world > 1:
             frame.zero_()  # the reduce sums whole frames: non-owned tiles must be +0.0
         s = step()
         kernel_ms.append(s["last_ms"])
+        resolve_ms.append(s["resolve_ms"])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -191,12 +194,13 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": measured_traffic(),
                          "kernel": "render_kernel<false>", "kernel_ms": round(avg_ms, 3),
+                         "resolve_ms": round(float(np.mean(resolve_ms)), 4),
                          "algorithmic_bytes_per_launch": bytes_launch},
             "counters": {k: st_counts[k] for k in ("camera_rays", "bounce_rays", "shadow_rays", "node_visits",
                                                    "tri_tests", "sphere_tests", "ext_hits", "wave_trav_steps",
                                                    "wave_rounds", "culled_samples", "queue_atomics", "shade_clocks",
                                                    "trav_clocks", "max_wave_clocks", "wave_wall_sum",
-                                                   "wave_wall_max")},
+                                                   "wave_wall_max", "hitshade_clocks")},
             "traversal_simd_efficiency": round(st_counts["node_visits"] / max(1, 64 * st_counts["wave_trav_steps"]), 4),
             "launch": {"grid_blocks": s["grid_blocks"], "block": 64, "blocks_per_cu_query": s["blocks_per_cu"]},
             "image_mean": float(img.mean()),

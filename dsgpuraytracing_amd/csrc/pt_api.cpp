@@ -83,13 +83,17 @@ struct pt_ctx {
   DevBuf<DBsdf> bsdfs;
   DevBuf<DLight> lights;
   DevBuf<int4> tiles;
+  std::vector<int4> tiles_host;  // what `tiles` holds
+  DevBuf<int4> blocks;           // footprint-clipped 8x8 pixel blocks of the tiles
+  std::vector<int4> blocks_host;
+  int64_t culled_px = 0;         // pixels of the last launch outside the footprint
   DevBuf<float> frame;  // device framebuffer for host-output renders
   DevBuf<float> partial;  // per-slot sample-group sums
   DevBuf<uint32_t> counter;
   DevBuf<unsigned long long> stats;
   DevBuf<float> q_f;    // ray-query scratch
   DevBuf<int32_t> q_i;
-  int n_lights = 0;
+  int n_lights = 0, n_bsdfs = 0;
   int64_t n_prims = 0;
   float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
   double root_lo_d[3] = {0, 0, 0}, root_hi_d[3] = {0, 0, 0};
@@ -119,7 +123,7 @@ int pt_create(int device, pt_ctx** out) {
   HIPCHK(hipEventCreate(&c->ev1));
   HIPCHK(hipEventCreate(&c->ev2));
   HIPCHK(c->counter.reserve(1));
-  HIPCHK(c->stats.reserve(16));
+  HIPCHK(c->stats.reserve(32));
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, device));
   // Persistent grid: as many one-wave workgroups as can be resident.  The
@@ -143,6 +147,7 @@ int pt_destroy(pt_ctx* c) {
   c->bsdfs.release();
   c->lights.release();
   c->tiles.release();
+  c->blocks.release();
   c->frame.release();
   c->counter.release();
   c->stats.release();
@@ -307,6 +312,7 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
   HIPCHK(hipMemcpy(c->bsdfs.p, bs.data(), bs.size() * sizeof(DBsdf), hipMemcpyHostToDevice));
   if (!ls.empty()) HIPCHK(hipMemcpy(c->lights.p, ls.data(), ls.size() * sizeof(DLight), hipMemcpyHostToDevice));
   c->n_lights = (int)ls.size();
+  c->n_bsdfs = (int)bs.size();
   c->n_prims = s->n_prims;
   for (int k = 0; k < 3; ++k) {
     c->root_lo[k] = round_down(N[0].bb_min[k]);
@@ -401,10 +407,16 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   const bool stats = (flags & PT_FLAG_STATS) != 0;
   std::memset(&c->last, 0, sizeof(c->last));
   if (tl.empty()) return PT_OK;
-  HIPCHK(c->tiles.reserve(tl.size()));
-  HIPCHK(hipMemcpyAsync(c->tiles.p, tl.data(), tl.size() * sizeof(int4), hipMemcpyHostToDevice, s));
+  // the tile list rarely changes between frames: upload it only when it does
+  if (tl.size() != c->tiles_host.size() ||
+      std::memcmp(tl.data(), c->tiles_host.data(), tl.size() * sizeof(int4)) != 0) {
+    c->tiles_host.clear();
+    HIPCHK(c->tiles.reserve(tl.size()));
+    HIPCHK(hipMemcpyAsync(c->tiles.p, tl.data(), tl.size() * sizeof(int4), hipMemcpyHostToDevice, s));
+    c->tiles_host = tl;
+  }
   HIPCHK(hipMemsetAsync(c->counter.p, 0, sizeof(uint32_t), s));
-  if (stats) HIPCHK(hipMemsetAsync(c->stats.p, 0, 16 * sizeof(unsigned long long), s));
+  if (stats) HIPCHK(hipMemsetAsync(c->stats.p, 0, 32 * sizeof(unsigned long long), s));
   KParams P;
   std::memset(&P, 0, sizeof(P));
   for (int k = 0; k < 3; ++k) {
@@ -422,6 +434,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.ns_area = c->params.ns_area_light;
   P.seed = c->params.seed;
   P.n_lights = c->n_lights;
+  P.n_bsdfs = c->n_bsdfs;
   P.n_tiles = (int)tl.size();
   P.nodes = c->nodes.p;
   P.prims = c->prims.p;
@@ -438,7 +451,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     P.root_hi[k] = c->root_hi[k];
   }
   screen_footprint(c, P);
-  P.shade_batch = 64;
+  P.shade_batch = PT_SHADE_BATCH;
   if (const char* sb = std::getenv("PT_SHADE_BATCH")) {  // tuning knob
     int v = std::atoi(sb);
     if (v >= 1 && v <= 64) P.shade_batch = v;
@@ -447,6 +460,30 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     int dx = -1, dy = -1;
     if (std::sscanf(dp, "%d,%d", &dx, &dy) == 2 && dx >= 0 && dy >= 0 && dx < P.W && dy < P.H) P.dbg_pix = dx + dy * P.W;
   }
+  // Render blocks: <= 8x8 rectangles of each tile clipped to the footprint.
+  std::vector<int4> bl;
+  int64_t px_in = 0, px_all = 0;
+  for (const int4& t : tl) {
+    px_all += (int64_t)t.z * t.w;
+    int x0 = std::max(t.x, P.cull_x0), x1 = std::min(t.x + t.z - 1, P.cull_x1);
+    int y0 = std::max(t.y, P.cull_y0), y1 = std::min(t.y + t.w - 1, P.cull_y1);
+    for (int by = y0; by <= y1; by += 8)
+      for (int bx = x0; bx <= x1; bx += 8) {
+        bl.push_back(make_int4(bx, by, std::min(8, x1 - bx + 1), std::min(8, y1 - by + 1)));
+        px_in += (int64_t)bl.back().z * bl.back().w;
+      }
+  }
+  c->culled_px = px_all - px_in;
+  if (bl.size() != c->blocks_host.size() ||
+      std::memcmp(bl.data(), c->blocks_host.data(), bl.size() * sizeof(int4)) != 0) {
+    c->blocks_host.clear();
+    HIPCHK(c->blocks.reserve(bl.size()));
+    if (!bl.empty())
+      HIPCHK(hipMemcpyAsync(c->blocks.p, bl.data(), bl.size() * sizeof(int4), hipMemcpyHostToDevice, s));
+    c->blocks_host = bl;
+  }
+  P.blocks = c->blocks.p;
+  P.n_blocks = (int)bl.size();
   // Work slots are (pixel, group of group_spp samples): small enough that
   // the dynamic queue balances the waves (a whole pixel per slot left the
   // launch waiting on a few waves holding 64-sample pixels).
@@ -461,17 +498,22 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     if (v > 0) P.group_spp = v;
   }
   P.group_spp = std::min(P.group_spp, P.spp);
-  for (;;) {  // the 32-bit queue head may overshoot by one chunk per wave
+  // 32-bit slot and partial indices (the queue head may overshoot by one
+  // chunk per wave); the per-pixel group sums stay within 4 GiB
+  const int64_t npx = (int64_t)P.W * P.H;
+  for (;;) {
     P.n_groups = (P.spp + P.group_spp - 1) / P.group_spp;
-    int64_t slots = (int64_t)tl.size() * 1024 * P.n_groups;
-    if (slots + want * PT_CHUNK < (int64_t)UINT32_MAX || P.n_groups == 1) break;
+    int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
+    bool fits = slots + want * PT_CHUNK < (int64_t)UINT32_MAX && npx * P.n_groups * 12 <= (4ll << 30);
+    if (fits || P.n_groups == 1) break;
     P.group_spp *= 2;
   }
-  int64_t slots = (int64_t)tl.size() * 1024 * P.n_groups;
-  if (slots + want * PT_CHUNK >= (int64_t)UINT32_MAX) return fail(PT_E_INVALID, "too many tiles for one launch");
-  HIPCHK(c->partial.reserve((size_t)slots * 3));
+  int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
+  if (slots + want * PT_CHUNK >= (int64_t)UINT32_MAX || npx * P.n_groups >= (int64_t)UINT32_MAX)
+    return fail(PT_E_INVALID, "frame too large for one launch");
+  HIPCHK(c->partial.reserve((size_t)(npx * P.n_groups) * 3));
   P.partial = c->partial.p;
-  int64_t max_grid = (slots + PT_BLOCK - 1) / PT_BLOCK;
+  int64_t max_grid = std::max<int64_t>(1, (slots + PT_BLOCK - 1) / PT_BLOCK);
   int grid = (int)std::min<int64_t>(want, max_grid);
   HIPCHK(hipEventRecord(c->ev0, s));
   HIPCHK(ptk_launch_render(&P, grid, stats, s));
@@ -495,8 +537,8 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags) {
   HIPCHK(hipEventElapsedTime(&ms, c->ev1, c->ev2));
   c->last.resolve_ms = ms;
   if (flags & PT_FLAG_STATS) {
-    unsigned long long v[16] = {0};
-    HIPCHK(hipMemcpy(v, c->stats.p, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    unsigned long long v[32] = {0};
+    HIPCHK(hipMemcpy(v, c->stats.p, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     c->last.camera_rays = (int64_t)v[0];
     c->last.bounce_rays = (int64_t)v[1];
     c->last.shadow_rays = (int64_t)v[2];
@@ -506,13 +548,14 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags) {
     c->last.ext_hits = (int64_t)v[6];
     c->last.wave_trav_steps = (int64_t)v[7];
     c->last.wave_rounds = (int64_t)v[8];
-    c->last.culled_samples = (int64_t)v[9];
+    c->last.culled_samples = c->culled_px * c->params.spp;
     c->last.queue_atomics = (int64_t)v[10];
     c->last.shade_clocks = (int64_t)v[11];
     c->last.trav_clocks = (int64_t)v[12];
     c->last.max_wave_clocks = (int64_t)v[13];
     c->last.wave_wall_sum = (int64_t)v[14];
     c->last.wave_wall_max = (int64_t)v[15];
+    c->last.hitshade_clocks = (int64_t)v[16];
     c->last.counters_valid = 1;
   }
   return PT_OK;

@@ -12,7 +12,16 @@
 #endif
 static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand");
 #ifndef PT_GROUP_SPP
-#define PT_GROUP_SPP 8  // default samples per work slot
+#define PT_GROUP_SPP 2  // default samples per work slot
+#endif
+#ifndef PT_SHADE_BATCH
+#define PT_SHADE_BATCH 48  // default: leave traversal when this many lanes finished their ray
+#endif
+#ifndef PT_LDS_BSDFS
+#define PT_LDS_BSDFS 16  // material tables up to this size are staged in LDS
+#endif
+#ifndef PT_LDS_LIGHTS
+#define PT_LDS_LIGHTS 8
 #endif
 #ifndef PT_STACK
 #define PT_STACK 32  // traversal stack entries per lane (LDS, lane-contiguous)
@@ -35,7 +44,7 @@ struct alignas(16) DPrim {
   float4 v0, e1, e2;
 };
 
-struct DBsdf {
+struct alignas(16) DBsdf {
   int type;
   float a[3];  // albedo / reflectance
   float t[3];  // transmittance
@@ -44,7 +53,7 @@ struct DBsdf {
   float pad;
 };
 
-struct DLight {
+struct alignas(16) DLight {
   int type;
   float rad[3];
   float pos[3];
@@ -62,6 +71,7 @@ struct KParams {
   int W, H, spp, max_depth, ns_area;
   uint32_t seed;
   int n_lights;
+  int n_bsdfs;
   int n_tiles;     // 32x32 (or smaller) tiles: 1024 pixels each
   int group_spp;   // samples per work slot (a slot is one pixel's sample group)
   int n_groups;    // ceil(spp / group_spp): slots per pixel
@@ -72,7 +82,9 @@ struct KParams {
   const DLight* lights;
   const int4* tiles;  // (x, y, w, h)
   float* out;         // W*H*3
-  float* partial;     // 3 floats per slot: the slot's sample sum, resolved into `out` in group order
+  float* partial;     // W*H*n_groups*3: each sample group's sum, resolved into `out` in group order
+  const int4* blocks;  // (x, y, w<=8, h<=8): footprint-clipped pixel blocks of the tiles
+  int n_blocks;
   uint32_t* work_counter;
   unsigned long long* stats;  // 7 counters (PT_FLAG_STATS)
   int dbg_pix;                // diagnostic printf trace of one pixel (-1: off)

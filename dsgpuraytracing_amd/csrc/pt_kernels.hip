@@ -109,6 +109,7 @@ struct RayState {
 struct Hit {
   float t, u, v;
   int prim;
+  int meta;  // the primitive's (bsdf << 1) | is_triangle, kept from the test
 };
 
 struct Counters {
@@ -139,6 +140,7 @@ __device__ __forceinline__ void trav_init(Trav& tr, float3 o, float3 d, float tm
   tr.hit.t = 0.0f;
   tr.hit.u = tr.hit.v = 0.0f;
   tr.hit.prim = -1;
+  tr.hit.meta = 0;
 }
 
 // Intersection of one primitive; updates the closest hit in `tr`.  Returns
@@ -183,6 +185,7 @@ __device__ __forceinline__ bool prim_test(const float4 v0, const float4 e1, cons
     tr.hit.u = u;
     tr.hit.v = v;
     tr.hit.prim = pi;
+    tr.hit.meta = meta;
     tr.found = true;
     return tr.any;
   }
@@ -287,6 +290,24 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   int* stk = s_stack + threadIdx.x;
   const int lane = threadIdx.x & 63;
 
+  // Material and light tables are read by every shading step: keep small
+  // ones in LDS (the usual case); larger ones stay in global memory.
+  __shared__ DBsdf s_bsdf[PT_LDS_BSDFS];
+  __shared__ DLight s_light[PT_LDS_LIGHTS];
+  const DBsdf* bsdfs = P.bsdfs;
+  const DLight* lights = P.lights;
+  if (P.n_bsdfs <= PT_LDS_BSDFS) {
+    const int n = P.n_bsdfs * (int)(sizeof(DBsdf) / 4);
+    for (int k = lane; k < n; k += PT_BLOCK) ((float*)s_bsdf)[k] = ((const float*)P.bsdfs)[k];
+    bsdfs = s_bsdf;
+  }
+  if (P.n_lights <= PT_LDS_LIGHTS) {
+    const int n = P.n_lights * (int)(sizeof(DLight) / 4);
+    for (int k = lane; k < n; k += PT_BLOCK) ((float*)s_light)[k] = ((const float*)P.lights)[k];
+    lights = s_light;
+  }
+  __syncthreads();
+
   // ---- per-lane state
   int mode = M_FETCH;
   bool shadow = false;  // the ray in flight is a shadow ray
@@ -308,15 +329,15 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   Counters ct = {0, 0, 0};
   uint32_t n_cam = 0, n_bounce = 0, n_shadow = 0, n_hits = 0;
   uint32_t n_titer = 0, n_rounds = 0;  // wave-level traversal steps / shading rounds (lane 0)
-  uint32_t n_culled = 0;               // samples of pixels outside the scene's screen footprint
   uint32_t n_atomics = 0;              // work-queue atomics (lane 0)
   uint32_t chunk_next = 0, chunk_end = 0;  // the wave's private range of work slots
   unsigned long long cyc_shade = 0, cyc_trav = 0;  // shader clocks per phase (lane 0)
+  unsigned long long cyc_hitshade = 0;              // of which: shading before the refill
   unsigned long long t_mark = STATS ? clock64() : 0ull;
   const unsigned long long w_start = STATS ? wall_clock64() : 0ull;
 
   const uint32_t n_groups = (uint32_t)P.n_groups;
-  const uint32_t total_slots = (uint32_t)P.n_tiles * 1024u * n_groups;
+  const uint32_t total_slots = (uint32_t)P.n_blocks * 64u * n_groups;
   const int batch = P.shade_batch;
 
   for (;;) {
@@ -339,9 +360,9 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         // not o + t*d, so their error is relative to the primitive and the
         // 256-ulp origin offset always clears the surface.
         const Hit h = tr.hit;
-        const DPrim pr = P.prims[h.prim];
-        const int meta = __float_as_int(pr.v0.w);
+        const int meta = h.meta;
         bsdf = meta >> 1;
+        const DPrim pr = P.prims[h.prim];
         if (meta & 1) {
           const float* nn = P.norms + 9 * (size_t)h.prim;
           float w0 = 1.0f - h.u - h.v;
@@ -361,19 +382,19 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if ((meta & 1) && dot(tr.d, ns) > 0.0f) ns = f3(0, 0, 0) - ns;
         ng = normalize(ng);
         wo = normalize(make_frame(ns).to_local(f3(0, 0, 0) - tr.d));
-        if (includeLe) L = L + mul(T, ld3(P.bsdfs[bsdf].e));
+        if (includeLe) L = L + mul(T, ld3(bsdfs[bsdf].e));
         if (DBG && pix == P.dbg_pix) printf("  depth %d hit prim %d bsdf %d t=%.9g n=(%.6g %.6g %.6g) T=(%.5g)\n", depth, h.prim, bsdf, h.t, ns.x, ns.y, ns.z, T.x);
         li = 0;
         ls = 0;
         stage = 0;
       }
       if (stage < 2) {
-        const DBsdf B = P.bsdfs[bsdf];
+        const DBsdf B = bsdfs[bsdf];
         const Frame fr = make_frame(ns);
         bool emitted = false;
         // ---- next-event estimation over all lights (pathtracer.cpp:469-523)
         while (li < P.n_lights) {
-          const DLight Lt = P.lights[li];
+          const DLight Lt = lights[li];
           const bool delta = Lt.type == 0 || Lt.type == 2;
           const int nls = delta ? 1 : P.ns_area;
           if (ls >= nls) {
@@ -513,6 +534,11 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         }
       }
     }
+    if (STATS) {
+      unsigned long long t = clock64();
+      cyc_hitshade += lane == 0 ? t - t_mark : 0ull;
+      t_mark = t;
+    }
     // ---- refill: wave-aggregated pixel fetch (one atomic per wave per round)
     // and camera rays.  Camera rays that miss the scene's root box carry zero
     // radiance (no environment light, pathtracer.cpp:421-426): they are
@@ -539,28 +565,24 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           if (slot >= total_slots) {
             mode = M_DONE;
           } else {
-            // slot = (tile * 1024 + pixel-in-tile) * n_groups + group: the
-            // groups of one pixel sit on neighbouring lanes (coherent rays)
-            uint32_t tq = slot / n_groups;
-            uint32_t g = slot - tq * n_groups;
-            int2 xy = tile_pixel(P.tiles[tq >> 10], tq & 1023u);
-            if (xy.x >= 0) {
-              px = xy.x;
-              py = xy.y;
+            // slot = (block * 64 + pixel-in-block) * n_groups + group: the
+            // groups of one pixel sit on neighbouring lanes (coherent rays).
+            // Blocks are <= 8x8 pixel rectangles of the tiles, clipped to the
+            // scene's screen footprint (pixels outside are written 0 by
+            // resolve_kernel: every ray through them misses the root box).
+            uint32_t bq = slot / n_groups;
+            uint32_t g = slot - bq * n_groups;
+            int4 b = P.blocks[bq >> 6];
+            int qx = (int)(bq & 7u), qy = (int)((bq >> 3) & 7u);
+            if (qx < b.z && qy < b.w) {
+              px = b.x + qx;
+              py = b.y + qy;
               pix = px + py * P.W;
               sample = (int)g * P.group_spp;
               s_end = min(P.spp, sample + P.group_spp);
-              wslot = slot;
+              wslot = (uint32_t)pix * n_groups + g;
               acc = f3(0, 0, 0);
               mode = M_CAMERA;
-              // Every ray of this pixel passes through the pinhole; if the
-              // pixel lies outside the scene box's conservative screen
-              // footprint, every sample misses the root box (zero radiance,
-              // written by resolve_kernel).
-              if (culled(P, px, py)) {
-                if (STATS) n_culled += s_end - sample;
-                mode = M_FETCH;
-              }
             }
           }
         }
@@ -630,7 +652,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
 
   if (STATS) {
     unsigned long long v[13] = {n_cam,   n_bounce, n_shadow,  ct.nodes,  ct.tris,  ct.spheres, n_hits,
-                                n_titer, n_rounds, n_culled, n_atomics, cyc_shade, cyc_trav};
+                                n_titer, n_rounds, 0u,       n_atomics, cyc_shade + cyc_hitshade, cyc_trav};
     for (int k = 0; k < 13; ++k) {
       unsigned long long s = v[k];
       for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
@@ -639,7 +661,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     // load balance: the slowest wave bounds the launch
     if (lane == 0) {
       unsigned long long w = wall_clock64() - w_start;
-      atomicMax(P.stats + 13, cyc_shade + cyc_trav);
+      atomicMax(P.stats + 13, cyc_shade + cyc_hitshade + cyc_trav);
+      atomicAdd(P.stats + 16, cyc_hitshade);
       atomicAdd(P.stats + 14, w);
       atomicMax(P.stats + 15, w);
     }
@@ -656,7 +679,7 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
   if (xy.x < 0) return;
   float3 acc = f3(0, 0, 0);
   if (!culled(P, xy.x, xy.y)) {
-    const float* p = P.partial + 3 * (size_t)tq * (size_t)P.n_groups;
+    const float* p = P.partial + 3 * ((size_t)xy.x + (size_t)xy.y * (size_t)P.W) * (size_t)P.n_groups;
     for (int g = 0; g < P.n_groups; ++g) acc = acc + ld3(p + 3 * g);
   }
   const float inv_spp = (float)(1.0 / (double)P.spp);

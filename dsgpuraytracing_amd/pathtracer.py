@@ -69,21 +69,24 @@ class Device:
 
     @staticmethod
     def _tiles(tiles: Sequence[Tuple[int, int, int, int]]):
-        arr = (native.pt_tile * max(1, len(tiles)))()
-        for i, (x, y, w, h) in enumerate(tiles):
-            arr[i] = native.pt_tile(x, y, w, h)
-        return arr
+        """pt_tile[] view of the tile list (an int32 (n, 4) array; the caller
+        keeps it alive for the duration of the call)."""
+        if isinstance(tiles, np.ndarray) and tiles.dtype == np.int32 and tiles.flags.c_contiguous:
+            arr = tiles.reshape(-1, 4)
+        else:
+            arr = np.ascontiguousarray(np.asarray(tiles, dtype=np.int32).reshape(-1, 4))
+        return arr, arr.ctypes.data_as(ctypes.POINTER(native.pt_tile))
 
     def render_tiles(self, tiles, out: np.ndarray, stats: bool = False):
         assert out.dtype == np.float32 and out.flags.c_contiguous
-        arr = self._tiles(tiles)
+        keep, arr = self._tiles(tiles)
         flags = native.PT_FLAG_STATS if stats else 0
-        check(self._lib.pt_render_tiles(self.handle, arr, len(tiles), out.ctypes.data, flags))
+        check(self._lib.pt_render_tiles(self.handle, arr, len(keep), out.ctypes.data, flags))
 
     def render_tiles_device(self, tiles, out_ptr: int, stream: int = 0, stats: bool = False):
-        arr = self._tiles(tiles)
+        keep, arr = self._tiles(tiles)
         flags = native.PT_FLAG_STATS if stats else 0
-        check(self._lib.pt_render_tiles_device(self.handle, arr, len(tiles), ctypes.c_void_p(out_ptr),
+        check(self._lib.pt_render_tiles_device(self.handle, arr, len(keep), ctypes.c_void_p(out_ptr),
                                                ctypes.c_void_p(stream or None), flags))
 
     def intersect(self, o, d, max_t):
