@@ -200,7 +200,7 @@ def main():
                                                    "tri_tests", "sphere_tests", "ext_hits", "wave_trav_steps",
                                                    "wave_rounds", "culled_samples", "queue_atomics", "shade_clocks",
                                                    "trav_clocks", "max_wave_clocks", "wave_wall_sum",
-                                                   "wave_wall_max", "hitshade_clocks")},
+                                                   "wave_wall_max", "hitshade_clocks", "leaf_steps")},
             "traversal_simd_efficiency": round(st_counts["node_visits"] / max(1, 64 * st_counts["wave_trav_steps"]), 4),
             "launch": {"grid_blocks": s["grid_blocks"], "block": 64, "blocks_per_cu_query": s["blocks_per_cu"]},
             "image_mean": float(img.mean()),

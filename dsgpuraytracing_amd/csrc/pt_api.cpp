@@ -200,7 +200,9 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
     }
   }
 
-  // ---- BVH: internal nodes only, pre-order, child boxes rounded outward.
+  // ---- BVH: internal nodes only, pre-order, child boxes rounded outward;
+  // leaves become cursors in their parent's child references.  Leaves of more
+  // than 8 primitives are split into small subtrees over primitive boxes.
   const pt_bvh_node* N = s->nodes;
   const int64_t nn = s->n_nodes;
   auto is_leaf = [&](int64_t i) { return N[i].left < 0 && N[i].right < 0; };
@@ -210,14 +212,59 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
     if (is_leaf(i) && (N[i].start < 0 || N[i].range <= 0 || N[i].start + N[i].range > s->n_prims))
       return fail(PT_E_INVALID, "pt_upload_scene: bad leaf range");
   }
-  std::vector<DNode> dn;
-  std::vector<int64_t> map(nn, -1);
-  int max_depth = 0;
-  auto set_child = [&](DNode& d, int side, int64_t ci) {
-    const pt_bvh_node& C = N[ci];
-    float lx = round_down(C.bb_min[0]), hx = round_up(C.bb_max[0]);
-    float ly = round_down(C.bb_min[1]), hy = round_up(C.bb_max[1]);
-    float lz = round_down(C.bb_min[2]), hz = round_up(C.bb_max[2]);
+  if (s->n_prims >= ((int64_t)1 << 27)) return fail(PT_E_INVALID, "pt_upload_scene: too many primitives for leaf cursors");
+  auto prim_box = [&](int64_t first, int64_t count, double lo[3], double hi[3]) {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = INFINITY;
+      hi[k] = -INFINITY;
+    }
+    for (int64_t i = first; i < first + count; ++i) {
+      const double* g = s->prim_geom + 9 * i;
+      for (int k = 0; k < 3; ++k) {
+        if (s->prim_type[i] == PT_PRIM_TRIANGLE) {
+          lo[k] = std::min({lo[k], g[k], g[3 + k], g[6 + k]});
+          hi[k] = std::max({hi[k], g[k], g[3 + k], g[6 + k]});
+        } else {
+          lo[k] = std::min(lo[k], g[k] - std::fabs(g[3]));
+          hi[k] = std::max(hi[k], g[k] + std::fabs(g[3]));
+        }
+      }
+    }
+  };
+  // a subtree to emit: a reference node, or a primitive range (split leaf)
+  struct Sub {
+    int64_t ref;          // >= 0: reference node; -1: primitive range
+    int64_t first, count;
+    double lo[3], hi[3];
+  };
+  auto sub_of_node = [&](int64_t r) {
+    Sub u{r, N[r].start, N[r].range, {}, {}};
+    for (int k = 0; k < 3; ++k) {
+      u.lo[k] = N[r].bb_min[k];
+      u.hi[k] = N[r].bb_max[k];
+    }
+    return u;
+  };
+  auto sub_of_range = [&](int64_t first, int64_t count) {
+    Sub u{-1, first, count, {}, {}};
+    prim_box(first, count, u.lo, u.hi);
+    return u;
+  };
+  auto sub_is_leaf = [&](const Sub& u) { return u.ref >= 0 ? is_leaf(u.ref) && u.count <= 8 : u.count <= 8; };
+  auto sub_children = [&](const Sub& u, Sub ch[2]) {
+    if (u.ref >= 0 && !is_leaf(u.ref)) {
+      ch[0] = sub_of_node(N[u.ref].left);
+      ch[1] = sub_of_node(N[u.ref].right);
+    } else {  // oversized leaf: halve the primitive range
+      int64_t h = u.count / 2;
+      ch[0] = sub_of_range(u.first, h);
+      ch[1] = sub_of_range(u.first + h, u.count - h);
+    }
+  };
+  auto set_box = [&](DNode& d, int side, const Sub& u) {
+    float lx = round_down(u.lo[0]), hx = round_up(u.hi[0]);
+    float ly = round_down(u.lo[1]), hy = round_up(u.hi[1]);
+    float lz = round_down(u.lo[2]), hz = round_up(u.hi[2]);
     if (side == 0) {
       d.a = make_float4(lx, hx, ly, hy);
       d.c.x = lz;
@@ -228,44 +275,48 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
       d.c.w = hz;
     }
   };
-  if (is_leaf(0)) {
+  auto cursor = [](int64_t first, int64_t count) { return (int)~((first << 3) | (count - 1)); };
+  std::vector<DNode> dn;
+  int max_depth = 0;
+  Sub root = sub_of_node(0);
+  if (sub_is_leaf(root)) {  // one leaf: a root node whose second child box is empty
     DNode d{};
-    set_child(d, 0, 0);
+    set_box(d, 0, root);
     d.b = make_float4(1.f, -1.f, 1.f, -1.f);
     d.c.z = 1.f;
     d.c.w = -1.f;
-    d.e = make_int4((int)N[0].start, 0, (int)N[0].range, -1);
+    d.e = make_int4(cursor(root.first, root.count), 0, 0, 0);
     dn.push_back(d);
     max_depth = 1;
   } else {
-    // explicit DFS: (ref node, parent dnode, side, depth)
-    struct Item { int64_t ref; int64_t parent; int side; int depth; };
-    std::vector<Item> st = {{0, -1, 0, 1}};
+    // explicit DFS: (subtree, parent dnode, side, depth)
+    struct Item { Sub u; int64_t parent; int side; int depth; };
+    std::vector<Item> st = {{root, -1, 0, 1}};
     while (!st.empty()) {
       Item it = st.back();
       st.pop_back();
       int64_t me = (int64_t)dn.size();
       dn.push_back(DNode{});
-      map[it.ref] = me;
       max_depth = std::max(max_depth, it.depth);
       if (it.parent >= 0) {
         if (it.side == 0) dn[it.parent].e.x = (int)me;
         else dn[it.parent].e.y = (int)me;
       }
-      const pt_bvh_node& R = N[it.ref];
-      int64_t ch[2] = {R.left, R.right};
+      Sub ch[2];
+      sub_children(it.u, ch);
       for (int side = 0; side < 2; ++side) {
-        set_child(dn[me], side, ch[side]);
-        if (is_leaf(ch[side])) {
-          if (side == 0) { dn[me].e.x = (int)N[ch[0]].start; dn[me].e.z = (int)N[ch[0]].range; }
-          else { dn[me].e.y = (int)N[ch[1]].start; dn[me].e.w = (int)N[ch[1]].range; }
+        set_box(dn[me], side, ch[side]);
+        if (sub_is_leaf(ch[side])) {
+          if (side == 0) dn[me].e.x = cursor(ch[0].first, ch[0].count);
+          else dn[me].e.y = cursor(ch[1].first, ch[1].count);
         }
       }
       // push right first so the left subtree follows its parent in memory
       for (int side = 1; side >= 0; --side)
-        if (!is_leaf(ch[side])) st.push_back({ch[side], me, side, it.depth + 1});
+        if (!sub_is_leaf(ch[side])) st.push_back({ch[side], me, side, it.depth + 1});
     }
   }
+  if ((int64_t)dn.size() >= ((int64_t)1 << 31)) return fail(PT_E_INVALID, "pt_upload_scene: too many BVH nodes");
   if (max_depth > PT_STACK)
     return fail(PT_E_INVALID, "pt_upload_scene: BVH deeper than the traversal stack (" + std::to_string(max_depth) +
                                   " > " + std::to_string(PT_STACK) + ")");
@@ -452,6 +503,11 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   }
   screen_footprint(c, P);
   P.shade_batch = PT_SHADE_BATCH;
+  P.leaf_weight = PT_LEAF_WEIGHT;
+  if (const char* lw = std::getenv("PT_LEAF_WEIGHT")) {  // tuning knob
+    int v = std::atoi(lw);
+    if (v >= 1) P.leaf_weight = v;
+  }
   if (const char* sb = std::getenv("PT_SHADE_BATCH")) {  // tuning knob
     int v = std::atoi(sb);
     if (v >= 1 && v <= 64) P.shade_batch = v;
@@ -549,6 +605,7 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags) {
     c->last.wave_trav_steps = (int64_t)v[7];
     c->last.wave_rounds = (int64_t)v[8];
     c->last.culled_samples = c->culled_px * c->params.spp;
+    c->last.leaf_steps = (int64_t)v[9];
     c->last.queue_atomics = (int64_t)v[10];
     c->last.shade_clocks = (int64_t)v[11];
     c->last.trav_clocks = (int64_t)v[12];

@@ -23,6 +23,9 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #ifndef PT_LDS_LIGHTS
 #define PT_LDS_LIGHTS 8
 #endif
+#ifndef PT_LEAF_WEIGHT
+#define PT_LEAF_WEIGHT 16  // leaf steps when leaf lanes >= node lanes * 16 / PT_LEAF_WEIGHT
+#endif
 #ifndef PT_STACK
 #define PT_STACK 32  // traversal stack entries per lane (LDS, lane-contiguous)
 #endif
@@ -31,8 +34,9 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 //  a = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
 //  b = (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
 //  c = (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
-//  e = (c0 ref, c1 ref, c0 count, c1 count): count 0 => ref is a node index,
-//      count > 0 => leaf primitives [ref, ref+count) in BVH order.
+//  e = (c0 ref, c1 ref, 0, 0): ref >= 0 is a node index; ref < 0 is a leaf
+//      cursor ~((first << 3) | (count - 1)): primitives [first, first+count)
+//      in BVH order, count <= 8 (longer leaves are split into subtrees).
 struct alignas(16) DNode {
   float4 a, b, c;
   int4 e;
@@ -89,6 +93,7 @@ struct KParams {
   unsigned long long* stats;  // 7 counters (PT_FLAG_STATS)
   int dbg_pix;                // diagnostic printf trace of one pixel (-1: off)
   int shade_batch;            // leave the traversal phase once this many lanes finished their ray
+  int leaf_weight;            // leaf steps run when leaf_weight * leaf lanes >= 16 * node lanes
   float root_lo[3], root_hi[3];  // scene bounds (root box, rounded outward)
   int cull_x0, cull_y0, cull_x1, cull_y1;  // pixels outside [x0,x1]x[y0,y1] see no geometry
 };

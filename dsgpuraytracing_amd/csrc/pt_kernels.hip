@@ -192,15 +192,28 @@ __device__ __forceinline__ bool prim_test(const float4 v0, const float4 e1, cons
   return false;
 }
 
-// One traversal step: fetch one node (both child boxes), intersect the
-// primitives of leaf children in place, then descend / push / pop.  Returns
-// true when the query is complete.  Semantics: nearest hit (bvh.cpp:227-279,
-// 343-362: the same closest hit, children visited near-first, boxes clipped to
-// the current [0, tmax]) or, with tr.any, occlusion within (0, tmax)
-// (bvh.cpp:282-341), leaving on the first hit.
+// Traversal is split into two kinds of step so that a wave runs one kind at a
+// time with most lanes active (if-if traversal with wave-level scheduling,
+// after Aila & Laine 2009):
+//  * node step (tr.node >= 0): fetch one node, slab-test both child boxes,
+//    continue with the nearer child and push the farther one;
+//  * leaf step (tr.node < 0, a leaf cursor): test up to two primitives of the
+//    leaf with all six 16-B loads issued together, then pop.
+// Children references (DNode.e.x/y) are node indices or leaf cursors, so a
+// leaf is entered, pushed and popped like a node.  Semantics: nearest hit
+// (bvh.cpp:227-279, 343-362: the same closest hit, children visited near-first,
+// boxes clipped to the current [0, tmax]) or, with tr.any, occlusion within
+// (0, tmax) (bvh.cpp:282-341), leaving on the first hit.
+__device__ __forceinline__ bool trav_pop(int* __restrict__ stk, int stride, Trav& tr) {
+  if (tr.sp == 0) return true;
+  --tr.sp;
+  tr.node = stk[tr.sp * stride];
+  return false;
+}
+
 template <bool STATS>
-__device__ __forceinline__ bool trav_step(const DNode* __restrict__ nodes, const DPrim* __restrict__ prims,
-                                          int* __restrict__ stk, int stride, Trav& tr, Counters& ct) {
+__device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, int* __restrict__ stk, int stride, Trav& tr,
+                                          Counters& ct) {
   const float kRobust = 1.0000005f;
   const float4 a = nodes[tr.node].a;
   const float4 b = nodes[tr.node].b;
@@ -219,24 +232,8 @@ __device__ __forceinline__ bool trav_step(const DNode* __restrict__ nodes, const
   float tf0 = fminf(fminf(fmaxf(l0x, h0x), fmaxf(l0y, h0y)), fminf(fmaxf(l0z, h0z), tr.tmax)) * kRobust;
   float tn1 = fmaxf(fmaxf(fminf(l1x, h1x), fminf(l1y, h1y)), fmaxf(fminf(l1z, h1z), 0.0f));
   float tf1 = fminf(fminf(fmaxf(l1x, h1x), fmaxf(l1y, h1y)), fminf(fmaxf(l1z, h1z), tr.tmax)) * kRobust;
-  bool hit0 = tn0 <= tf0;
-  bool hit1 = tn1 <= tf1;
-  // Leaf children: intersect their primitives now, two at a time with all six
-  // 16-B loads issued together (one memory round trip per pair).
-  const bool leaf0 = hit0 && e.z > 0, leaf1 = hit1 && e.w > 0;
-  const int c0 = leaf0 ? e.z : 0;
-  const int total = c0 + (leaf1 ? e.w : 0);
-  for (int k = 0; k < total; k += 2) {
-    const int pa = k < c0 ? e.x + k : e.y + (k - c0);
-    const bool two = k + 1 < total;
-    const int pb = !two ? pa : (k + 1 < c0 ? e.x + k + 1 : e.y + (k + 1 - c0));
-    const float4 a0 = prims[pa].v0, a1 = prims[pa].e1, a2 = prims[pa].e2;
-    const float4 b0 = prims[pb].v0, b1 = prims[pb].e1, b2 = prims[pb].e2;
-    if (prim_test<STATS>(a0, a1, a2, pa, tr, ct)) return true;
-    if (two && prim_test<STATS>(b0, b1, b2, pb, tr, ct)) return true;
-  }
-  bool in0 = hit0 && e.z == 0 && tn0 <= tr.tmax;
-  bool in1 = hit1 && e.w == 0 && tn1 <= tr.tmax;
+  bool in0 = tn0 <= tf0;
+  bool in1 = tn1 <= tf1;
   if (in0 && in1) {
     bool first0 = tn0 <= tn1;
     stk[tr.sp * stride] = first0 ? e.y : e.x;
@@ -247,11 +244,37 @@ __device__ __forceinline__ bool trav_step(const DNode* __restrict__ nodes, const
   } else if (in1) {
     tr.node = e.y;
   } else {
-    if (tr.sp == 0) return true;
-    --tr.sp;
-    tr.node = stk[tr.sp * stride];
+    return trav_pop(stk, stride, tr);
   }
   return false;
+}
+
+// Leaf cursor: ~((first << 3) | (count - 1)), count in [1, 8].
+__device__ __forceinline__ int leaf_first(int cur) { return (~cur) >> 3; }
+__device__ __forceinline__ int leaf_count(int cur) { return ((~cur) & 7) + 1; }
+
+template <bool STATS>
+__device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, int* __restrict__ stk, int stride,
+                                          Trav& tr, Counters& ct) {
+  const int pa = leaf_first(tr.node);
+  const int n = leaf_count(tr.node);
+  const bool two = n >= 2;
+  const int pb = two ? pa + 1 : pa;
+  const float4 a0 = prims[pa].v0, a1 = prims[pa].e1, a2 = prims[pa].e2;
+  const float4 b0 = prims[pb].v0, b1 = prims[pb].e1, b2 = prims[pb].e2;
+  if (prim_test<STATS>(a0, a1, a2, pa, tr, ct)) return true;
+  if (two && prim_test<STATS>(b0, b1, b2, pb, tr, ct)) return true;
+  if (n > 2) {
+    tr.node = ~(((pa + 2) << 3) | (n - 3));
+    return false;
+  }
+  return trav_pop(stk, stride, tr);
+}
+
+template <bool STATS>
+__device__ __forceinline__ bool trav_step(const DNode* __restrict__ nodes, const DPrim* __restrict__ prims,
+                                          int* __restrict__ stk, int stride, Trav& tr, Counters& ct) {
+  return tr.node < 0 ? leaf_step<STATS>(prims, stk, stride, tr, ct) : node_step<STATS>(nodes, stk, stride, tr, ct);
 }
 
 template <bool STATS>
@@ -329,6 +352,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   Counters ct = {0, 0, 0};
   uint32_t n_cam = 0, n_bounce = 0, n_shadow = 0, n_hits = 0;
   uint32_t n_titer = 0, n_rounds = 0;  // wave-level traversal steps / shading rounds (lane 0)
+  uint32_t n_leafit = 0;               // of the traversal steps: leaf steps
   uint32_t n_atomics = 0;              // work-queue atomics (lane 0)
   uint32_t chunk_next = 0, chunk_end = 0;  // the wave's private range of work slots
   unsigned long long cyc_shade = 0, cyc_trav = 0;  // shader clocks per phase (lane 0)
@@ -638,7 +662,20 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     }
     for (;;) {
       if (STATS) n_titer += lane == 0;
-      if (mode == M_TRAV && trav_step<STATS>(P.nodes, P.prims, stk, PT_BLOCK, tr, ct)) mode = M_SHADE;
+      // one kind of step per iteration: leaf steps once enough lanes wait on
+      // a leaf (or nothing else is left), node steps otherwise
+      const bool trav = mode == M_TRAV;
+      const bool at_leaf = trav && tr.node < 0;
+      const int n_leaf = __popcll(__ballot(at_leaf));
+      const int n_node = __popcll(__ballot(trav && !at_leaf));
+      bool done = false;
+      if (n_leaf > 0 && (n_node == 0 || n_leaf * P.leaf_weight >= n_node * 16)) {
+        if (at_leaf) done = leaf_step<STATS>(P.prims, stk, PT_BLOCK, tr, ct);
+        if (STATS) n_leafit += lane == 0;
+      } else {
+        if (trav && !at_leaf) done = node_step<STATS>(P.nodes, stk, PT_BLOCK, tr, ct);
+      }
+      if (done) mode = M_SHADE;
       unsigned long long ready = __ballot(mode == M_SHADE);
       unsigned long long busy = __ballot(mode == M_TRAV);
       if (busy == 0ull || __popcll(ready) >= batch) break;
@@ -652,7 +689,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
 
   if (STATS) {
     unsigned long long v[13] = {n_cam,   n_bounce, n_shadow,  ct.nodes,  ct.tris,  ct.spheres, n_hits,
-                                n_titer, n_rounds, 0u,       n_atomics, cyc_shade + cyc_hitshade, cyc_trav};
+                                n_titer, n_rounds, n_leafit,  n_atomics, cyc_shade + cyc_hitshade, cyc_trav};
     for (int k = 0; k < 13; ++k) {
       unsigned long long s = v[k];
       for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);

@@ -165,6 +165,7 @@ typedef struct pt_stats {
   int64_t max_wave_clocks; /* shader clocks of the slowest wave */
   int64_t wave_wall_sum;   /* wave lifetimes summed, device wall-clock ticks */
   int64_t wave_wall_max;   /* longest wave lifetime, device wall-clock ticks */
+  int64_t leaf_steps;      /* of wave_trav_steps: leaf (primitive) steps */
   int64_t hitshade_clocks; /* of shade_clocks: hit records, NEE and bounces (the rest is refill) */
   double resolve_ms;       /* device time of the sample-group resolve kernel */
 } pt_stats;
