@@ -146,6 +146,42 @@ def test_hip_ray_queries_vs_reference_kat():
     assert (anyh == ref["any"]).mean() >= 0.995
 
 
+def _single_leaf_scene(name):
+    """The scene with its BVH replaced by ONE leaf holding every primitive:
+    the upload must split it into <= 8-primitive leaves over primitive boxes."""
+    d = dict(ptdump.read(golden(f"{name}.scene.ptd")))
+    n = len(d["prim_type"])
+    assert n > 8
+    d["node_bb"] = d["node_bb"].reshape(-1, 6)[:1].reshape(-1).copy()
+    d["node_info"] = np.array([0, n, -1, -1], dtype=d["node_info"].dtype)
+    return Scene(native.SceneArrays(d))
+
+
+@pytest.mark.parametrize("name", ["c1_default_64x64", "CBspheres_64x64"])
+def test_hip_oversize_leaf_split_matches_reference_bvh(name):
+    """Closest hits do not depend on the BVH: a scene whose reference BVH is a
+    single oversize leaf renders like the reference BVH."""
+    from dsgpuraytracing_amd.pathtracer import Device
+    rays = ptdump.read(golden("c1_rays.ptd"))
+    res = []
+    for sc in (Scene.from_dump(golden(f"{name}.scene.ptd")), _single_leaf_scene(name)):
+        dev = Device(0)
+        dev.upload_scene(sc)
+        res.append(dev.intersect(rays["ray_o"], rays["ray_d"], rays["ray_maxt"]))
+        pt = PathTracer(ns_aa=4, max_ray_depth=4, ns_area_light=1, seed=9)
+        pt.set_frame_size(64, 64)
+        pt.set_camera(sc.camera)
+        pt.set_scene(sc)
+        pt.start_raytracing()
+        res.append(pt.sampleBuffer.copy())
+    (h0, t0, p0, a0), img0, (h1, t1, p1, a1), img1 = res
+    assert (h0 == h1).mean() >= 0.999 and (a0 == a1).mean() >= 0.999
+    same = (h0 == 1) & (h1 == 1)
+    assert np.allclose(t0[same], t1[same], rtol=1e-5, atol=1e-6)
+    frac, rel_mean = near_exact_report(img1, img0)
+    assert frac >= 0.995 and rel_mean <= 1e-3, (frac, rel_mean)
+
+
 def test_hip_stats_counters():
     _, st = gpu_render("c1_default_64x64", 64, 64, 2, stats=True)
     assert st["counters_valid"] == 1
