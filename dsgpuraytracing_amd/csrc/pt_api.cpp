@@ -94,6 +94,7 @@ struct pt_ctx {
   DevBuf<float> q_f;    // ray-query scratch
   DevBuf<int32_t> q_i;
   int n_lights = 0, n_bsdfs = 0;
+  int bvh_stack = 0;  // worst-case traversal stack entries of the uploaded BVH
   int64_t n_prims = 0;
   float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
   double root_lo_d[3] = {0, 0, 0}, root_hi_d[3] = {0, 0, 0};
@@ -261,65 +262,134 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
       ch[1] = sub_of_range(u.first + h, u.count - h);
     }
   };
-  auto set_box = [&](DNode& d, int side, const Sub& u) {
-    float lx = round_down(u.lo[0]), hx = round_up(u.hi[0]);
-    float ly = round_down(u.lo[1]), hy = round_up(u.hi[1]);
-    float lz = round_down(u.lo[2]), hz = round_up(u.hi[2]);
-    if (side == 0) {
-      d.a = make_float4(lx, hx, ly, hy);
-      d.c.x = lz;
-      d.c.y = hz;
-    } else {
-      d.b = make_float4(lx, hx, ly, hy);
-      d.c.z = lz;
-      d.c.w = hz;
+  // (1) binary tree over the reference topology: child boxes rounded outward
+  // to fp32, child references are node indices or leaf cursors
+  struct B2 {
+    float lo[2][3], hi[2][3];
+    int ref[2];
+  };
+  auto set_box = [&](B2& d, int side, const Sub& u) {
+    for (int k = 0; k < 3; ++k) {
+      d.lo[side][k] = round_down(u.lo[k]);
+      d.hi[side][k] = round_up(u.hi[k]);
     }
   };
   auto cursor = [](int64_t first, int64_t count) { return (int)~((first << 3) | (count - 1)); };
-  std::vector<DNode> dn;
-  int max_depth = 0;
+  std::vector<B2> b2;
   Sub root = sub_of_node(0);
-  if (sub_is_leaf(root)) {  // one leaf: a root node whose second child box is empty
-    DNode d{};
+  if (sub_is_leaf(root)) {  // one leaf: a root whose second child box is empty
+    B2 d{};
     set_box(d, 0, root);
-    d.b = make_float4(1.f, -1.f, 1.f, -1.f);
-    d.c.z = 1.f;
-    d.c.w = -1.f;
-    d.e = make_int4(cursor(root.first, root.count), 0, 0, 0);
-    dn.push_back(d);
-    max_depth = 1;
+    for (int k = 0; k < 3; ++k) d.lo[1][k] = d.hi[1][k] = INFINITY;
+    d.ref[0] = cursor(root.first, root.count);
+    d.ref[1] = 0;
+    b2.push_back(d);
   } else {
-    // explicit DFS: (subtree, parent dnode, side, depth)
-    struct Item { Sub u; int64_t parent; int side; int depth; };
-    std::vector<Item> st = {{root, -1, 0, 1}};
+    // explicit DFS: (subtree, parent node, side)
+    struct Item { Sub u; int64_t parent; int side; };
+    std::vector<Item> st = {{root, -1, 0}};
     while (!st.empty()) {
       Item it = st.back();
       st.pop_back();
-      int64_t me = (int64_t)dn.size();
-      dn.push_back(DNode{});
-      max_depth = std::max(max_depth, it.depth);
-      if (it.parent >= 0) {
-        if (it.side == 0) dn[it.parent].e.x = (int)me;
-        else dn[it.parent].e.y = (int)me;
-      }
+      int64_t me = (int64_t)b2.size();
+      b2.push_back(B2{});
+      if (it.parent >= 0) b2[it.parent].ref[it.side] = (int)me;
       Sub ch[2];
       sub_children(it.u, ch);
       for (int side = 0; side < 2; ++side) {
-        set_box(dn[me], side, ch[side]);
-        if (sub_is_leaf(ch[side])) {
-          if (side == 0) dn[me].e.x = cursor(ch[0].first, ch[0].count);
-          else dn[me].e.y = cursor(ch[1].first, ch[1].count);
-        }
+        set_box(b2[me], side, ch[side]);
+        if (sub_is_leaf(ch[side])) b2[me].ref[side] = cursor(ch[side].first, ch[side].count);
       }
-      // push right first so the left subtree follows its parent in memory
       for (int side = 1; side >= 0; --side)
-        if (!sub_is_leaf(ch[side])) st.push_back({ch[side], me, side, it.depth + 1});
+        if (!sub_is_leaf(ch[side])) st.push_back({ch[side], me, side});
     }
   }
-  if ((int64_t)dn.size() >= ((int64_t)1 << 31)) return fail(PT_E_INVALID, "pt_upload_scene: too many BVH nodes");
-  if (max_depth > PT_STACK)
-    return fail(PT_E_INVALID, "pt_upload_scene: BVH deeper than the traversal stack (" + std::to_string(max_depth) +
+  if ((int64_t)b2.size() >= ((int64_t)1 << 31)) return fail(PT_E_INVALID, "pt_upload_scene: too many BVH nodes");
+
+  // (2) collapse to 4-wide nodes: repeatedly open the internal child of the
+  // largest surface area (the usual BVH2 -> BVH4 collapse).  Pre-order, so
+  // a node's first child follows it in memory.
+  struct Child {
+    float lo[3], hi[3];
+    int ref;
+  };
+  auto area = [](const Child& c) {
+    float dx = c.hi[0] - c.lo[0], dy = c.hi[1] - c.lo[1], dz = c.hi[2] - c.lo[2];
+    return dx * dy + dy * dz + dz * dx;
+  };
+  auto kids = [&](int n, Child out[2]) {
+    for (int s2 = 0; s2 < 2; ++s2) {
+      for (int k = 0; k < 3; ++k) {
+        out[s2].lo[k] = b2[(size_t)n].lo[s2][k];
+        out[s2].hi[k] = b2[(size_t)n].hi[s2][k];
+      }
+      out[s2].ref = b2[(size_t)n].ref[s2];
+    }
+  };
+  std::vector<DNode> dn;
+  int max_stack = 0;
+  {
+    struct Item4 { int b2node; int64_t parent; int slot; int stack; };
+    std::vector<Item4> st = {{0, -1, 0, 0}};
+    while (!st.empty()) {
+      Item4 it = st.back();
+      st.pop_back();
+      Child ch[4];
+      int n = 2;
+      kids(it.b2node, ch);
+      while (n < 4) {
+        int best = -1;
+        float ba = -1.f;
+        for (int k = 0; k < n; ++k)
+          if (ch[k].ref >= 0 && area(ch[k]) > ba) {
+            ba = area(ch[k]);
+            best = k;
+          }
+        if (best < 0) break;
+        Child two[2];
+        kids(ch[best].ref, two);
+        ch[best] = two[0];
+        ch[n++] = two[1];
+      }
+      int64_t me = (int64_t)dn.size();
+      dn.push_back(DNode{});
+      if (it.parent >= 0) (&dn[(size_t)it.parent].ref.x)[it.slot] = (int)me;
+      DNode& d = dn[(size_t)me];
+      float* lox = &d.lox.x; float* hix = &d.hix.x; float* loy = &d.loy.x;
+      float* hiy = &d.hiy.x; float* loz = &d.loz.x; float* hiz = &d.hiz.x;
+      int* ref = &d.ref.x;
+      for (int k = 0; k < 4; ++k) {
+        if (k < n) {
+          lox[k] = ch[k].lo[0]; hix[k] = ch[k].hi[0];
+          loy[k] = ch[k].lo[1]; hiy[k] = ch[k].hi[1];
+          loz[k] = ch[k].lo[2]; hiz[k] = ch[k].hi[2];
+          ref[k] = ch[k].ref;
+        } else {  // empty slot: the box at +inf, which no ray enters (an inverted
+                  // box would not do: the slab test orders each pair of planes)
+          lox[k] = loy[k] = loz[k] = hix[k] = hiy[k] = hiz[k] = INFINITY;
+          ref[k] = 0;
+        }
+      }
+      // a visit pushes at most n-1 siblings before descending
+      const int below = it.stack + (n - 1);
+      max_stack = std::max(max_stack, below);
+      for (int k = n - 1; k >= 0; --k)
+        if (ch[k].ref >= 0) st.push_back({ch[k].ref, me, k, below});
+    }
+  }
+  // Traversal termination rests on this: node references only point forward
+  // (pre-order), so a ray can never re-enter a node it has left.
+  for (size_t i = 0; i < dn.size(); ++i)
+    for (int k = 0; k < 4; ++k) {
+      int r = (&dn[i].ref.x)[k];
+      bool empty = std::isinf((&dn[i].lox.x)[k]);
+      if (!empty && r >= 0 && (r <= (int)i || r >= (int)dn.size()))
+        return fail(PT_E_INVALID, "pt_upload_scene: BVH4 child reference is not forward");
+    }
+  if (max_stack > PT_STACK)
+    return fail(PT_E_INVALID, "pt_upload_scene: BVH needs a deeper traversal stack (" + std::to_string(max_stack) +
                                   " > " + std::to_string(PT_STACK) + ")");
+  c->bvh_stack = max_stack;
 
   std::vector<DBsdf> bs((size_t)s->n_bsdfs);
   for (int i = 0; i < s->n_bsdfs; ++i) {
@@ -480,6 +550,8 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.cam_ay = (float)(c->cam.screen_h / c->cam.screen_dist);
   P.W = c->params.width;
   P.H = c->params.height;
+  P.inv_w = 1.0f / (float)P.W;
+  P.inv_h = 1.0f / (float)P.H;
   P.spp = c->params.spp;
   P.max_depth = c->params.max_depth;
   P.ns_area = c->params.ns_area_light;

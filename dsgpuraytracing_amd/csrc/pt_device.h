@@ -30,16 +30,15 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #define PT_STACK 32  // traversal stack entries per lane (LDS, lane-contiguous)
 #endif
 
-// BVH2 node, 64 B: both child boxes + child references.
-//  a = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
-//  b = (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
-//  c = (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
-//  e = (c0 ref, c1 ref, 0, 0): ref >= 0 is a node index; ref < 0 is a leaf
-//      cursor ~((first << 3) | (count - 1)): primitives [first, first+count)
-//      in BVH order, count <= 8 (longer leaves are split into subtrees).
+// BVH4 node, 128 B (one L2 line): four child boxes in SoA form, component k
+// of each float4 belongs to child k, then the four child references.
+//  ref >= 0 is a node index; ref < 0 is a leaf cursor ~((first << 3) | (count - 1)):
+//  primitives [first, first+count) in BVH order, count <= 8 (longer leaves
+//  are split into subtrees).  Unused slots hold a box at +inf (never entered).
 struct alignas(16) DNode {
-  float4 a, b, c;
-  int4 e;
+  float4 lox, hix, loy, hiy, loz, hiz;
+  int4 ref;
+  int4 pad;
 };
 
 // Primitive, 48 B.  Triangle: v0 = (p1, meta), e1 = p2-p1, e2 = p3-p1.
@@ -73,6 +72,7 @@ struct KParams {
   float c2w_col0[3], c2w_col1[3], c2w_col2[3];
   float cam_ax, cam_ay;  // screenW/screenDist, screenH/screenDist
   int W, H, spp, max_depth, ns_area;
+  float inv_w, inv_h;  // 1/W, 1/H
   uint32_t seed;
   int n_lights;
   int n_bsdfs;

@@ -47,6 +47,7 @@ __device__ __forceinline__ float3 cross(float3 u, float3 v) {
 // determinant do not need IEEE division's last bit, and one instruction
 // replaces a ~10-instruction correctly rounded sequence.
 __device__ __forceinline__ float3 normalize(float3 v) { return v * __builtin_amdgcn_rsqf(dot(v, v)); }
+__device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float illum(float3 s) { return 0.2126f * s.x + 0.7152f * s.y + 0.0722f * s.z; }
 __device__ __forceinline__ float3 ld3(const float* p) { return f3(p[0], p[1], p[2]); }
 __device__ __forceinline__ void store3(float* p, float3 v) {
@@ -198,11 +199,12 @@ __device__ __forceinline__ bool prim_test(const float4 v0, const float4 e1, cons
 // Traversal is split into two kinds of step so that a wave runs one kind at a
 // time with most lanes active (if-if traversal with wave-level scheduling,
 // after Aila & Laine 2009):
-//  * node step (tr.node >= 0): fetch one node, slab-test both child boxes,
-//    continue with the nearer child and push the farther one;
+//  * node step (tr.node >= 0): fetch one 4-wide node (128 B), slab-test the
+//    four child boxes, continue with the nearest child and push the others
+//    farthest-first;
 //  * leaf step (tr.node < 0, a leaf cursor): test up to two primitives of the
 //    leaf with all six 16-B loads issued together, then pop.
-// Children references (DNode.e.x/y) are node indices or leaf cursors, so a
+// Children references (DNode.ref) are node indices or leaf cursors, so a
 // leaf is entered, pushed and popped like a node.  Semantics: nearest hit
 // (bvh.cpp:227-279, 343-362: the same closest hit, children visited near-first,
 // boxes clipped to the current [0, tmax]) or, with tr.any, occlusion within
@@ -214,41 +216,54 @@ __device__ __forceinline__ bool trav_pop(int* __restrict__ stk, int stride, Trav
   return false;
 }
 
+__device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb) {
+  const bool sw = db < da;
+  const float td = sw ? db : da, tr = sw ? rb : ra;
+  db = sw ? da : db;
+  rb = sw ? ra : rb;
+  da = td;
+  ra = tr;
+}
+
 template <bool STATS>
 __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, int* __restrict__ stk, int stride, Trav& tr,
                                           Counters& ct) {
   const float kRobust = 1.0000005f;
-  const float4 a = nodes[tr.node].a;
-  const float4 b = nodes[tr.node].b;
-  const float4 c = nodes[tr.node].c;
-  const int4 e = nodes[tr.node].e;
+  const DNode* nd = nodes + tr.node;
+  const float4 lx = nd->lox, hx = nd->hix, ly = nd->loy, hy = nd->hiy, lz = nd->loz, hz = nd->hiz;
+  const int4 rf = nd->ref;
   if (STATS) ct.nodes++;
   const float3 o = tr.o, inv = tr.inv;
   const float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
-  float l0x = fmaf(a.x, inv.x, -oi.x), h0x = fmaf(a.y, inv.x, -oi.x);
-  float l0y = fmaf(a.z, inv.y, -oi.y), h0y = fmaf(a.w, inv.y, -oi.y);
-  float l0z = fmaf(c.x, inv.z, -oi.z), h0z = fmaf(c.y, inv.z, -oi.z);
-  float l1x = fmaf(b.x, inv.x, -oi.x), h1x = fmaf(b.y, inv.x, -oi.x);
-  float l1y = fmaf(b.z, inv.y, -oi.y), h1y = fmaf(b.w, inv.y, -oi.y);
-  float l1z = fmaf(c.z, inv.z, -oi.z), h1z = fmaf(c.w, inv.z, -oi.z);
-  float tn0 = fmaxf(fmaxf(fminf(l0x, h0x), fminf(l0y, h0y)), fmaxf(fminf(l0z, h0z), 0.0f));
-  float tf0 = fminf(fminf(fmaxf(l0x, h0x), fmaxf(l0y, h0y)), fminf(fmaxf(l0z, h0z), tr.tmax)) * kRobust;
-  float tn1 = fmaxf(fmaxf(fminf(l1x, h1x), fminf(l1y, h1y)), fmaxf(fminf(l1z, h1z), 0.0f));
-  float tf1 = fminf(fminf(fmaxf(l1x, h1x), fmaxf(l1y, h1y)), fminf(fmaxf(l1z, h1z), tr.tmax)) * kRobust;
-  bool in0 = tn0 <= tf0;
-  bool in1 = tn1 <= tf1;
-  if (in0 && in1) {
-    bool first0 = tn0 <= tn1;
-    stk[tr.sp * stride] = first0 ? e.y : e.x;
-    ++tr.sp;
-    tr.node = first0 ? e.x : e.y;
-  } else if (in0) {
-    tr.node = e.x;
-  } else if (in1) {
-    tr.node = e.y;
-  } else {
-    return trav_pop(stk, stride, tr);
+  const float kMiss = 3.0e38f;
+  float d[4];
+  const float* LX = &lx.x; const float* HX = &hx.x; const float* LY = &ly.x;
+  const float* HY = &hy.x; const float* LZ = &lz.x; const float* HZ = &hz.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float ax = fmaf(LX[k], inv.x, -oi.x), bx = fmaf(HX[k], inv.x, -oi.x);
+    float ay = fmaf(LY[k], inv.y, -oi.y), by = fmaf(HY[k], inv.y, -oi.y);
+    float az = fmaf(LZ[k], inv.z, -oi.z), bz = fmaf(HZ[k], inv.z, -oi.z);
+    float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
+    float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tr.tmax)) * kRobust;
+    d[k] = tn <= tf ? tn : kMiss;
   }
+  int r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
+  float d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3];
+  // near-first order: 5-exchange sorting network on the entry distances
+  cswap(d0, r0, d1, r1);
+  cswap(d2, r2, d3, r3);
+  cswap(d0, r0, d2, r2);
+  cswap(d1, r1, d3, r3);
+  cswap(d1, r1, d2, r2);
+  if (d0 == kMiss) return trav_pop(stk, stride, tr);
+  // push the farther hits (farthest first), continue with the nearest
+  int sp = tr.sp;
+  if (d3 != kMiss) stk[(sp++) * stride] = r3;
+  if (d2 != kMiss) stk[(sp++) * stride] = r2;
+  if (d1 != kMiss) stk[(sp++) * stride] = r1;
+  tr.sp = sp;
+  tr.node = r0;
   return false;
 }
 
@@ -440,8 +455,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             float cosL = dot(dv, ld3(Lt.dir));
             float sq = dot(dv, dv);
             dist = sqrtf(sq);
-            wi = dv * (1.0f / dist);
-            pdf = sq / (Lt.area * fabsf(cosL));  // unnormalised d.dir, as the reference
+            wi = dv * rcp(dist);
+            pdf = sq * rcp(Lt.area * fabsf(cosL));  // unnormalised d.dir, as the reference
             lit = cosL < 0.0f;
           } else if (Lt.type == 1) {  // InfiniteHemisphereLight (light.cpp:34-42)
             float r1 = ptrng::draw(rbase, rdim++);
@@ -454,7 +469,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           } else if (Lt.type == 2) {  // PointLight (light.cpp:49-57)
             float3 dv = ld3(Lt.pos) - hp;
             dist = sqrtf(dot(dv, dv));
-            wi = dv * (1.0f / dist);
+            wi = dv * rcp(dist);
             pdf = 1.0f;
           } else {  // DirectionalLight (light.cpp:17-23)
             wi = ld3(Lt.dir);
@@ -468,7 +483,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           float cos_t = fmaxf(0.0f, fr.to_local(wi).z);
           if (!(cos_t > 0.0f)) continue;
           float3 f = ld3(B.a) * 0.31830988618379067f;
-          pend = mul(mul(T, ld3(Lt.rad) * (cos_t / pdf)), f) * scale;
+          pend = mul(mul(T, ld3(Lt.rad) * (cos_t * rcp(pdf))), f) * scale;
           // shadow ray (pathtracer.cpp:497-504): delta lights offset EPS_N along n
           float3 so = delta ? hp + ns * 5e-3f : offset_ray(hp, dot(wi, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng);
           trav_init(tr, so, wi, dist * 0.999f, true);
@@ -539,7 +554,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             finish = true;
           } else {
             if (DBG && pix == P.dbg_pix) printf("    bounce wi=(%.6g %.6g %.6g) pdf %.5g p %.4g dim %u\n", wi.x, wi.y, wi.z, pdf, pterm, rdim);
-            T = mul(T, f * (fabsf(wi.z) / (pdf * (1.0f - pterm))));
+            T = mul(T, f * (fabsf(wi.z) * rcp(pdf * (1.0f - pterm))));
             float3 v = normalize(fr.to_world(wi));
             trav_init(tr, offset_ray(hp, dot(v, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng), v, 3.0e38f, false);
             includeLe = B.type == 1 || B.type == 2 || B.type == 3;
@@ -627,8 +642,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         rdim = 0;
         float ry = ptrng::draw(rbase, rdim++);  // UniformGridSampler2D draws y first
         float rx = ptrng::draw(rbase, rdim++);
-        float fx = ((float)px + rx) / (float)P.W;
-        float fy = ((float)py + ry) / (float)P.H;
+        float fx = ((float)px + rx) * P.inv_w;
+        float fy = ((float)py + ry) * P.inv_h;
         float3 sp = f3((0.5f - fx) * P.cam_ax, (0.5f - fy) * P.cam_ay, 1.0f);
         float3 wsp = ld3(P.c2w_col0) * sp.x + ld3(P.c2w_col1) * sp.y + ld3(P.c2w_col2) * sp.z;
         float3 d = normalize(f3(0, 0, 0) - wsp);
