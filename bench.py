@@ -141,8 +141,10 @@ def main():
                        frame, tiles, rank, world)
         return dev.stats()
 
-    # counters for the roofline's algorithmic bytes (deterministic: same work as every step)
-    st_counts = step(stats=True)
+    # counters for the roofline's algorithmic bytes: the reference's binary BVH
+    # (SURVEY.md §8(d) cost model); and the launch's own counters (4-wide BVH)
+    st_counts = step(stats="ref")
+    st_perf = step(stats=True)
     for _ in range(args.warmup):
         frame.zero_()
         step()
@@ -197,11 +199,11 @@ def main():
                          "resolve_ms": round(float(np.mean(resolve_ms)), 4),
                          "algorithmic_bytes_per_launch": bytes_launch},
             "counters": {k: st_counts[k] for k in ("camera_rays", "bounce_rays", "shadow_rays", "node_visits",
-                                                   "tri_tests", "sphere_tests", "ext_hits", "wave_trav_steps",
-                                                   "wave_rounds", "culled_samples", "queue_atomics", "shade_clocks",
-                                                   "trav_clocks", "max_wave_clocks", "wave_wall_sum",
-                                                   "wave_wall_max", "hitshade_clocks", "leaf_steps")},
-            "traversal_simd_efficiency": round(st_counts["node_visits"] / max(1, 64 * st_counts["wave_trav_steps"]), 4),
+                                                   "tri_tests", "sphere_tests", "ext_hits", "culled_samples")},
+            "launch_counters": {k: st_perf[k] for k in ("node_visits", "tri_tests", "sphere_tests", "wave_trav_steps",
+                                                        "leaf_steps", "wave_rounds", "queue_atomics", "shade_clocks",
+                                                        "hitshade_clocks", "trav_clocks", "max_wave_clocks",
+                                                        "wave_wall_sum", "wave_wall_max")},
             "launch": {"grid_blocks": s["grid_blocks"], "block": 64, "blocks_per_cu_query": s["blocks_per_cu"]},
             "image_mean": float(img.mean()),
         }

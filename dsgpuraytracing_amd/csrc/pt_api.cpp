@@ -78,6 +78,7 @@ struct pt_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   DevBuf<DNode> nodes;
+  DevBuf<DNode2> nodes2;  // binary tree for PT_FLAG_REF_COUNTS
   DevBuf<DPrim> prims;
   DevBuf<float> norms;
   DevBuf<DBsdf> bsdfs;
@@ -143,6 +144,7 @@ int pt_destroy(pt_ctx* c) {
   if (!c) return PT_OK;
   (void)hipSetDevice(c->device);
   c->nodes.release();
+  c->nodes2.release();
   c->prims.release();
   c->norms.release();
   c->bsdfs.release();
@@ -422,6 +424,16 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
     d.area = L.area;
   }
 
+  std::vector<DNode2> d2(b2.size());
+  for (size_t i = 0; i < b2.size(); ++i) {
+    const B2& q = b2[i];
+    d2[i].a = make_float4(q.lo[0][0], q.hi[0][0], q.lo[0][1], q.hi[0][1]);
+    d2[i].b = make_float4(q.lo[1][0], q.hi[1][0], q.lo[1][1], q.hi[1][1]);
+    d2[i].c = make_float4(q.lo[0][2], q.hi[0][2], q.lo[1][2], q.hi[1][2]);
+    d2[i].e = make_int4(q.ref[0], q.ref[1], 0, 0);
+  }
+  HIPCHK(c->nodes2.reserve(d2.size()));
+  HIPCHK(hipMemcpy(c->nodes2.p, d2.data(), d2.size() * sizeof(DNode2), hipMemcpyHostToDevice));
   HIPCHK(c->nodes.reserve(dn.size()));
   HIPCHK(c->prims.reserve(prims.size()));
   HIPCHK(c->norms.reserve(norms.size()));
@@ -525,7 +537,7 @@ static void screen_footprint(const pt_ctx* c, KParams& P) {
 }
 
 static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStream_t s, uint32_t flags) {
-  const bool stats = (flags & PT_FLAG_STATS) != 0;
+  const bool stats = (flags & (PT_FLAG_STATS | PT_FLAG_REF_COUNTS)) != 0;
   std::memset(&c->last, 0, sizeof(c->last));
   if (tl.empty()) return PT_OK;
   // the tile list rarely changes between frames: upload it only when it does
@@ -560,6 +572,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.n_bsdfs = c->n_bsdfs;
   P.n_tiles = (int)tl.size();
   P.nodes = c->nodes.p;
+  P.nodes2 = c->nodes2.p;
   P.prims = c->prims.p;
   P.norms = c->norms.p;
   P.bsdfs = c->bsdfs.p;
@@ -644,7 +657,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   int64_t max_grid = std::max<int64_t>(1, (slots + PT_BLOCK - 1) / PT_BLOCK);
   int grid = (int)std::min<int64_t>(want, max_grid);
   HIPCHK(hipEventRecord(c->ev0, s));
-  HIPCHK(ptk_launch_render(&P, grid, stats, s));
+  HIPCHK(ptk_launch_render(&P, grid, stats, (flags & PT_FLAG_REF_COUNTS) != 0, s));
   HIPCHK(hipEventRecord(c->ev1, s));
   HIPCHK(ptk_launch_resolve(&P, s));
   HIPCHK(hipEventRecord(c->ev2, s));
@@ -664,7 +677,7 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags) {
   c->last.last_ms = ms;
   HIPCHK(hipEventElapsedTime(&ms, c->ev1, c->ev2));
   c->last.resolve_ms = ms;
-  if (flags & PT_FLAG_STATS) {
+  if (flags & (PT_FLAG_STATS | PT_FLAG_REF_COUNTS)) {
     unsigned long long v[32] = {0};
     HIPCHK(hipMemcpy(v, c->stats.p, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     c->last.camera_rays = (int64_t)v[0];

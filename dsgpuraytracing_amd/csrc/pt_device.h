@@ -41,6 +41,16 @@ struct alignas(16) DNode {
   int4 pad;
 };
 
+// Binary node of the reference topology, 64 B: both child boxes + child
+// references (as DNode.ref).  Only traversed by the reference-count launch
+// (PT_FLAG_REF_COUNTS), whose node visits feed SURVEY.md §8(d)'s cost model.
+//  a = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y), b = the same for c1,
+//  c = (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z), e = (c0 ref, c1 ref, 0, 0)
+struct alignas(16) DNode2 {
+  float4 a, b, c;
+  int4 e;
+};
+
 // Primitive, 48 B.  Triangle: v0 = (p1, meta), e1 = p2-p1, e2 = p3-p1.
 // Sphere: v0 = (o, meta), e1 = (r, r*r, 0, 0).  meta = (bsdf << 1) | is_triangle.
 struct alignas(16) DPrim {
@@ -80,6 +90,7 @@ struct KParams {
   int group_spp;   // samples per work slot (a slot is one pixel's sample group)
   int n_groups;    // ceil(spp / group_spp): slots per pixel
   const DNode* nodes;
+  const DNode2* nodes2;  // the binary tree (reference-count launch only)
   const DPrim* prims;
   const float* norms;  // 9 floats per primitive (vertex normals n1,n2,n3)
   const DBsdf* bsdfs;
@@ -98,7 +109,7 @@ struct KParams {
   int cull_x0, cull_y0, cull_x1, cull_y1;  // pixels outside [x0,x1]x[y0,y1] see no geometry
 };
 
-extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, hipStream_t s);
+extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, bool ref_counts, hipStream_t s);
 extern "C" hipError_t ptk_launch_resolve(const KParams* P, hipStream_t s);
 extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prims, const float* o, const float* d,
                                            const float* maxt, int64_t n, int32_t* hit, float* t, int32_t* prim,

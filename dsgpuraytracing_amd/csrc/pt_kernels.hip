@@ -48,6 +48,13 @@ __device__ __forceinline__ float3 cross(float3 u, float3 v) {
 // replaces a ~10-instruction correctly rounded sequence.
 __device__ __forceinline__ float3 normalize(float3 v) { return v * __builtin_amdgcn_rsqf(dot(v, v)); }
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+// sin / cos of 2*pi*x for x in [0, 1) (v_sin_f32 / v_cos_f32 take revolutions)
+__device__ __forceinline__ float sin_rev(float x) { return __builtin_amdgcn_sinf(x); }
+__device__ __forceinline__ float cos_rev(float x) { return __builtin_amdgcn_cosf(x); }
+
+// Conservative slab-test factor on the far distance (Ize 2013: 1 + 2*gamma_3
+// for exact reciprocals), with margin for the ~1-ulp v_rcp_f32 of 1/d.
+#define PT_ROBUST 1.0000008f
 __device__ __forceinline__ float illum(float3 s) { return 0.2126f * s.x + 0.7152f * s.y + 0.0722f * s.z; }
 __device__ __forceinline__ float3 ld3(const float* p) { return f3(p[0], p[1], p[2]); }
 __device__ __forceinline__ void store3(float* p, float3 v) {
@@ -135,7 +142,7 @@ __device__ __forceinline__ void trav_init(Trav& tr, float3 o, float3 d, float tm
                  fabsf(d.z) < kTiny ? copysignf(kTiny, d.z) : d.z);
   tr.o = o;
   tr.d = d;
-  tr.inv = f3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
+  tr.inv = f3(rcp(dd.x), rcp(dd.y), rcp(dd.z));
   tr.tmax = tmax;
   tr.node = 0;
   tr.sp = 0;
@@ -228,7 +235,7 @@ __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb) {
 template <bool STATS>
 __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, int* __restrict__ stk, int stride, Trav& tr,
                                           Counters& ct) {
-  const float kRobust = 1.0000005f;
+  const float kRobust = PT_ROBUST;
   const DNode* nd = nodes + tr.node;
   const float4 lx = nd->lox, hx = nd->hix, ly = nd->loy, hy = nd->hiy, lz = nd->loz, hz = nd->hiz;
   const int4 rf = nd->ref;
@@ -264,6 +271,45 @@ __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, int* 
   if (d1 != kMiss) stk[(sp++) * stride] = r1;
   tr.sp = sp;
   tr.node = r0;
+  return false;
+}
+
+// Binary node step over the reference topology (reference-count launch).
+template <bool STATS>
+__device__ __forceinline__ bool node_step2(const DNode2* __restrict__ nodes, int* __restrict__ stk, int stride,
+                                           Trav& tr, Counters& ct) {
+  const float kRobust = PT_ROBUST;
+  const float4 a = nodes[tr.node].a;
+  const float4 b = nodes[tr.node].b;
+  const float4 c = nodes[tr.node].c;
+  const int4 e = nodes[tr.node].e;
+  if (STATS) ct.nodes++;
+  const float3 o = tr.o, inv = tr.inv;
+  const float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+  float l0x = fmaf(a.x, inv.x, -oi.x), h0x = fmaf(a.y, inv.x, -oi.x);
+  float l0y = fmaf(a.z, inv.y, -oi.y), h0y = fmaf(a.w, inv.y, -oi.y);
+  float l0z = fmaf(c.x, inv.z, -oi.z), h0z = fmaf(c.y, inv.z, -oi.z);
+  float l1x = fmaf(b.x, inv.x, -oi.x), h1x = fmaf(b.y, inv.x, -oi.x);
+  float l1y = fmaf(b.z, inv.y, -oi.y), h1y = fmaf(b.w, inv.y, -oi.y);
+  float l1z = fmaf(c.z, inv.z, -oi.z), h1z = fmaf(c.w, inv.z, -oi.z);
+  float tn0 = fmaxf(fmaxf(fminf(l0x, h0x), fminf(l0y, h0y)), fmaxf(fminf(l0z, h0z), 0.0f));
+  float tf0 = fminf(fminf(fmaxf(l0x, h0x), fmaxf(l0y, h0y)), fminf(fmaxf(l0z, h0z), tr.tmax)) * kRobust;
+  float tn1 = fmaxf(fmaxf(fminf(l1x, h1x), fminf(l1y, h1y)), fmaxf(fminf(l1z, h1z), 0.0f));
+  float tf1 = fminf(fminf(fmaxf(l1x, h1x), fmaxf(l1y, h1y)), fminf(fmaxf(l1z, h1z), tr.tmax)) * kRobust;
+  bool in0 = tn0 <= tf0;
+  bool in1 = tn1 <= tf1;
+  if (in0 && in1) {
+    bool first0 = tn0 <= tn1;
+    stk[tr.sp * stride] = first0 ? e.y : e.x;
+    ++tr.sp;
+    tr.node = first0 ? e.x : e.y;
+  } else if (in0) {
+    tr.node = e.x;
+  } else if (in1) {
+    tr.node = e.y;
+  } else {
+    return trav_pop(stk, stride, tr);
+  }
   return false;
 }
 
@@ -314,7 +360,7 @@ __device__ __forceinline__ bool box_hit(const Trav& tr, const float* lo, const f
   float ly = fmaf(lo[1], tr.inv.y, -oi.y), hy = fmaf(hi[1], tr.inv.y, -oi.y);
   float lz = fmaf(lo[2], tr.inv.z, -oi.z), hz = fmaf(hi[2], tr.inv.z, -oi.z);
   float tn = fmaxf(fmaxf(fminf(lx, hx), fminf(ly, hy)), fmaxf(fminf(lz, hz), 0.0f));
-  float tf = fminf(fminf(fmaxf(lx, hx), fmaxf(ly, hy)), fminf(fmaxf(lz, hz), tr.tmax)) * 1.0000005f;
+  float tf = fminf(fminf(fmaxf(lx, hx), fmaxf(ly, hy)), fminf(fmaxf(lz, hz), tr.tmax)) * PT_ROBUST;
   return tn <= tf;
 }
 
@@ -325,7 +371,8 @@ enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 #ifndef PT_MIN_WAVES_PER_SIMD
 #define PT_MIN_WAVES_PER_SIMD 4
 #endif
-template <bool STATS, bool DBG>
+// BIN: the reference-count variant, traversing the binary tree (P.nodes2).
+template <bool STATS, bool DBG, bool BIN = false>
 __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel(KParams P) {
   __shared__ int s_stack[PT_STACK * PT_BLOCK];
   int* stk = s_stack + threadIdx.x;
@@ -462,8 +509,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             float r1 = ptrng::draw(rbase, rdim++);
             float r2 = ptrng::draw(rbase, rdim++);
             float st = sqrtf(fmaxf(0.0f, 1.0f - r1 * r1));
-            float ph = 6.28318530717958647f * r2;
-            wi = f3(st * cosf(ph), r1, -st * sinf(ph));
+            wi = f3(st * cos_rev(r2), r1, -st * sin_rev(r2));  // phi = 2 pi r2
             dist = 3.0e38f;
             pdf = 0.15915494309189535f;
           } else if (Lt.type == 2) {  // PointLight (light.cpp:49-57)
@@ -507,8 +553,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             float r2 = ptrng::draw(rbase, rdim++);
             float ct = sqrtf(1.0f - r1);  // cos(acos(1 - 2 r1) / 2)
             float stt = sqrtf(r1);
-            float ph = 6.28318530717958647f * r2;
-            wi = f3(stt * cosf(ph), stt * sinf(ph), ct);
+            wi = f3(stt * cos_rev(r2), stt * sin_rev(r2), ct);  // phi = 2 pi r2
             pdf = ct * 0.31830988618379067f;
             f = B.type == 0 ? ld3(B.a) * 0.31830988618379067f : f3(0, 0, 0);
           } else if (B.type == 1) {  // MirrorBSDF::sample_f (bsdf.cpp:60-69)
@@ -691,7 +736,10 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if (at_leaf) done = leaf_step<STATS>(P.prims, stk, PT_BLOCK, tr, ct);
         if (STATS) n_leafit += lane == 0;
       } else {
-        if (trav && !at_leaf) done = node_step<STATS>(P.nodes, stk, PT_BLOCK, tr, ct);
+        if (trav && !at_leaf) {
+          if constexpr (BIN) done = node_step2<STATS>(P.nodes2, stk, PT_BLOCK, tr, ct);
+          else done = node_step<STATS>(P.nodes, stk, PT_BLOCK, tr, ct);
+        }
       }
       if (done) mode = M_SHADE;
       unsigned long long ready = __ballot(mode == M_SHADE);
@@ -770,8 +818,10 @@ __global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __rest
 }  // namespace ptk
 
 // ------------------------------------------------------------------ launchers
-extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, hipStream_t s) {
-  if (P->dbg_pix >= 0)
+extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, bool ref_counts, hipStream_t s) {
+  if (ref_counts)
+    hipLaunchKernelGGL((ptk::render_kernel<true, false, true>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+  else if (P->dbg_pix >= 0)
     hipLaunchKernelGGL((ptk::render_kernel<false, true>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
   else if (stats)
     hipLaunchKernelGGL((ptk::render_kernel<true, false>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);

@@ -22,6 +22,7 @@ PT_E_NOSCENE = -3
 PT_E_ALLOC = -4
 PT_E_IO = -5
 PT_FLAG_STATS = 1
+PT_FLAG_REF_COUNTS = 2
 
 PRIM_SPHERE, PRIM_TRIANGLE = 0, 1
 BSDF_DIFFUSE, BSDF_MIRROR, BSDF_REFRACTION, BSDF_GLASS, BSDF_EMISSION = range(5)

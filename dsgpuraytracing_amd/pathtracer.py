@@ -33,6 +33,14 @@ from .native import check, lib
 TILE = 32  # imageTileSize (pathtracer.cpp:57)
 
 
+def _flags(stats) -> int:
+    """stats=True: counters of the launch itself; stats="ref": counters of the
+    reference's binary BVH (PT_FLAG_REF_COUNTS, SURVEY.md §8(d) cost model)."""
+    if stats == "ref":
+        return native.PT_FLAG_REF_COUNTS
+    return native.PT_FLAG_STATS if stats else 0
+
+
 class Device:
     """One pt_ctx on one GPU (CUDAPathTracer's device state, setup.h:90-148)."""
 
@@ -80,12 +88,12 @@ class Device:
     def render_tiles(self, tiles, out: np.ndarray, stats: bool = False):
         assert out.dtype == np.float32 and out.flags.c_contiguous
         keep, arr = self._tiles(tiles)
-        flags = native.PT_FLAG_STATS if stats else 0
+        flags = _flags(stats)
         check(self._lib.pt_render_tiles(self.handle, arr, len(keep), out.ctypes.data, flags))
 
     def render_tiles_device(self, tiles, out_ptr: int, stream: int = 0, stats: bool = False):
         keep, arr = self._tiles(tiles)
-        flags = native.PT_FLAG_STATS if stats else 0
+        flags = _flags(stats)
         check(self._lib.pt_render_tiles_device(self.handle, arr, len(keep), ctypes.c_void_p(out_ptr),
                                                ctypes.c_void_p(stream or None), flags))
 

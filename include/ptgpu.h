@@ -171,6 +171,8 @@ typedef struct pt_stats {
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */
+#define PT_FLAG_REF_COUNTS 2u /* as PT_FLAG_STATS, but traverse the reference's binary BVH so node_visits
+                                 and primitive tests follow SURVEY.md §8(d)'s reference-layout cost model */
 
 int pt_create(int device, pt_ctx** out);
 int pt_destroy(pt_ctx* ctx);

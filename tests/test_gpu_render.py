@@ -190,6 +190,12 @@ def test_hip_stats_counters():
     assert st["node_visits"] > st["camera_rays"]
     assert st["shadow_rays"] > 0 and st["bounce_rays"] > 0 and st["sphere_tests"] > 0
     assert st["last_ms"] > 0
+    # reference-layout counts (binary BVH): same rays, more (smaller) node visits
+    _, ref = gpu_render("c1_default_64x64", 64, 64, 2, stats="ref")
+    assert ref["counters_valid"] == 1
+    assert ref["camera_rays"] == st["camera_rays"]
+    assert abs(ref["shadow_rays"] - st["shadow_rays"]) <= 0.001 * st["shadow_rays"]
+    assert ref["node_visits"] > st["node_visits"]
 
 
 def test_hip_error_paths():
