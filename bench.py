@@ -52,17 +52,35 @@ def algorithmic_bytes(st: dict) -> float:
             + 36.0 * st["ext_hits"] + 12.0 * st["pixels"])
 
 
-def measured_traffic():
+def measured_traffic(workload: str):
     """HBM bytes per launch of the render kernel on this workload, from the
-    rocprofv3 PMC passes committed under profiles/ (FETCH_SIZE doubled per the
-    gfx950 correction of MI355X_MICROARCH.md §HBM, + WRITE_SIZE; KB -> bytes).
-    None when no summary for this workload is committed."""
+    rocprofv3 PMC passes committed under profiles/ (tools/profile_summary.py:
+    FETCH_SIZE doubled per the gfx950 correction of MI355X_MICROARCH.md §HBM,
+    + WRITE_SIZE; KB -> bytes).  None when no summary for this workload is
+    committed."""
     p = os.path.join(ROOT, "profiles", "latest_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
+        return d.get("hbm_bytes_per_launch") if d.get("workload") == workload else None
     except (OSError, ValueError):
+        return None
+
+
+def measured_pmc(workload: str):
+    """Issue/latency view of the render kernel from the committed PMC summary
+    (informational: the kernel is latency- and issue-bound, not HBM-bound)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "latest_traffic.json")) as f:
+            src = json.load(f)["source"]
+        with open(os.path.join(ROOT, src)) as f:
+            d = json.load(f)
+        if d.get("workload") != workload:
+            return None
+        keys = ("avg_ms", "hbm_gbs", "l2_hit_rate", "valu_issue_util", "sq_wait_any_frac", "sq_wait_inst_any_frac",
+                "sq_active_inst_any_frac")
+        return {k: (round(d[k], 4) if isinstance(d.get(k), float) else d.get(k)) for k in keys} | {"source": src}
+    except (OSError, ValueError, KeyError):
         return None
 
 
@@ -194,17 +212,19 @@ def main():
                        "parallelism": f"tiles{world}" if world > 1 else "single",
                        "render_time_s": round(elapsed / frames, 4), "scene_load_s": round(t_load, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": measured_traffic(),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": measured_traffic(args.workload),
                          "kernel": "render_kernel<false>", "kernel_ms": round(avg_ms, 3),
                          "resolve_ms": round(float(np.mean(resolve_ms)), 4),
-                         "algorithmic_bytes_per_launch": bytes_launch},
+                         "algorithmic_bytes_per_launch": bytes_launch,
+                         "pmc": measured_pmc(args.workload)},
             "counters": {k: st_counts[k] for k in ("camera_rays", "bounce_rays", "shadow_rays", "node_visits",
                                                    "tri_tests", "sphere_tests", "ext_hits", "culled_samples")},
             "launch_counters": {k: st_perf[k] for k in ("node_visits", "tri_tests", "sphere_tests", "wave_trav_steps",
                                                         "leaf_steps", "wave_rounds", "queue_atomics", "shade_clocks",
                                                         "hitshade_clocks", "trav_clocks", "max_wave_clocks",
                                                         "wave_wall_sum", "wave_wall_max")},
-            "launch": {"grid_blocks": s["grid_blocks"], "block": 64, "blocks_per_cu_query": s["blocks_per_cu"]},
+            "launch": {"grid_blocks": s["grid_blocks"], "block": 64, "blocks_per_cu_query": s["blocks_per_cu"],
+                       "bvh_nodes": s["bvh_nodes"], "bvh_stack": s["bvh_stack"]},
             "image_mean": float(img.mean()),
         }
         rays = st_counts["camera_rays"] + st_counts["bounce_rays"] + st_counts["shadow_rays"]

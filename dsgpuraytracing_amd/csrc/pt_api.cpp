@@ -96,6 +96,7 @@ struct pt_ctx {
   DevBuf<int32_t> q_i;
   int n_lights = 0, n_bsdfs = 0;
   int bvh_stack = 0;  // worst-case traversal stack entries of the uploaded BVH
+  size_t n_nodes4 = 0;
   int64_t n_prims = 0;
   float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
   double root_lo_d[3] = {0, 0, 0}, root_hi_d[3] = {0, 0, 0};
@@ -392,6 +393,7 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
     return fail(PT_E_INVALID, "pt_upload_scene: BVH needs a deeper traversal stack (" + std::to_string(max_stack) +
                                   " > " + std::to_string(PT_STACK) + ")");
   c->bvh_stack = max_stack;
+  c->n_nodes4 = dn.size();
 
   std::vector<DBsdf> bs((size_t)s->n_bsdfs);
   for (int i = 0; i < s->n_bsdfs; ++i) {
@@ -666,6 +668,8 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   int64_t px = 0;
   for (const int4& t : tl) px += (int64_t)t.z * t.w;
   c->last.pixels = px;
+  c->last.bvh_stack = c->bvh_stack;
+  c->last.bvh_nodes = (int64_t)c->n_nodes4;
   c->last.samples = px * c->params.spp;
   return PT_OK;
 }

@@ -48,6 +48,8 @@ __device__ __forceinline__ float3 cross(float3 u, float3 v) {
 // replaces a ~10-instruction correctly rounded sequence.
 __device__ __forceinline__ float3 normalize(float3 v) { return v * __builtin_amdgcn_rsqf(dot(v, v)); }
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+// v_sqrt_f32 (about 1 ulp) for sampling; the sphere test keeps sqrtf
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 // sin / cos of 2*pi*x for x in [0, 1) (v_sin_f32 / v_cos_f32 take revolutions)
 __device__ __forceinline__ float sin_rev(float x) { return __builtin_amdgcn_sinf(x); }
 __device__ __forceinline__ float cos_rev(float x) { return __builtin_amdgcn_cosf(x); }
@@ -501,20 +503,20 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             float3 dv = ld3(Lt.pos) + ld3(Lt.dimx) * sx + ld3(Lt.dimy) * sy - hp;
             float cosL = dot(dv, ld3(Lt.dir));
             float sq = dot(dv, dv);
-            dist = sqrtf(sq);
+            dist = fsqrt(sq);
             wi = dv * rcp(dist);
             pdf = sq * rcp(Lt.area * fabsf(cosL));  // unnormalised d.dir, as the reference
             lit = cosL < 0.0f;
           } else if (Lt.type == 1) {  // InfiniteHemisphereLight (light.cpp:34-42)
             float r1 = ptrng::draw(rbase, rdim++);
             float r2 = ptrng::draw(rbase, rdim++);
-            float st = sqrtf(fmaxf(0.0f, 1.0f - r1 * r1));
+            float st = fsqrt(fmaxf(0.0f, 1.0f - r1 * r1));
             wi = f3(st * cos_rev(r2), r1, -st * sin_rev(r2));  // phi = 2 pi r2
             dist = 3.0e38f;
             pdf = 0.15915494309189535f;
           } else if (Lt.type == 2) {  // PointLight (light.cpp:49-57)
             float3 dv = ld3(Lt.pos) - hp;
-            dist = sqrtf(dot(dv, dv));
+            dist = fsqrt(dot(dv, dv));
             wi = dv * rcp(dist);
             pdf = 1.0f;
           } else {  // DirectionalLight (light.cpp:17-23)
@@ -551,8 +553,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           if (B.type == 0 || B.type == 4) {  // cosine hemisphere (sampler.cpp:44-55)
             float r1 = ptrng::draw(rbase, rdim++);
             float r2 = ptrng::draw(rbase, rdim++);
-            float ct = sqrtf(1.0f - r1);  // cos(acos(1 - 2 r1) / 2)
-            float stt = sqrtf(r1);
+            float ct = fsqrt(1.0f - r1);  // cos(acos(1 - 2 r1) / 2)
+            float stt = fsqrt(r1);
             wi = f3(stt * cos_rev(r2), stt * sin_rev(r2), ct);  // phi = 2 pi r2
             pdf = ct * 0.31830988618379067f;
             f = B.type == 0 ? ld3(B.a) * 0.31830988618379067f : f3(0, 0, 0);
@@ -568,7 +570,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             }
             float cos2 = 1.0f - ratio * ratio * (1.0f - wo.z * wo.z);
             bool tir = cos2 < 0.0f;
-            wi = tir ? f3(-wo.x, -wo.y, wo.z) : normalize(f3(-wo.x * ratio, -wo.y * ratio, sgn * sqrtf(cos2)));
+            wi = tir ? f3(-wo.x, -wo.y, wo.z) : normalize(f3(-wo.x * ratio, -wo.y * ratio, sgn * fsqrt(cos2)));
             float ni = B.ior, no = 1.0f;
             if (wo.z < 0.0f) {
               ni = 1.0f;

@@ -86,7 +86,8 @@ class pt_stats(ctypes.Structure):
                 ("culled_samples", c_int64), ("queue_atomics", c_int64),
                 ("shade_clocks", c_int64), ("trav_clocks", c_int64),
                 ("max_wave_clocks", c_int64), ("wave_wall_sum", c_int64), ("wave_wall_max", c_int64),
-                ("leaf_steps", c_int64), ("hitshade_clocks", c_int64), ("resolve_ms", c_double)]
+                ("leaf_steps", c_int64), ("hitshade_clocks", c_int64), ("resolve_ms", c_double),
+                ("bvh_stack", c_int32), ("bvh_nodes", c_int64)]
 
 
 # Every symbol include/ptgpu.h and include/ptgpu_scene.h declare, with ctypes signatures.

@@ -1,0 +1,91 @@
+"""Summarise a rocprofv3 profiling session of bench.py into profiles/<round>/.
+
+Reads the passes written by tools/profile_session.sh under gpurun_out/prof/:
+  kt/     --kernel-trace --stats      (per-kernel average duration)
+  fetch/  --pmc FETCH_SIZE            (KB; doubled per MI355X_MICROARCH.md §HBM)
+  write/  --pmc WRITE_SIZE            (KB)
+  sq/     --pmc SQ_*                  (quad-cycle units for *_CYCLES / WAIT / ACTIVE)
+  tcc/    --pmc TCC_HIT_sum TCC_MISS_sum
+and writes <out>/<workload>_kernel_stats.csv, <out>/<workload>_summary.json and
+profiles/latest_traffic.json (read by bench.py for roofline.traffic).
+Usage: python tools/profile_summary.py <workload> <out_dir> [prof_dir]
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+KERNEL = "render_kernel<false, false, false>"
+
+
+def _pmc(path):
+    agg = collections.defaultdict(list)
+    if not os.path.exists(path):
+        return {}
+    for r in csv.DictReader(open(path)):
+        if KERNEL in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    workload, out = sys.argv[1], sys.argv[2]
+    prof = sys.argv[3] if len(sys.argv) > 3 else "gpurun_out/prof"
+    os.makedirs(out, exist_ok=True)
+    ks = os.path.join(prof, "kt", "kt_kernel_stats.csv")
+    shutil.copy(ks, os.path.join(out, f"{workload}_kernel_stats.csv"))
+    stats = {r["Name"]: r for r in csv.DictReader(open(ks))}
+    render = next(v for k, v in stats.items() if KERNEL in k)
+    resolve = next((v for k, v in stats.items() if "resolve_kernel" in k), None)
+    fetch = _pmc(os.path.join(prof, "fetch", "fetch_counter_collection.csv"))
+    write = _pmc(os.path.join(prof, "write", "write_counter_collection.csv"))
+    sq = _pmc(os.path.join(prof, "sq", "sq_counter_collection.csv"))
+    tcc = _pmc(os.path.join(prof, "tcc", "tcc_counter_collection.csv"))
+    for name, d in (("fetch", fetch), ("write", write), ("sq", sq), ("tcc", tcc)):
+        src = os.path.join(prof, name, f"{name}_counter_collection.csv")
+        if os.path.exists(src):
+            rows = [r for r in csv.DictReader(open(src)) if KERNEL in r["Kernel_Name"]]
+            with open(os.path.join(out, f"{workload}_pmc_{name}.csv"), "w", newline="") as f:
+                w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
+                w.writeheader()
+                w.writerows(rows)
+    avg_ns = float(render["AverageNs"])
+    s = {
+        "workload": workload,
+        "kernel": KERNEL,
+        "calls": int(render["Calls"]),
+        "avg_ms": avg_ns / 1e6,
+        "resolve_avg_ms": float(resolve["AverageNs"]) / 1e6 if resolve else None,
+    }
+    if "FETCH_SIZE" in fetch and "WRITE_SIZE" in write:
+        s["fetch_size_kb"] = fetch["FETCH_SIZE"]
+        s["write_size_kb"] = write["WRITE_SIZE"]
+        s["hbm_bytes_per_launch"] = (2.0 * fetch["FETCH_SIZE"] + write["WRITE_SIZE"]) * 1024.0
+        s["hbm_gbs"] = s["hbm_bytes_per_launch"] / (avg_ns * 1e-9) / 1e9
+    if sq:
+        cyc = avg_ns * 1e-9 * 2.4e9
+        s["sq"] = sq
+        if "SQ_INSTS_VALU" in sq:  # 256 CUs, 2 wave64 VALU issues per CU-cycle (4 SIMD-32)
+            s["valu_issue_util"] = sq["SQ_INSTS_VALU"] / (256 * 2 * cyc)
+        if "SQ_WAVE_CYCLES" in sq:
+            wc = sq["SQ_WAVE_CYCLES"]
+            for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                if k in sq:
+                    s[k.lower() + "_frac"] = sq[k] / wc
+    if tcc:
+        s["tcc"] = tcc
+        if "TCC_HIT_sum" in tcc:
+            s["l2_hit_rate"] = tcc["TCC_HIT_sum"] / (tcc["TCC_HIT_sum"] + tcc["TCC_MISS_sum"])
+    with open(os.path.join(out, f"{workload}_summary.json"), "w") as f:
+        json.dump(s, f, indent=1)
+    if "hbm_bytes_per_launch" in s:
+        with open("profiles/latest_traffic.json", "w") as f:
+            json.dump({"workload": workload, "kernel": KERNEL, "hbm_bytes_per_launch": s["hbm_bytes_per_launch"],
+                       "avg_ms": s["avg_ms"], "source": os.path.join(out, f"{workload}_summary.json")}, f, indent=1)
+    print(json.dumps(s, indent=1))
+
+
+if __name__ == "__main__":
+    main()
