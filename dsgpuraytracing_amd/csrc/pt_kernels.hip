@@ -6,22 +6,22 @@
 //   GPU: traceScenePT -> tracePixelPT -> traceRay (cuda_src/kernel.cu:31-349),
 //        BVH_traversal (traversal.cu:3-222), intersect.cu, bsdf.cu, light.cu
 //
-// Design (MI355X-first, not a translation):
-//  * one persistent megakernel; a lane owns a PIXEL and runs its spp samples in
-//    order (deterministic per-pixel sum, no float atomics, results independent
-//    of tile->GPU assignment);
+// Design (MI355X-first, not a translation; DESIGN.md §4):
+//  * one persistent megakernel, one wave64 per workgroup; a lane owns one
+//    (pixel, sample group) work slot at a time, renders its samples in order
+//    and stores their sum; resolve_kernel sums a pixel's groups in group order
+//    (deterministic, no float atomics, independent of tile->GPU assignment);
 //  * the recursion of trace_ray becomes an iterative throughput loop driven by a
-//    per-lane state machine that emits exactly ONE ray per loop iteration
-//    (extension ray or shadow ray), so every lane of a wave64 traverses in every
-//    iteration; finished lanes refill from a wave-aggregated atomic pixel queue
-//    (one atomic per wave per refill, pixels handed out in 8x8 blocks of 32x32
-//    tiles for primary-ray coherence);
-//  * BVH2 in the reference's topology re-laid out as 64-B two-child-box nodes
-//    (one node fetch = 4 x dwordx4 = both child boxes), leaves referenced by
-//    (start,count) in the parent, triangles as {v0,e1,e2} float4 x3 (48 B) in BVH
-//    order, shading normals in a side array fetched once per hit;
-//  * slab tests via v_min3/v_max3-friendly fminf/fmaxf chains, Moller-Trumbore
-//    triangles, traversal stack per lane in LDS (lane-contiguous, conflict-free);
+//    per-lane state machine that owns exactly ONE ray (extension or shadow);
+//    rounds alternate a shading phase (finished lanes shade and refill from a
+//    wave-chunked atomic queue over footprint-clipped 8x8 pixel blocks) and a
+//    traversal phase that runs until shade_batch lanes are done;
+//  * if-if traversal: each iteration the wave runs either node steps (BVH4,
+//    128-B SoA node, 4 slab tests, sorting-network near-first order) or leaf
+//    steps (two primitives per step, loads issued together), whichever kind
+//    more lanes wait on; leaves are cursors in the child references;
+//  * traversal stack per lane in LDS (lane-contiguous, conflict-free);
+//    material/light tables staged in LDS;
 //  * fp32 throughout; self-intersection handled by the integer-ulp origin offset
 //    (Waechter & Binder, Ray Tracing Gems ch.6) instead of the reference's
 //    EPS_D = 1e-11 double offsets, which are meaningless in fp32.
