@@ -69,7 +69,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if verbose and out:
             sys.stderr.write(out.decode(errors="replace"))
     tmp = LIB + ".tmp"
-    link = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+    link = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-lz"]
     r = subprocess.run(link, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(link)}\n{r.stdout.decode(errors='replace')}")

@@ -108,6 +108,8 @@ _SIGS = {
     "pt_host_scene_view": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "pt_host_scene_dump": (c_int32, [c_void_p, c_char_p]),
     "pt_host_scene_free": (None, [c_void_p]),
+    "pt_host_load_exr": (c_int32, [c_char_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_void_p)]),
+    "pt_host_free": (None, [c_void_p]),
 }
 
 _lib = None

@@ -51,3 +51,18 @@ def load_dae(path: str, width: int, height: int, cam_info: Optional[str] = None)
         p = os.path.join(td, "scene.ptd")
         dump_dae(path, width, height, p, cam_info)
         return ptdump.read(p)
+
+
+def load_exr(path: str) -> np.ndarray:
+    """OpenEXR environment map -> float32 (h, w, 3), row 0 = first scanline,
+    through the native reader (pt_host_load_exr: load_exr, main.cpp:30-67)."""
+    L = native.lib()
+    w, h = ctypes.c_int32(), ctypes.c_int32()
+    p = ctypes.c_void_p()
+    native.check(L.pt_host_load_exr(path.encode(), ctypes.byref(w), ctypes.byref(h), ctypes.byref(p)))
+    try:
+        n = w.value * h.value * 3
+        arr = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_float)), shape=(n,)).copy()
+    finally:
+        L.pt_host_free(p)
+    return arr.reshape(h.value, w.value, 3)

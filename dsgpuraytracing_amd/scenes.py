@@ -106,3 +106,25 @@ if __name__ == "__main__":
     import sys
     for lv in (int(a) for a in sys.argv[1:] or ["1"]):
         print(proxy_path(lv))
+
+
+def synthetic_envmap(width: int = 512, height: int = 256, seed: int = 7) -> np.ndarray:
+    """Deterministic lat-long HDR sky (float32, (height, width, 3), row 0 = +y,
+    the reference's EnvironmentLight convention theta = (y+0.5)/h*pi): a
+    horizon gradient, a darker ground, a small bright sun and low-amplitude
+    seeded noise (CBlucy's map is absent)."""
+    rng = np.random.RandomState(seed)
+    th = (np.arange(height, dtype=np.float64) + 0.5) / height * np.pi       # polar angle from +y
+    ph = (np.arange(width, dtype=np.float64) + 0.5) / width * 2.0 * np.pi
+    T, Pp = np.meshgrid(th, ph, indexing="ij")
+    up = np.cos(T)
+    sky = np.stack([0.35 + 0.25 * (1 - up), 0.45 + 0.2 * (1 - up), 0.9 - 0.1 * (1 - up)], -1) * (up > 0)[..., None]
+    ground = np.stack([0.18, 0.15, 0.12], -1) * np.ones_like(T)[..., None] * (up <= 0)[..., None]
+    # sun at theta = 0.28 pi, phi = 1.3 pi
+    sd = np.stack([np.sin(T) * np.cos(Pp), np.cos(T), np.sin(T) * np.sin(Pp)], -1)
+    s = np.array([np.sin(0.28 * np.pi) * np.cos(1.3 * np.pi), np.cos(0.28 * np.pi), np.sin(0.28 * np.pi) * np.sin(1.3 * np.pi)])
+    cosang = np.clip(sd @ s, -1.0, 1.0)
+    sun = 60.0 * np.exp(-(1.0 - cosang) / 0.0015)[..., None] * np.array([1.0, 0.92, 0.8])
+    noise = 1.0 + 0.08 * rng.standard_normal((height, width, 1))
+    env = (sky + ground) * noise + sun
+    return np.ascontiguousarray(np.maximum(env, 0.0).astype(np.float32))

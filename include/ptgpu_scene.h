@@ -17,6 +17,9 @@
  *   pt_host_scene_view   borrowed pt_scene / pt_camera views of the result
  *   pt_host_scene_dump   PTDUMP file (the oracle's scene interchange format)
  *   pt_host_scene_free   release
+ *   pt_host_load_exr     load_exr (src/main.cpp:30-67) over tinyexr: an OpenEXR
+ *                        environment map as float RGB (scanline; NONE/ZIPS/ZIP;
+ *                        HALF/FLOAT), channels 2,1,0 of the name-sorted list as R,G,B
  *
  * The result is bit-identical to what the reference's own host code builds
  * (primitive order, vertex order, area-weighted normals, BVH topology and
@@ -45,6 +48,11 @@ int pt_host_scene_view(const pt_host_scene* hs, pt_scene* scene, pt_camera* cam)
 /* Writes the flattened scene as a PTDUMP file. */
 int pt_host_scene_dump(const pt_host_scene* hs, const char* path);
 void pt_host_scene_free(pt_host_scene* hs);
+
+/* Reads an OpenEXR file into a malloc'd float RGB array (width*height*3, row 0
+ * = first scanline = +y for lat-long maps); free it with pt_host_free. */
+int pt_host_load_exr(const char* path, int32_t* width, int32_t* height, float** rgb);
+void pt_host_free(void* p);
 
 #ifdef __cplusplus
 }

@@ -15,6 +15,17 @@
 //   dump   : writes the flattened scene the GPU seam would receive (PTDUMP)
 //   rays   : answers BVHAccel::intersect nearest/any-hit queries (KATs)
 //   rng    : prints the first rand() draws and the sampler draw order
+//   exr    : decodes --envmap with the reference's tinyexr + load_exr (main.cpp:30-67)
+//            and writes the HDRImageBuffer (float32 w*h*3) to a PTDUMP
+//   exrw   : writes the PTDUMP "rgb" (w, h) of --in as a ZIP OpenEXR with the
+//            reference's tinyexr (SaveMultiChannelEXRToFile), channels B,G,R,
+//            pixel type --half 0/1 (fixtures for the native EXR loader)
+// --envmap <file.exr> adds the EnvironmentLight exactly as main.cpp -e does:
+// PathTracer(..., envmap) pushes it after the scene's lights (pathtracer.cpp:42-46,88-90).
+// the reference's tinyexr, implemented in this TU as src/main.cpp:4 does
+// (first, so no earlier include of the header swallows the implementation)
+#define TINYEXR_IMPLEMENTATION
+#include "tinyexr.h"
 #include "pathtracer.h"
 #include "bsdf.h"
 #include "camera.h"
@@ -37,16 +48,20 @@
 #include <vector>
 
 #include "ptdump.h"
+#include "static_scene/environment_light.h"
 
 using namespace CMU462;
 using std::string;
 using std::vector;
 
 struct Opts {
-  string scene, mode = "render", out, cam, rays_in;
+  string scene, mode = "render", out, cam, rays_in, envmap, in;
+  int half = 0;
   size_t w = 64, h = 64, spp = 1, depth = 4, lights = 1, threads = 1;
   unsigned seed = 1;
 };
+
+static HDRImageBuffer* g_envmap = nullptr;  // --envmap, owned by the EnvironmentLight
 
 static void die(const char* m) {
   std::fprintf(stderr, "ref_driver: %s\n", m);
@@ -107,6 +122,80 @@ static void build_scene(const Opts& o, Camera& camera, DynamicScene::Scene*& dsc
     camera.place(target, acos(c_dir.y), atan2(c_dir.x, c_dir.z), view_distance,
                  canonical_view_distance / 10.0, canonical_view_distance * 20.0);
   }
+}
+
+// Restatement of load_exr (src/main.cpp:30-67): channels taken by index
+// 2,1,0 of the file's (name-sorted) channel list as R,G,B.
+static HDRImageBuffer* load_exr(const char* file_path) {
+  const char* err;
+  EXRImage exr;
+  InitEXRImage(&exr);
+  int ret = ParseMultiChannelEXRHeaderFromFile(&exr, file_path, &err);
+  if (ret != 0) die("cannot parse EXR header");
+  for (int i = 0; i < exr.num_channels; i++)
+    if (exr.pixel_types[i] == TINYEXR_PIXELTYPE_HALF) exr.requested_pixel_types[i] = TINYEXR_PIXELTYPE_FLOAT;
+  ret = LoadMultiChannelEXRFromFile(&exr, file_path, &err);
+  if (ret != 0) die("cannot load EXR");
+  HDRImageBuffer* envmap = new HDRImageBuffer();
+  envmap->resize(exr.width, exr.height);
+  float* channel_r = (float*)exr.images[2];
+  float* channel_g = (float*)exr.images[1];
+  float* channel_b = (float*)exr.images[0];
+  for (size_t i = 0; i < (size_t)exr.width * exr.height; i++)
+    envmap->data[i] = Spectrum(channel_r[i], channel_g[i], channel_b[i]);
+  return envmap;
+}
+
+static int exr_modes(const Opts& o) {
+  if (o.mode == "exr") {
+    HDRImageBuffer* m = load_exr(o.envmap.c_str());
+    ptdump::Writer w(o.out.c_str());
+    vector<float> rgb(m->w * m->h * 3);
+    for (size_t i = 0; i < m->w * m->h; ++i) {
+      rgb[3 * i] = m->data[i].r;
+      rgb[3 * i + 1] = m->data[i].g;
+      rgb[3 * i + 2] = m->data[i].b;
+    }
+    w.f4("rgb", rgb);
+    w.i8("shape", {(int64_t)m->h, (int64_t)m->w, 3});
+    return 0;
+  }
+  // exrw: PTDUMP {rgb f4 (h*w*3), shape i8 (h, w, 3)} -> ZIP EXR (B, G, R)
+  std::vector<ptdump::Record> R;
+  if (!ptdump::read_all(o.in.c_str(), R)) die("cannot read --in");
+  vector<float> rgb;
+  vector<int64_t> shape;
+  if (!ptdump::get(R, "rgb", rgb) || !ptdump::get(R, "shape", shape) || shape.size() != 3) die("bad --in");
+  int h = (int)shape[0], wd = (int)shape[1];
+  vector<float> ch[3];
+  vector<uint16_t> hch[3];
+  const char* names[3] = {"B", "G", "R"};
+  for (int c = 0; c < 3; ++c) {
+    ch[c].resize((size_t)wd * h);
+    for (size_t i = 0; i < (size_t)wd * h; ++i) ch[c][i] = rgb[3 * i + (2 - c)];
+  }
+  EXRImage img;
+  InitEXRImage(&img);
+  img.num_channels = 3;
+  img.channel_names = names;
+  unsigned char* ptrs[3];
+  int ptype[3], rtype[3];
+  for (int c = 0; c < 3; ++c) {
+    ptype[c] = o.half ? TINYEXR_PIXELTYPE_HALF : TINYEXR_PIXELTYPE_FLOAT;
+    rtype[c] = ptype[c];
+    ptrs[c] = reinterpret_cast<unsigned char*>(ch[c].data());  // float input; converted on save
+  }
+  img.images = ptrs;
+  img.pixel_types = ptype;
+  img.requested_pixel_types = rtype;
+  img.width = wd;
+  img.height = h;
+  if (o.half) {  // tinyexr saves HALF channels from float input data
+    for (int c = 0; c < 3; ++c) ptype[c] = TINYEXR_PIXELTYPE_FLOAT;
+  }
+  const char* err = nullptr;
+  if (SaveMultiChannelEXRToFile(&img, o.out.c_str(), &err) != 0) die(err ? err : "cannot write EXR");
+  return 0;
 }
 
 // Restatement of Application::loadCamera (application.cpp:823-853).
@@ -183,8 +272,13 @@ static void dump_scene(const Opts& o, PathTracer& pt) {
   vector<int32_t> ltype;
   vector<float> lrad, larea;
   vector<double> lgeom;
+  const StaticScene::EnvironmentLight* env = nullptr;
   for (StaticScene::SceneLight* l : pt.scene->lights) {
     int t = l->getType();
+    if (auto* e = dynamic_cast<StaticScene::EnvironmentLight*>(l)) {  // getType() says 1
+      env = e;
+      t = 4;
+    }
     double g[12] = {0};
     Spectrum rad;
     float area = 0;
@@ -193,6 +287,8 @@ static void dump_scene(const Opts& o, PathTracer& pt) {
       rad = d->radiance; g[3] = d->dirToLight.x; g[4] = d->dirToLight.y; g[5] = d->dirToLight.z;
     } else if (t == 1) {
       rad = static_cast<StaticScene::InfiniteHemisphereLight*>(l)->radiance;
+    } else if (t == 4) {
+      // the map travels in env_rgb below
     } else if (t == 2) {
       auto* d = static_cast<StaticScene::PointLight*>(l);
       rad = d->radiance; g[0] = d->position.x; g[1] = d->position.y; g[2] = d->position.z;
@@ -212,6 +308,17 @@ static void dump_scene(const Opts& o, PathTracer& pt) {
   w.f4("light_rad", lrad);
   w.f8("light_geom", lgeom);
   w.f4("light_area", larea);
+  if (env) {
+    const HDRImageBuffer* m = g_envmap;  // the map handed to the PathTracer ctor
+    vector<float> rgb(m->w * m->h * 3);
+    for (size_t i = 0; i < m->w * m->h; ++i) {
+      rgb[3 * i] = m->data[i].r;
+      rgb[3 * i + 1] = m->data[i].g;
+      rgb[3 * i + 2] = m->data[i].b;
+    }
+    w.i8("env_shape", {(int64_t)m->h, (int64_t)m->w});
+    w.f4("env_rgb", rgb);
+  }
 
   const vector<StaticScene::Primitive*>& prims = pt.bvh->primitives;
   vector<int32_t> ptype, pbsdf, porig;
@@ -319,6 +426,9 @@ int main(int argc, char** argv) {
     else if (a == "-l") o.lights = std::stoul(nxt());
     else if (a == "-t") o.threads = std::stoul(nxt());
     else if (a == "--seed") o.seed = (unsigned)std::stoul(nxt());
+    else if (a == "--envmap") o.envmap = nxt();
+    else if (a == "--in") o.in = nxt();
+    else if (a == "--half") o.half = std::stoi(nxt());
     else o.scene = a;
   }
   if (o.mode == "rng") {
@@ -331,12 +441,14 @@ int main(int argc, char** argv) {
     std::printf("sample %.17g %.17g\nrand %d %d\n", s.x, s.y, r0, r1);
     return 0;
   }
+  if (o.mode == "exr" || o.mode == "exrw") return exr_modes(o);
   if (o.scene.empty()) die("no scene");
 
   Camera camera;
   DynamicScene::Scene* dscene = nullptr;
   build_scene(o, camera, dscene);
-  PathTracer* pt = new PathTracer(o.spp, o.depth, o.lights, 1, 1, 1, o.threads, nullptr);
+  g_envmap = o.envmap.empty() ? nullptr : load_exr(o.envmap.c_str());
+  PathTracer* pt = new PathTracer(o.spp, o.depth, o.lights, 1, 1, 1, o.threads, g_envmap);
   pt->useCPU = true;
   // set_up_pathtracer (application.cpp:624-633)
   pt->set_camera(&camera);

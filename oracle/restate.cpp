@@ -27,6 +27,7 @@
 // the reference BVH topology (written by oracle/_ref/ref_driver --mode dump or
 // by the product's native loader).  Compile exactly like the reference
 // (g++ -O3, no -march, no -ffast-math): see oracle/Makefile.
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdint>
@@ -149,7 +150,7 @@ struct Bsdf {
   float ior, rough;
 };
 struct Light {
-  int type;  // 0 directional 1 hemisphere 2 point 3 area
+  int type;  // 0 directional 1 hemisphere 2 point 3 area 4 environment
   Spec rad;
   V3 pos, dir, dimx, dimy;
   float area;
@@ -159,7 +160,44 @@ struct Camera {
   M3 c2w;
   double W, H, dist;
 };
+// EnvironmentLight (src/static_scene/environment_light.cpp:6-203): the map and
+// the tables its constructor builds, in its float arithmetic and order.
+struct EnvMap {
+  int w = 0, h = 0;
+  std::vector<Spec> data;                          // HDRImageBuffer, row 0 = +y
+  std::vector<std::vector<float>> pThetaPhi, pPhiGivenTheta;
+  std::vector<float> pTheta;
+  void build() {  // environment_light.cpp:6-48
+    pThetaPhi.assign(h, std::vector<float>(w));
+    pTheta.assign(h, 0);
+    pPhiGivenTheta.assign(h, std::vector<float>(w));
+    float C = 0;
+    for (int y = 0; y < h; y++) {
+      float theta = (y + 0.5) / h * PI_D;
+      float sin_theta = ::sin((double)theta);  // ::sin(double): no std overloads visible there
+      for (int x = 0; x < w; x++) {
+        pThetaPhi[y][x] = data[x + w * y].illum() * sin_theta;
+        C += pThetaPhi[y][x];
+      }
+    }
+    for (int y = 0; y < h; y++) {
+      for (int x = 0; x < w; x++) {
+        pThetaPhi[y][x] /= C;
+        pTheta[y] += pThetaPhi[y][x];
+      }
+      if (pTheta[y] != 0)
+        for (int x = 0; x < w; x++) pPhiGivenTheta[y][x] = pThetaPhi[y][x] / pTheta[y];
+    }
+    for (int y = 0; y < h; y++) {
+      if (y > 0) pTheta[y] += pTheta[y - 1];
+      for (int x = 0; x < w; x++)
+        if (x > 0) pPhiGivenTheta[y][x] += pPhiGivenTheta[y][x - 1];
+    }
+  }
+};
+
 struct Scene {
+  EnvMap env;
   std::vector<Prim> prims;
   std::vector<Node> nodes;
   std::vector<Bsdf> bsdfs;
@@ -194,6 +232,12 @@ struct Rng {
     uint32_t h = lowbias32(seed * 0x9E3779B9U ^ pixel);
     base = lowbias32(h ^ (sample * 0x85EBCA6BU));
     dim = 0;
+  }
+  // rand()/(float)RAND_MAX (environment_light.cpp:67-68): float division
+  float next_f() {
+    if (mode == 0) return std::rand() / (float)RAND_MAX;
+    uint32_t h = lowbias32(base ^ ((dim++) * 0xC2B2AE35U + 0x27D4EB2FU));
+    return (float)(h >> 8) * (1.0f / 16777216.0f);
   }
   double next() {
     if (mode == 0) return std::rand() / (double)RAND_MAX;
@@ -329,8 +373,75 @@ struct Tracer {
   }
   bool intersect(const Ray& r, Isect* is) { return node_isect(0, r, is); }
 
+  // EnvironmentLight::sample_dir (environment_light.cpp:130-199)
+  Spec env_dir(const V3& d) const {
+    const EnvMap& E = S.env;
+    const int w = E.w, h = E.h;
+    double theta = ::acos(d[1]);
+    double sin_theta = ::sqrt(1 - d[1] * d[1]);
+    double phi = sin_theta == 0 ? PI_D : ::acos(std::min(std::max(d[2] / sin_theta, -1.0), 1.0));
+    if (d[0] > 0) phi = 2 * PI_D - phi;
+    double u = phi / (2 * PI_D);
+    double v = theta / PI_D;
+    float tu = u * w - 0.5;
+    float tv = v * h - 0.5;
+    int su = (int)tu;
+    int sv = (int)tv;
+    float a, b;
+    int px1, px2, py1, py2;
+    if (tu < 0) {
+      a = tu + 1; px1 = w - 1; px2 = 0;
+    } else if (tu >= w - 1) {
+      a = tu - w + 1; px1 = w - 1; px2 = 0;
+    } else {
+      a = tu - su; px1 = su; px2 = su + 1;
+    }
+    if (tv < 0) {
+      b = tv + 1; py1 = h - 1; py2 = 0;
+    } else if (tv >= h - 1) {
+      b = tv - h + 1; py1 = h - 1; py2 = 0;
+    } else {
+      b = tv - sv; py1 = sv; py2 = sv + 1;
+    }
+    Spec z11 = E.data[px1 + w * py1], z21 = E.data[px2 + w * py1];
+    Spec z12 = E.data[px1 + w * py2], z22 = E.data[px2 + w * py2];
+    Spec zy1 = z11 * (1 - a) + z21 * a;
+    Spec zy2 = z12 * (1 - a) + z22 * a;
+    return zy1 * (1 - b) + zy2 * b;
+  }
+
+  // EnvironmentLight::importanceSampling (environment_light.cpp:69-115)
+  void env_importance(V3* wi, float* pdf, Rng& rng) const {
+    const EnvMap& E = S.env;
+    float r1 = rng.next_f();
+    float r2 = rng.next_f();
+    r1 *= E.pTheta.back();
+    auto itr = std::lower_bound(E.pTheta.begin(), E.pTheta.end(), r1);
+    int t = (int)(itr - E.pTheta.begin());
+    float prev = t > 0 ? *(itr - 1) : 0;
+    float y = t + (r1 - prev) / (*itr - prev);
+    float theta = std::min(y / E.h, 1.f) * PI_D;
+    const std::vector<float>& row = E.pPhiGivenTheta[t];
+    r2 *= row.back();
+    itr = std::lower_bound(row.begin(), row.end(), r2);
+    int q = (int)(itr - row.begin());
+    prev = q > 0 ? *(itr - 1) : 0;
+    float x = q + (r2 - prev) / (*itr - prev);
+    float phi = std::min(x / E.w, 1.f) * 2 * PI_D;
+    double sin_theta = ::sin((double)theta);
+    double cos_theta = ::cos((double)theta);
+    *pdf = E.pThetaPhi[t][q];
+    *pdf /= (sin_theta * (2 * PI_D / E.w) * (PI_D / E.h));
+    *wi = V3(-sin_theta * ::sin((double)phi), cos_theta, sin_theta * ::cos((double)phi));
+  }
+
   // light.cpp:17-92
   Spec sample_L(const Light& L, const V3& p, V3* wi, float* dist, float* pdf, Rng& rng) {
+    if (L.type == 4) {  // EnvironmentLight::sample_L (environment_light.cpp:117-128)
+      env_importance(wi, pdf, rng);
+      *dist = (float)INF_D;
+      return env_dir(*wi);
+    }
     if (L.type == 0) {
       *wi = L.dir;
       *dist = (float)INF_D;
@@ -458,7 +569,10 @@ struct Tracer {
   Spec trace_ray(const Ray& r, bool includeLe, Rng& rng) {
     st.rays++;
     Isect isect;
-    if (!intersect(r, &isect)) return Spec(0, 0, 0);
+    if (!intersect(r, &isect)) {  // pathtracer.cpp:411-427
+      if (S.env.w > 0 && includeLe) return env_dir(r.d);
+      return Spec(0, 0, 0);
+    }
     const Prim& P = S.prims[isect.prim];
     const Bsdf& B = S.bsdfs[P.bsdf];
     RS_DBG("  depth %zu hit prim %d (type %d bsdf %d) t=%.9g n=(%.6g %.6g %.6g)\n", r.depth, isect.prim, P.type,
@@ -560,6 +674,17 @@ static bool load_scene(const char* path, Scene& S) {
     b.e = Spec(p[6], p[7], p[8]);
     b.ior = p[9];
     b.rough = p[10];
+  }
+  {
+    std::vector<int64_t> eshape;
+    std::vector<float> ergb;
+    if (ptdump::get(R, "env_shape", eshape) && ptdump::get(R, "env_rgb", ergb) && eshape.size() == 2) {
+      S.env.h = (int)eshape[0];
+      S.env.w = (int)eshape[1];
+      S.env.data.resize((size_t)S.env.w * S.env.h);
+      for (size_t i = 0; i < S.env.data.size(); ++i) S.env.data[i] = Spec(ergb[3 * i], ergb[3 * i + 1], ergb[3 * i + 2]);
+      S.env.build();
+    }
   }
   S.lights.resize(ltype.size());
   for (size_t i = 0; i < ltype.size(); ++i) {
