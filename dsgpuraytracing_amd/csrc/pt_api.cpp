@@ -71,6 +71,49 @@ float round_up(double x) {
   return f;
 }
 
+// EnvironmentLight's constructor tables (environment_light.cpp:6-48) in its own
+// float arithmetic and summation order, so the GPU's inverse-CDF sampling
+// picks the same texel as the reference for the same (r1, r2):
+//   pThetaPhi[y][x] = illum * sin(theta_y) / C, pTheta = running row sums,
+//   pPhiGivenTheta = running sums of pThetaPhi / pTheta[y] within the row.
+struct EnvTables {
+  std::vector<float4> tex;
+  std::vector<float> p_theta, p_phi, p_theta_phi;
+};
+#pragma clang fp contract(off)
+void build_env_tables(const float* rgb, int w, int h, EnvTables& t) {
+  const double kPi = 3.14159265358979323;  // CMU462 PI
+  t.tex.resize((size_t)w * h);
+  t.p_theta.assign((size_t)h, 0.f);
+  t.p_phi.assign((size_t)w * h, 0.f);
+  t.p_theta_phi.assign((size_t)w * h, 0.f);
+  for (size_t i = 0; i < (size_t)w * h; ++i) t.tex[i] = make_float4(rgb[3 * i], rgb[3 * i + 1], rgb[3 * i + 2], 0.f);
+  float C = 0;
+  for (int y = 0; y < h; y++) {
+    float theta = (y + 0.5) / h * kPi;
+    float sin_theta = std::sin((double)theta);
+    for (int x = 0; x < w; x++) {
+      const float* p = rgb + 3 * ((size_t)x + (size_t)w * y);
+      float illum = 0.2126f * p[0] + 0.7152f * p[1] + 0.0722f * p[2];  // Spectrum::illum
+      t.p_theta_phi[(size_t)y * w + x] = illum * sin_theta;
+      C += t.p_theta_phi[(size_t)y * w + x];
+    }
+  }
+  for (int y = 0; y < h; y++) {
+    for (int x = 0; x < w; x++) {
+      t.p_theta_phi[(size_t)y * w + x] /= C;
+      t.p_theta[y] += t.p_theta_phi[(size_t)y * w + x];
+    }
+    if (t.p_theta[y] != 0)
+      for (int x = 0; x < w; x++) t.p_phi[(size_t)y * w + x] = t.p_theta_phi[(size_t)y * w + x] / t.p_theta[y];
+  }
+  for (int y = 0; y < h; y++) {
+    if (y > 0) t.p_theta[y] += t.p_theta[y - 1];
+    for (int x = 1; x < w; x++) t.p_phi[(size_t)y * w + x] += t.p_phi[(size_t)y * w + x - 1];
+  }
+}
+#pragma clang fp contract(on)
+
 }  // namespace
 
 struct pt_ctx {
@@ -79,6 +122,9 @@ struct pt_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   DevBuf<DNode> nodes;
   DevBuf<DNode2> nodes2;  // binary tree for PT_FLAG_REF_COUNTS
+  DevBuf<float4> env_tex;          // environment map RGB (w*h, .w unused)
+  DevBuf<float> env_ptheta, env_pphi, env_pdf;  // EnvironmentLight tables
+  int env_w = 0, env_h = 0;
   DevBuf<DPrim> prims;
   DevBuf<float> norms;
   DevBuf<DBsdf> bsdfs;
@@ -146,6 +192,10 @@ int pt_destroy(pt_ctx* c) {
   (void)hipSetDevice(c->device);
   c->nodes.release();
   c->nodes2.release();
+  c->env_tex.release();
+  c->env_ptheta.release();
+  c->env_pphi.release();
+  c->env_pdf.release();
   c->prims.release();
   c->norms.release();
   c->bsdfs.release();
@@ -410,9 +460,12 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
     d.pad = 0.f;
   }
   std::vector<DLight> ls((size_t)std::max(0, s->n_lights));
+  int n_env = 0;
   for (int i = 0; i < s->n_lights; ++i) {
     const pt_light& L = s->lights[i];
-    if (L.type < 0 || L.type > 3) return fail(PT_E_INVALID, "pt_upload_scene: unsupported light type");
+    if (L.type < 0 || L.type > 4) return fail(PT_E_INVALID, "pt_upload_scene: unsupported light type");
+    if (L.type == PT_LIGHT_ENVIRONMENT && ++n_env > 1)
+      return fail(PT_E_INVALID, "pt_upload_scene: more than one environment light");
     DLight& d = ls[(size_t)i];
     std::memset(&d, 0, sizeof(d));
     d.type = L.type;
@@ -425,6 +478,12 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
     }
     d.area = L.area;
   }
+
+  if (n_env && (!s->env_rgb || s->env_width <= 0 || s->env_height <= 0))
+    return fail(PT_E_INVALID, "pt_upload_scene: environment light without a map (env_rgb/env_width/env_height)");
+  if (!n_env && s->env_rgb) return fail(PT_E_INVALID, "pt_upload_scene: env_rgb given but no PT_LIGHT_ENVIRONMENT light");
+  EnvTables env;
+  if (n_env) build_env_tables(s->env_rgb, s->env_width, s->env_height, env);
 
   std::vector<DNode2> d2(b2.size());
   for (size_t i = 0; i < b2.size(); ++i) {
@@ -446,6 +505,18 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
   HIPCHK(hipMemcpy(c->norms.p, norms.data(), norms.size() * sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(c->bsdfs.p, bs.data(), bs.size() * sizeof(DBsdf), hipMemcpyHostToDevice));
   if (!ls.empty()) HIPCHK(hipMemcpy(c->lights.p, ls.data(), ls.size() * sizeof(DLight), hipMemcpyHostToDevice));
+  c->env_w = n_env ? s->env_width : 0;
+  c->env_h = n_env ? s->env_height : 0;
+  if (n_env) {
+    HIPCHK(c->env_tex.reserve(env.tex.size()));
+    HIPCHK(c->env_ptheta.reserve(env.p_theta.size()));
+    HIPCHK(c->env_pphi.reserve(env.p_phi.size()));
+    HIPCHK(c->env_pdf.reserve(env.p_theta_phi.size()));
+    HIPCHK(hipMemcpy(c->env_tex.p, env.tex.data(), env.tex.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->env_ptheta.p, env.p_theta.data(), env.p_theta.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->env_pphi.p, env.p_phi.data(), env.p_phi.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->env_pdf.p, env.p_theta_phi.data(), env.p_theta_phi.size() * 4, hipMemcpyHostToDevice));
+  }
   c->n_lights = (int)ls.size();
   c->n_bsdfs = (int)bs.size();
   c->n_prims = s->n_prims;
@@ -504,6 +575,7 @@ static void screen_footprint(const pt_ctx* c, KParams& P) {
   P.cull_x1 = P.W - 1;
   P.cull_y1 = P.H - 1;
   if (std::getenv("PT_NO_FOOTPRINT_CULL")) return;
+  if (c->env_w > 0) return;  // rays that miss the scene see the environment map
   const pt_camera& cam = c->cam;
   for (int i = 0; i < 3; ++i)  // coordinates by dot products need an orthonormal c2w
     for (int j = 0; j < 3; ++j) {
@@ -579,6 +651,12 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.norms = c->norms.p;
   P.bsdfs = c->bsdfs.p;
   P.lights = c->lights.p;
+  P.env_w = c->env_w;
+  P.env_h = c->env_h;
+  P.env_tex = c->env_tex.p;
+  P.env_ptheta = c->env_ptheta.p;
+  P.env_pphi = c->env_pphi.p;
+  P.env_pdf = c->env_pdf.p;
   P.tiles = c->tiles.p;
   P.out = out_dev;
   P.work_counter = c->counter.p;

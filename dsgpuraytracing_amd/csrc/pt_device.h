@@ -95,6 +95,11 @@ struct KParams {
   const float* norms;  // 9 floats per primitive (vertex normals n1,n2,n3)
   const DBsdf* bsdfs;
   const DLight* lights;
+  int env_w, env_h;          // environment map size (0: no environment light)
+  const float4* env_tex;     // map RGB, row 0 = +y
+  const float* env_ptheta;   // EnvironmentLight::pTheta (running sums over rows)
+  const float* env_pphi;     // pPhiGivenTheta (running sums within each row)
+  const float* env_pdf;      // pThetaPhi
   const int4* tiles;  // (x, y, w, h)
   float* out;         // W*H*3
   float* partial;     // W*H*n_groups*3: each sample group's sum, resolved into `out` in group order

@@ -366,6 +366,80 @@ __device__ __forceinline__ bool box_hit(const Trav& tr, const float* lo, const f
   return tn <= tf;
 }
 
+// ---- EnvironmentLight (src/static_scene/environment_light.cpp), fp32.
+// sample_dir (130-199): lat-long bilinear lookup, wrapping in both directions
+// exactly as the reference does.
+__device__ __forceinline__ float3 env_dir(const KParams& P, float3 d) {
+  const float kPi = 3.14159265358979323f;
+  const int w = P.env_w, h = P.env_h;
+  const float theta = acosf(fminf(fmaxf(d.y, -1.0f), 1.0f));
+  const float sin_theta = fsqrt(fmaxf(0.0f, 1.0f - d.y * d.y));
+  float phi = sin_theta == 0.0f ? kPi : acosf(fminf(fmaxf(d.z / sin_theta, -1.0f), 1.0f));
+  if (d.x > 0.0f) phi = 2.0f * kPi - phi;
+  const float tu = phi * (0.15915494309189535f * (float)w) - 0.5f;
+  const float tv = theta * (0.31830988618379067f * (float)h) - 0.5f;
+  const int su = (int)tu, sv = (int)tv;
+  float a, b;
+  int px1, px2, py1, py2;
+  if (tu < 0.0f) {
+    a = tu + 1.0f; px1 = w - 1; px2 = 0;
+  } else if (tu >= (float)(w - 1)) {
+    a = tu - (float)w + 1.0f; px1 = w - 1; px2 = 0;
+  } else {
+    a = tu - (float)su; px1 = su; px2 = su + 1;
+  }
+  if (tv < 0.0f) {
+    b = tv + 1.0f; py1 = h - 1; py2 = 0;
+  } else if (tv >= (float)(h - 1)) {
+    b = tv - (float)h + 1.0f; py1 = h - 1; py2 = 0;
+  } else {
+    b = tv - (float)sv; py1 = sv; py2 = sv + 1;
+  }
+  const float4 z11 = P.env_tex[px1 + w * py1], z21 = P.env_tex[px2 + w * py1];
+  const float4 z12 = P.env_tex[px1 + w * py2], z22 = P.env_tex[px2 + w * py2];
+  const float3 zy1 = f3(z11.x, z11.y, z11.z) * (1.0f - a) + f3(z21.x, z21.y, z21.z) * a;
+  const float3 zy2 = f3(z12.x, z12.y, z12.z) * (1.0f - a) + f3(z22.x, z22.y, z22.z) * a;
+  return zy1 * (1.0f - b) + zy2 * b;
+}
+
+// First index of the ascending array a[0..n) with a[i] >= v (std::lower_bound).
+__device__ __forceinline__ int lower_bound_f(const float* __restrict__ a, int n, float v) {
+  int lo = 0;
+  while (n > 0) {
+    const int half = n >> 1;
+    if (a[lo + half] < v) {
+      lo += half + 1;
+      n -= half + 1;
+    } else {
+      n = half;
+    }
+  }
+  return lo;
+}
+
+// importanceSampling (69-115): inverse CDF over rows (pTheta), then within the
+// row (pPhiGivenTheta), linear inside the texel; pdf per solid angle.
+__device__ __forceinline__ void env_sample(const KParams& P, float r1, float r2, float3& wi, float& pdf) {
+  const float kPi = 3.14159265358979323f;
+  const int w = P.env_w, h = P.env_h;
+  r1 *= P.env_ptheta[h - 1];
+  const int t = lower_bound_f(P.env_ptheta, h, r1);
+  float prev = t > 0 ? P.env_ptheta[t - 1] : 0.0f;
+  const float y = (float)t + (r1 - prev) / (P.env_ptheta[t] - prev);
+  const float theta = fminf(y / (float)h, 1.0f) * kPi;
+  const float* row = P.env_pphi + (size_t)t * w;
+  r2 *= row[w - 1];
+  const int q = lower_bound_f(row, w, r2);
+  prev = q > 0 ? row[q - 1] : 0.0f;
+  const float x = (float)q + (r2 - prev) / (row[q] - prev);
+  const float phi = fminf(x / (float)w, 1.0f) * (2.0f * kPi);
+  float st, ct, sp, cp;
+  __sincosf(theta, &st, &ct);
+  __sincosf(phi, &sp, &cp);
+  pdf = P.env_pdf[(size_t)t * w + q] / (st * ((2.0f * kPi / (float)w) * (kPi / (float)h)));
+  wi = f3(-st * sp, ct, st * cp);
+}
+
 // Lane modes of the persistent kernel.
 enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 
@@ -374,7 +448,9 @@ enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 #define PT_MIN_WAVES_PER_SIMD 4
 #endif
 // BIN: the reference-count variant, traversing the binary tree (P.nodes2).
-template <bool STATS, bool DBG, bool BIN = false>
+// ENV: the scene has an environment light (kept out of the common build: its
+// lookups and sampling cost registers).
+template <bool STATS, bool DBG, bool BIN, bool ENV>
 __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel(KParams P) {
   __shared__ int s_stack[PT_STACK * PT_BLOCK];
   int* stk = s_stack + threadIdx.x;
@@ -442,7 +518,9 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if (DBG && pix == P.dbg_pix) printf("    shadow %s (pend %.6g) prim %d t %.9g\n", found ? "occluded" : "clear", pend.x, tr.hit.prim, tr.hit.t);
         stage = 0;
       } else if (!found) {
-        finish = true;  // miss: no environment light (pathtracer.cpp:421-426)
+        // miss: the environment map if there is one and includeLe (pathtracer.cpp:411-427)
+        if (ENV && includeLe) L = L + mul(T, env_dir(P, tr.d));
+        finish = true;
         stage = 2;
       } else {
         if (STATS) n_hits++;
@@ -496,7 +574,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           float3 wi;
           float dist, pdf;
           bool lit = true;
-          if (Lt.type == 3) {  // AreaLight::sample_L (light.cpp:80-92); grid sampler draws y first
+          if (ENV && Lt.type == 4) {  // EnvironmentLight::sample_L (environment_light.cpp:117-128)
+            float r1 = ptrng::draw(rbase, rdim++);
+            float r2 = ptrng::draw(rbase, rdim++);
+            env_sample(P, r1, r2, wi, pdf);
+            dist = 3.0e38f;
+          } else if (Lt.type == 3) {  // AreaLight::sample_L (light.cpp:80-92); grid sampler draws y first
             float u0 = ptrng::draw(rbase, rdim++);
             float u1 = ptrng::draw(rbase, rdim++);
             float sx = u1 - 0.5f, sy = u0 - 0.5f;
@@ -531,7 +614,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           float cos_t = fmaxf(0.0f, fr.to_local(wi).z);
           if (!(cos_t > 0.0f)) continue;
           float3 f = ld3(B.a) * 0.31830988618379067f;
-          pend = mul(mul(T, ld3(Lt.rad) * (cos_t * rcp(pdf))), f) * scale;
+          const float3 Le = (ENV && Lt.type == 4) ? env_dir(P, wi) : ld3(Lt.rad);
+          pend = mul(mul(T, Le * (cos_t * rcp(pdf))), f) * scale;
           // shadow ray (pathtracer.cpp:497-504): delta lights offset EPS_N along n
           float3 so = delta ? hp + ns * 5e-3f : offset_ray(hp, dot(wi, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng);
           trav_init(tr, so, wi, dist * 0.999f, true);
@@ -706,7 +790,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           mode = M_TRAV;
           break;
         }
-        // miss: the sample contributes 0
+        // miss: the sample sees the environment (includeLe) or nothing
+        if (ENV) acc = acc + env_dir(P, d);
         if (++sample >= s_end) {
           store3(P.partial + 3 * (size_t)wslot, acc);
           mode = M_FETCH;
@@ -820,15 +905,23 @@ __global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __rest
 }  // namespace ptk
 
 // ------------------------------------------------------------------ launchers
-extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, bool ref_counts, hipStream_t s) {
+template <bool ENV>
+static void launch_render(const KParams* P, int grid, bool stats, bool ref_counts, hipStream_t s) {
   if (ref_counts)
-    hipLaunchKernelGGL((ptk::render_kernel<true, false, true>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+    hipLaunchKernelGGL((ptk::render_kernel<true, false, true, ENV>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
   else if (P->dbg_pix >= 0)
-    hipLaunchKernelGGL((ptk::render_kernel<false, true>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+    hipLaunchKernelGGL((ptk::render_kernel<false, true, false, ENV>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
   else if (stats)
-    hipLaunchKernelGGL((ptk::render_kernel<true, false>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+    hipLaunchKernelGGL((ptk::render_kernel<true, false, false, ENV>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
   else
-    hipLaunchKernelGGL((ptk::render_kernel<false, false>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+    hipLaunchKernelGGL((ptk::render_kernel<false, false, false, ENV>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+}
+
+extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, bool ref_counts, hipStream_t s) {
+  if (P->env_w > 0)
+    launch_render<true>(P, grid, stats, ref_counts, s);
+  else
+    launch_render<false>(P, grid, stats, ref_counts, s);
   return hipGetLastError();
 }
 
@@ -850,6 +943,8 @@ extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prim
 
 extern "C" hipError_t ptk_render_occupancy(int* blocks_per_cu, bool stats) {
   if (stats)
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ptk::render_kernel<true, false>, PT_BLOCK, 0);
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ptk::render_kernel<false, false>, PT_BLOCK, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ptk::render_kernel<true, false, false, false>,
+                                                        PT_BLOCK, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ptk::render_kernel<false, false, false, false>,
+                                                      PT_BLOCK, 0);
 }

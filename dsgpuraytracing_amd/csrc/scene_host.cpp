@@ -1113,6 +1113,8 @@ struct pt_host_scene {
   std::vector<pt_light> lights;
   pt_camera cam{};
   double hfov = 0, vfov = 0;
+  int32_t env_w = 0, env_h = 0;  // EnvironmentLight map (pt_host_scene_set_envmap)
+  std::vector<float> env_rgb;
 };
 
 namespace {
@@ -1401,6 +1403,9 @@ int pt_host_scene_view(const pt_host_scene* s, pt_scene* scene, pt_camera* cam) 
     scene->bsdfs = s->bsdfs.data();
     scene->n_lights = (int32_t)s->lights.size();
     scene->lights = s->lights.data();
+    scene->env_width = s->env_w;
+    scene->env_height = s->env_h;
+    scene->env_rgb = s->env_w > 0 ? s->env_rgb.data() : nullptr;
   }
   if (cam) *cam = s->cam;
   return PT_OK;
@@ -1444,6 +1449,10 @@ int pt_host_scene_dump(const pt_host_scene* s, const char* path) {
   w.f4("light_rad", lr);
   w.f8("light_geom", lg);
   w.f4("light_area", la);
+  if (s->env_w > 0) {
+    w.i8("env_shape", {(int64_t)s->env_h, (int64_t)s->env_w});
+    w.f4("env_rgb", s->env_rgb);
+  }
   w.i4("prim_type", s->prim_type);
   w.i4("prim_bsdf", s->prim_bsdf);
   w.i4("prim_orig", s->prim_orig);
@@ -1462,6 +1471,28 @@ int pt_host_scene_dump(const pt_host_scene* s, const char* path) {
   w.f8("node_bb", nbb);
   w.i8("node_info", ni);
   w.close();
+  return PT_OK;
+}
+
+// PathTracer(..., envmap) + set_scene (src/pathtracer.cpp:42-46, 88-90): the
+// environment light joins the scene's lights last; main.cpp -e loads the map.
+int pt_host_scene_set_envmap(pt_host_scene* s, const char* exr_path) {
+  if (!s || !exr_path) return pt_fail(PT_E_INVALID, "pt_host_scene_set_envmap: NULL argument");
+  int32_t w = 0, h = 0;
+  float* rgb = nullptr;
+  int rc = pt_host_load_exr(exr_path, &w, &h, &rgb);
+  if (rc) return rc;
+  s->env_rgb.assign(rgb, rgb + (size_t)w * h * 3);
+  pt_host_free(rgb);
+  s->env_w = w;
+  s->env_h = h;
+  bool have = false;
+  for (const pt_light& l : s->lights) have = have || l.type == PT_LIGHT_ENVIRONMENT;
+  if (!have) {
+    pt_light l{};
+    l.type = PT_LIGHT_ENVIRONMENT;
+    s->lights.push_back(l);
+  }
   return PT_OK;
 }
 

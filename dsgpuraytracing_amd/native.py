@@ -21,6 +21,7 @@ PT_E_HIP = -2
 PT_E_NOSCENE = -3
 PT_E_ALLOC = -4
 PT_E_IO = -5
+PT_LIGHT_ENVIRONMENT = 4
 PT_FLAG_STATS = 1
 PT_FLAG_REF_COUNTS = 2
 
@@ -65,7 +66,8 @@ class pt_scene(ctypes.Structure):
                 ("prim_geom", POINTER(c_double)), ("prim_norm", POINTER(c_double)),
                 ("n_nodes", c_int64), ("nodes", POINTER(pt_bvh_node)),
                 ("n_bsdfs", c_int32), ("bsdfs", POINTER(pt_bsdf)),
-                ("n_lights", c_int32), ("lights", POINTER(pt_light))]
+                ("n_lights", c_int32), ("lights", POINTER(pt_light)),
+                ("env_width", c_int32), ("env_height", c_int32), ("env_rgb", POINTER(c_float))]
 
 
 class pt_params(ctypes.Structure):
@@ -108,6 +110,7 @@ _SIGS = {
     "pt_host_scene_view": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "pt_host_scene_dump": (c_int32, [c_void_p, c_char_p]),
     "pt_host_scene_free": (None, [c_void_p]),
+    "pt_host_scene_set_envmap": (c_int32, [c_void_p, c_char_p]),
     "pt_host_load_exr": (c_int32, [c_char_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_void_p)]),
     "pt_host_free": (None, [c_void_p]),
 }
@@ -203,6 +206,12 @@ class SceneArrays:
             n_nodes=nn, nodes=self.nodes,
             n_bsdfs=len(bt), bsdfs=self.bsdfs,
             n_lights=len(lt), lights=self.lights)
+        if "env_rgb" in d:  # EnvironmentLight map (light type 4)
+            eh, ew = (int(v) for v in d["env_shape"])
+            self.env_rgb = np.ascontiguousarray(d["env_rgb"], dtype=np.float32)
+            assert self.env_rgb.size == ew * eh * 3
+            self.scene.env_width, self.scene.env_height = ew, eh
+            self.scene.env_rgb = self.env_rgb.ctypes.data_as(POINTER(c_float))
         cam = d["cam"]
         self.camera = pt_camera()
         self.camera.pos[:] = cam[0:3].tolist()

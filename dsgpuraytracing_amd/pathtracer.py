@@ -127,9 +127,11 @@ class Scene:
         return cls(native.SceneArrays(ptdump.read(path)))
 
     @classmethod
-    def from_dae(cls, path: str, width: int, height: int, cam_info: Optional[str] = None) -> "Scene":
+    def from_dae(cls, path: str, width: int, height: int, cam_info: Optional[str] = None,
+                 envmap: Optional[str] = None) -> "Scene":
+        """envmap: OpenEXR lat-long map for the EnvironmentLight (the reference's -e)."""
         from . import scene_loader
-        return cls(native.SceneArrays(scene_loader.load_dae(path, width, height, cam_info)))
+        return cls(native.SceneArrays(scene_loader.load_dae(path, width, height, cam_info, envmap)))
 
     @property
     def camera(self) -> native.pt_camera:

@@ -33,23 +33,27 @@ def _bind(L):
     L._scene_bound = True
 
 
-def dump_dae(path: str, width: int, height: int, out_path: str, cam_info: Optional[str] = None) -> str:
+def dump_dae(path: str, width: int, height: int, out_path: str, cam_info: Optional[str] = None,
+             envmap: Optional[str] = None) -> str:
     L = native.lib()
     _bind(L)
     h = ctypes.c_void_p()
     native.check(L.pt_host_scene_load(path.encode(), width, height, cam_info.encode() if cam_info else None,
                                       ctypes.byref(h)))
     try:
+        if envmap:
+            native.check(L.pt_host_scene_set_envmap(h, envmap.encode()))
         native.check(L.pt_host_scene_dump(h, out_path.encode()))
     finally:
         L.pt_host_scene_free(h)
     return out_path
 
 
-def load_dae(path: str, width: int, height: int, cam_info: Optional[str] = None) -> Dict[str, np.ndarray]:
+def load_dae(path: str, width: int, height: int, cam_info: Optional[str] = None,
+             envmap: Optional[str] = None) -> Dict[str, np.ndarray]:
     with tempfile.TemporaryDirectory() as td:
         p = os.path.join(td, "scene.ptd")
-        dump_dae(path, width, height, p, cam_info)
+        dump_dae(path, width, height, p, cam_info, envmap)
         return ptdump.read(p)
 
 

@@ -58,11 +58,15 @@ extern "C" {
 #define PT_BSDF_REFRACTION 2
 #define PT_BSDF_GLASS 3
 #define PT_BSDF_EMISSION 4
-/* Light types follow SceneLight::getType(): Directional 0, Hemisphere 1, Point 2, Area 3. */
+/* Light types follow SceneLight::getType(): Directional 0, Hemisphere 1, Point 2, Area 3;
+ * Environment 4 (EnvironmentLight, src/static_scene/environment_light.cpp, whose own
+ * getType() says 1) — its map is pt_scene.env_*; at most one, last in the list as
+ * PathTracer::set_scene pushes it (src/pathtracer.cpp:88-90). */
 #define PT_LIGHT_DIRECTIONAL 0
 #define PT_LIGHT_HEMISPHERE 1
 #define PT_LIGHT_POINT 2
 #define PT_LIGHT_AREA 3
+#define PT_LIGHT_ENVIRONMENT 4
 
 typedef struct pt_ctx pt_ctx;
 
@@ -126,6 +130,11 @@ typedef struct pt_scene {
   const pt_bsdf* bsdfs;
   int32_t n_lights;
   const pt_light* lights;
+  /* HDRImageBuffer of the environment light (NULL / 0 when there is none):
+   * env_width x env_height float RGB, row 0 = +y (theta = (y+0.5)/h*pi). */
+  int32_t env_width;
+  int32_t env_height;
+  const float* env_rgb;
 } pt_scene;
 
 /* Integrator settings (PathTracer members) and frame size. */

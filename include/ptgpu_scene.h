@@ -45,6 +45,9 @@ int pt_host_scene_load(const char* dae_path, int32_t width, int32_t height, cons
                        pt_host_scene** out);
 /* Borrowed views, valid until pt_host_scene_free. Either pointer may be NULL. */
 int pt_host_scene_view(const pt_host_scene* hs, pt_scene* scene, pt_camera* cam);
+/* Adds the EnvironmentLight of an OpenEXR lat-long map (main.cpp -e +
+ * PathTracer::set_scene: appended after the scene's lights). */
+int pt_host_scene_set_envmap(pt_host_scene* hs, const char* exr_path);
 /* Writes the flattened scene as a PTDUMP file. */
 int pt_host_scene_dump(const pt_host_scene* hs, const char* path);
 void pt_host_scene_free(pt_host_scene* hs);

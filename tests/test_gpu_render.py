@@ -48,6 +48,9 @@ def near_exact_report(a, b):
     ("CBspheres_lambertian_ambientlight_64x64", 64, 64, 4, 4, 2, 3), # hemisphere light, 2 samples
     ("c1_default_64x64", 64, 64, 4, 0, 1, 1),                        # max_ray_depth 0: direct only
     ("c1_default_64x64", 64, 64, 4, 1, 4, 1),                        # AppConfig defaults: -m 1 -l 4
+    ("c1env_64x64", 64, 64, 4, 4, 1, 3),                             # + environment light (-e)
+    ("c1env_64x64", 64, 64, 4, 4, 2, 4),
+    ("CBspheresenv_64x64", 64, 64, 4, 4, 1, 3),                      # env seen through mirror / glass
 ])
 def test_hip_near_exact_vs_restatement_counter_rng(restate, scene, w, h, spp, m, l, seed):
     got, st = gpu_render(scene, w, h, spp, m, l, seed)
@@ -82,6 +85,21 @@ def test_hip_mirror_glass_statistical_vs_reference_golden():
     r1 = ptdump.read(golden("CBspheres_128x128_s64_m4_l1_seed1.hdr.ptd"))["hdr"].reshape(128, 128, 3)
     r2 = ptdump.read(golden("CBspheres_128x128_s64_m4_l1_seed2.hdr.ptd"))["hdr"].reshape(128, 128, 3)
     g, _ = gpu_render("CBspheres_128x128", 128, 128, 64, 4, 1, seed=999)
+    floor = np.linalg.norm(r1 - r2, axis=2).mean()
+    dist = np.linalg.norm(g - r1, axis=2).mean()
+    sigma = (r1 - r2).mean(axis=2).std() / np.sqrt(128 * 128)
+    bias = abs(g.mean() - r1.mean())
+    print(f"L2 {dist:.5f} vs floor {floor:.5f}; bias {bias:.2e} vs 3 sigma {3*sigma:.2e}")
+    assert dist <= 1.10 * floor
+    assert bias <= 3 * sigma
+
+
+@pytest.mark.parametrize("seed", [77])
+def test_hip_environment_light_statistical_vs_reference_golden(seed):
+    """C1 + EnvironmentLight at 128x128 @ 64 spp vs the reference binary (-e)."""
+    r1 = ptdump.read(golden("c1env_128x128_s64_m4_l1_seed1.hdr.ptd"))["hdr"].reshape(128, 128, 3)
+    r2 = ptdump.read(golden("c1env_128x128_s64_m4_l1_seed2.hdr.ptd"))["hdr"].reshape(128, 128, 3)
+    g, _ = gpu_render("c1env_128x128", 128, 128, 64, 4, 1, seed=seed)
     floor = np.linalg.norm(r1 - r2, axis=2).mean()
     dist = np.linalg.norm(g - r1, axis=2).mean()
     sigma = (r1 - r2).mean(axis=2).std() / np.sqrt(128 * 128)

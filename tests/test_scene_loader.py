@@ -38,6 +38,19 @@ def test_bsdf_and_light_variants_bit_identical(name):
         assert np.array_equal(got[k], ref[k]), k
 
 
+@pytest.mark.parametrize("fixture,dae", [("c1env_64x64", "CBspheres_lambertian.dae"),
+                                         ("CBspheresenv_64x64", "CBspheres.dae")])
+def test_environment_light_scene_bit_identical(fixture, dae):
+    """-e map: the environment light is appended last and the map read by the
+    native EXR reader equals the reference's (tinyexr) decode."""
+    got = scene_loader.load_dae(os.path.join(ROOT, "assets", dae), 64, 64, envmap=golden("env_sky_64x32.exr"))
+    ref = ptdump.read(golden(f"{fixture}.scene.ptd"))
+    assert sorted(got) == sorted(ref)
+    for k in ref:
+        assert np.array_equal(got[k], ref[k]), k
+    assert got["light_type"][-1] == native.PT_LIGHT_ENVIRONMENT
+
+
 @pytest.mark.parametrize("key", ["CBbunny.dae@1024x1024", "CBbunny_sub1.dae@1024x1024", "CBbunny_sub1.dae@1920x1080"])
 def test_bunny_scenes_match_reference_checksums(key):
     want = json.load(open(golden("scene_hashes.json")))[key]
