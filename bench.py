@@ -38,6 +38,9 @@ WORKLOADS = {
                desc="C3 CBbunny_sub1 (114,316 tris; CBdragon proxy) 1024x1024 64spp -m 4 -l 1"),
     "c4": dict(scene="sub1", w=1920, h=1080, spp=256,
                desc="C4 CBbunny_sub1 (CBdragon proxy) 1920x1080 256spp -m 4 -l 1, tiles over N GPUs"),
+    "c5": dict(scene="c5", w=1920, h=1080, spp=512,
+               desc="C5 CBbunny_sub2_c5 (457,228 tris, glass bunny + mirror sphere; CBlucy proxy) + synthetic "
+                    "512x256 environment light, 1920x1080 512spp -m 4 -l 1, tiles over N GPUs"),
 }
 W, H, SPP, DEPTH, NSL, SEED = 1024, 1024, 64, 4, 1, 1
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -139,8 +142,14 @@ def main():
         scene = Scene.from_dump(args.scene_dump)
         dump_path = args.scene_dump
     else:
-        dae = scenes.proxy_path(1) if wl["scene"] == "sub1" else scenes.C1_DAE
-        scene = Scene.from_dae(dae, W, H)
+        envmap = None
+        if wl["scene"] == "sub1":
+            dae = scenes.proxy_path(1)
+        elif wl["scene"] == "c5":
+            dae, envmap = scenes.c5_path(2), scenes.c5_envmap_path()
+        else:
+            dae = scenes.C1_DAE
+        scene = Scene.from_dae(dae, W, H, envmap=envmap)
         dump_path = None
     dev = Device(local)
     dev.upload_scene(scene)
@@ -206,7 +215,11 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic: deterministic CBbunny_sub1 proxy for the missing CBdragon.dae (SURVEY §8(d))",
+            "data": {"c5": "synthetic: deterministic CBbunny_sub2 glass/mirror proxy for the missing CBlucy.dae + "
+                           "seeded 512x256 environment map (SURVEY §8(d))",
+                     "c1": "CBspheres_lambertian.dae from the reference", "c2": "CBspheres_lambertian.dae from the reference"
+                     }.get(args.workload,
+                           "synthetic: deterministic CBbunny_sub1 proxy for the missing CBdragon.dae (SURVEY §8(d))"),
             "config": {"workload": wl["desc"] + ", default camera",
                        "width": W, "height": H, "spp": SPP, "max_ray_depth": DEPTH, "ns_area_light": NSL,
                        "parallelism": f"tiles{world}" if world > 1 else "single",
@@ -236,7 +249,7 @@ def main():
                 if dp is None:
                     from dsgpuraytracing_amd import scene_loader
                     dp = os.path.join(ROOT, "_scenes", f"bench_{args.workload}.ptd")
-                    scene_loader.dump_dae(dae, W, H, dp)
+                    scene_loader.dump_dae(dae, W, H, dp, envmap=envmap)
                 out["cpu_baseline"] = cpu_baseline(dp)
             except Exception as e:  # reported, never silently replaced
                 out["cpu_baseline"] = {"error": repr(e)}

@@ -136,6 +136,7 @@ struct pt_ctx {
   int64_t culled_px = 0;         // pixels of the last launch outside the footprint
   DevBuf<float> frame;  // device framebuffer for host-output renders
   DevBuf<float> partial;  // per-slot sample-group sums
+  DevBuf<int> spill;      // traversal stack entries beyond PT_STACK
   DevBuf<uint32_t> counter;
   DevBuf<unsigned long long> stats;
   DevBuf<float> q_f;    // ray-query scratch
@@ -202,6 +203,7 @@ int pt_destroy(pt_ctx* c) {
   c->lights.release();
   c->tiles.release();
   c->blocks.release();
+  c->spill.release();
   c->frame.release();
   c->counter.release();
   c->stats.release();
@@ -439,9 +441,9 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
       if (!empty && r >= 0 && (r <= (int)i || r >= (int)dn.size()))
         return fail(PT_E_INVALID, "pt_upload_scene: BVH4 child reference is not forward");
     }
-  if (max_stack > PT_STACK)
+  if (max_stack > PT_STACK_MAX)
     return fail(PT_E_INVALID, "pt_upload_scene: BVH needs a deeper traversal stack (" + std::to_string(max_stack) +
-                                  " > " + std::to_string(PT_STACK) + ")");
+                                  " > " + std::to_string(PT_STACK_MAX) + ")");
   c->bvh_stack = max_stack;
   c->n_nodes4 = dn.size();
 
@@ -736,6 +738,11 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.partial = c->partial.p;
   int64_t max_grid = std::max<int64_t>(1, (slots + PT_BLOCK - 1) / PT_BLOCK);
   int grid = (int)std::min<int64_t>(want, max_grid);
+  P.stack_spill = nullptr;
+  if (c->bvh_stack > PT_STACK) {  // worst-case depth beyond the LDS stack
+    HIPCHK(c->spill.reserve((size_t)(c->bvh_stack - PT_STACK) * grid * PT_BLOCK));
+    P.stack_spill = c->spill.p;
+  }
   HIPCHK(hipEventRecord(c->ev0, s));
   HIPCHK(ptk_launch_render(&P, grid, stats, (flags & PT_FLAG_REF_COUNTS) != 0, s));
   HIPCHK(hipEventRecord(c->ev1, s));
@@ -844,8 +851,13 @@ int pt_intersect(pt_ctx* c, int64_t n, const double* o, const double* d, const d
   int32_t* dh = c->q_i.p;
   int32_t* dp = c->q_i.p + n;
   int32_t* da = c->q_i.p + 2 * n;
+  int* spill = nullptr;
+  if (c->bvh_stack > PT_STACK) {
+    HIPCHK(c->spill.reserve((size_t)(c->bvh_stack - PT_STACK) * (size_t)((n + PT_BLOCK - 1) / PT_BLOCK * PT_BLOCK)));
+    spill = c->spill.p;
+  }
   HIPCHK(ptk_launch_intersect(c->nodes.p, c->prims.p, c->q_f.p, c->q_f.p + 3 * n, c->q_f.p + 6 * n, n, dh, dt, dp, da,
-                              c->stream));
+                              spill, c->stream));
   std::vector<int32_t> ib((size_t)n * 3);
   std::vector<float> tb((size_t)n);
   HIPCHK(hipMemcpyAsync(ib.data(), c->q_i.p, ib.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));

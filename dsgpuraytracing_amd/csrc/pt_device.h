@@ -27,7 +27,10 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #define PT_LEAF_WEIGHT 16  // leaf steps when leaf lanes >= node lanes * 16 / PT_LEAF_WEIGHT
 #endif
 #ifndef PT_STACK
-#define PT_STACK 32  // traversal stack entries per lane (LDS, lane-contiguous)
+#define PT_STACK 32  // traversal stack entries per lane in LDS (lane-contiguous)
+#endif
+#ifndef PT_STACK_MAX
+#define PT_STACK_MAX 128  // deepest worst-case stack accepted (entries past PT_STACK spill to global memory)
 #endif
 
 // BVH4 node, 128 B (one L2 line): four child boxes in SoA form, component k
@@ -106,7 +109,8 @@ struct KParams {
   const int4* blocks;  // (x, y, w<=8, h<=8): footprint-clipped pixel blocks of the tiles
   int n_blocks;
   uint32_t* work_counter;
-  unsigned long long* stats;  // 7 counters (PT_FLAG_STATS)
+  unsigned long long* stats;  // counters (PT_FLAG_STATS / PT_FLAG_REF_COUNTS)
+  int* stack_spill;           // traversal stack entries beyond PT_STACK (null if the BVH never needs them)
   int dbg_pix;                // diagnostic printf trace of one pixel (-1: off)
   int shade_batch;            // leave the traversal phase once this many lanes finished their ray
   int leaf_weight;            // leaf steps run when leaf_weight * leaf lanes >= 16 * node lanes
@@ -118,5 +122,5 @@ extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, 
 extern "C" hipError_t ptk_launch_resolve(const KParams* P, hipStream_t s);
 extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prims, const float* o, const float* d,
                                            const float* maxt, int64_t n, int32_t* hit, float* t, int32_t* prim,
-                                           int32_t* anyhit, hipStream_t s);
+                                           int32_t* anyhit, int* spill, hipStream_t s);
 extern "C" hipError_t ptk_render_occupancy(int* blocks_per_cu, bool stats);

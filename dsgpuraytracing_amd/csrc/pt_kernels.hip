@@ -218,10 +218,26 @@ __device__ __forceinline__ bool prim_test(const float4 v0, const float4 e1, cons
 // (bvh.cpp:227-279, 343-362: the same closest hit, children visited near-first,
 // boxes clipped to the current [0, tmax]) or, with tr.any, occlusion within
 // (0, tmax) (bvh.cpp:282-341), leaving on the first hit.
-__device__ __forceinline__ bool trav_pop(int* __restrict__ stk, int stride, Trav& tr) {
+// Per-lane traversal stack: the first PT_STACK entries in LDS (lane-
+// contiguous, conflict-free), deeper ones in a global per-lane spill area that
+// only BVHs with a worst-case depth beyond PT_STACK get (rarely touched).
+struct Stack {
+  int* lds;       // s_stack + lane, stride PT_BLOCK
+  int* spill;     // P.stack_spill + global lane id, stride sstride (may be null)
+  uint32_t sstride;
+  __device__ __forceinline__ void put(int i, int v) const {
+    if (i < PT_STACK) lds[i * PT_BLOCK] = v;
+    else spill[(size_t)(i - PT_STACK) * sstride] = v;
+  }
+  __device__ __forceinline__ int get(int i) const {
+    return i < PT_STACK ? lds[i * PT_BLOCK] : spill[(size_t)(i - PT_STACK) * sstride];
+  }
+};
+
+__device__ __forceinline__ bool trav_pop(const Stack& stk, Trav& tr) {
   if (tr.sp == 0) return true;
   --tr.sp;
-  tr.node = stk[tr.sp * stride];
+  tr.node = stk.get(tr.sp);
   return false;
 }
 
@@ -235,7 +251,7 @@ __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb) {
 }
 
 template <bool STATS>
-__device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, int* __restrict__ stk, int stride, Trav& tr,
+__device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, const Stack& stk, Trav& tr,
                                           Counters& ct) {
   const float kRobust = PT_ROBUST;
   const DNode* nd = nodes + tr.node;
@@ -265,12 +281,12 @@ __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, int* 
   cswap(d0, r0, d2, r2);
   cswap(d1, r1, d3, r3);
   cswap(d1, r1, d2, r2);
-  if (d0 == kMiss) return trav_pop(stk, stride, tr);
+  if (d0 == kMiss) return trav_pop(stk, tr);
   // push the farther hits (farthest first), continue with the nearest
   int sp = tr.sp;
-  if (d3 != kMiss) stk[(sp++) * stride] = r3;
-  if (d2 != kMiss) stk[(sp++) * stride] = r2;
-  if (d1 != kMiss) stk[(sp++) * stride] = r1;
+  if (d3 != kMiss) stk.put(sp++, r3);
+  if (d2 != kMiss) stk.put(sp++, r2);
+  if (d1 != kMiss) stk.put(sp++, r1);
   tr.sp = sp;
   tr.node = r0;
   return false;
@@ -278,8 +294,8 @@ __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, int* 
 
 // Binary node step over the reference topology (reference-count launch).
 template <bool STATS>
-__device__ __forceinline__ bool node_step2(const DNode2* __restrict__ nodes, int* __restrict__ stk, int stride,
-                                           Trav& tr, Counters& ct) {
+__device__ __forceinline__ bool node_step2(const DNode2* __restrict__ nodes, const Stack& stk, Trav& tr,
+                                           Counters& ct) {
   const float kRobust = PT_ROBUST;
   const float4 a = nodes[tr.node].a;
   const float4 b = nodes[tr.node].b;
@@ -302,7 +318,7 @@ __device__ __forceinline__ bool node_step2(const DNode2* __restrict__ nodes, int
   bool in1 = tn1 <= tf1;
   if (in0 && in1) {
     bool first0 = tn0 <= tn1;
-    stk[tr.sp * stride] = first0 ? e.y : e.x;
+    stk.put(tr.sp, first0 ? e.y : e.x);
     ++tr.sp;
     tr.node = first0 ? e.x : e.y;
   } else if (in0) {
@@ -310,7 +326,7 @@ __device__ __forceinline__ bool node_step2(const DNode2* __restrict__ nodes, int
   } else if (in1) {
     tr.node = e.y;
   } else {
-    return trav_pop(stk, stride, tr);
+    return trav_pop(stk, tr);
   }
   return false;
 }
@@ -320,8 +336,8 @@ __device__ __forceinline__ int leaf_first(int cur) { return (~cur) >> 3; }
 __device__ __forceinline__ int leaf_count(int cur) { return ((~cur) & 7) + 1; }
 
 template <bool STATS>
-__device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, int* __restrict__ stk, int stride,
-                                          Trav& tr, Counters& ct) {
+__device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const Stack& stk, Trav& tr,
+                                          Counters& ct) {
   const int pa = leaf_first(tr.node);
   const int n = leaf_count(tr.node);
   const bool two = n >= 2;
@@ -334,22 +350,22 @@ __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, int* 
     tr.node = ~(((pa + 2) << 3) | (n - 3));
     return false;
   }
-  return trav_pop(stk, stride, tr);
+  return trav_pop(stk, tr);
 }
 
 template <bool STATS>
 __device__ __forceinline__ bool trav_step(const DNode* __restrict__ nodes, const DPrim* __restrict__ prims,
-                                          int* __restrict__ stk, int stride, Trav& tr, Counters& ct) {
-  return tr.node < 0 ? leaf_step<STATS>(prims, stk, stride, tr, ct) : node_step<STATS>(nodes, stk, stride, tr, ct);
+                                          const Stack& stk, Trav& tr, Counters& ct) {
+  return tr.node < 0 ? leaf_step<STATS>(prims, stk, tr, ct) : node_step<STATS>(nodes, stk, tr, ct);
 }
 
 template <bool STATS>
 __device__ __forceinline__ bool traverse(const DNode* __restrict__ nodes, const DPrim* __restrict__ prims,
-                                         int* __restrict__ stk, int stride, float3 o, float3 d, float tmax,
+                                         const Stack& stk, float3 o, float3 d, float tmax,
                                          bool any, Hit& hit, Counters& ct) {
   Trav tr;
   trav_init(tr, o, d, tmax, any);
-  while (!trav_step<STATS>(nodes, prims, stk, stride, tr, ct)) {
+  while (!trav_step<STATS>(nodes, prims, stk, tr, ct)) {
   }
   hit = tr.hit;
   return tr.found;
@@ -453,8 +469,9 @@ enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 template <bool STATS, bool DBG, bool BIN, bool ENV>
 __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel(KParams P) {
   __shared__ int s_stack[PT_STACK * PT_BLOCK];
-  int* stk = s_stack + threadIdx.x;
   const int lane = threadIdx.x & 63;
+  const uint32_t gid = blockIdx.x * PT_BLOCK + threadIdx.x;
+  const Stack stk{s_stack + threadIdx.x, P.stack_spill ? P.stack_spill + gid : nullptr, gridDim.x * PT_BLOCK};
 
   // Material and light tables are read by every shading step: keep small
   // ones in LDS (the usual case); larger ones stay in global memory.
@@ -820,12 +837,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       const int n_node = __popcll(__ballot(trav && !at_leaf));
       bool done = false;
       if (n_leaf > 0 && (n_node == 0 || n_leaf * P.leaf_weight >= n_node * 16)) {
-        if (at_leaf) done = leaf_step<STATS>(P.prims, stk, PT_BLOCK, tr, ct);
+        if (at_leaf) done = leaf_step<STATS>(P.prims, stk, tr, ct);
         if (STATS) n_leafit += lane == 0;
       } else {
         if (trav && !at_leaf) {
-          if constexpr (BIN) done = node_step2<STATS>(P.nodes2, stk, PT_BLOCK, tr, ct);
-          else done = node_step<STATS>(P.nodes, stk, PT_BLOCK, tr, ct);
+          if constexpr (BIN) done = node_step2<STATS>(P.nodes2, stk, tr, ct);
+          else done = node_step<STATS>(P.nodes, stk, tr, ct);
         }
       }
       if (done) mode = M_SHADE;
@@ -881,10 +898,10 @@ __global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __rest
                                                            const DPrim* __restrict__ prims, const float* __restrict__ o,
                                                            const float* __restrict__ d, const float* __restrict__ maxt,
                                                            int64_t n, int32_t* hit, float* t, int32_t* prim,
-                                                           int32_t* anyhit) {
+                                                           int32_t* anyhit, int* spill) {
   __shared__ int s_stack[PT_STACK * PT_BLOCK];
-  int* stk = s_stack + threadIdx.x;
   int64_t i = (int64_t)blockIdx.x * PT_BLOCK + threadIdx.x;
+  const Stack stk{s_stack + threadIdx.x, spill ? spill + i : nullptr, gridDim.x * PT_BLOCK};
   if (i >= n) return;
   float3 O = f3(o[3 * i], o[3 * i + 1], o[3 * i + 2]);
   float3 D = f3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
@@ -893,12 +910,12 @@ __global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __rest
   h.u = h.v = 0;
   h.prim = -1;
   Counters ct = {0, 0, 0};
-  bool f = traverse<false>(nodes, prims, stk, PT_BLOCK, O, D, 3.0e38f, false, h, ct);
+  bool f = traverse<false>(nodes, prims, stk, O, D, 3.0e38f, false, h, ct);
   hit[i] = f ? 1 : 0;
   t[i] = f ? h.t : -1.0f;
   prim[i] = f ? h.prim : -1;
   Hit h2;
-  bool a = traverse<false>(nodes, prims, stk, PT_BLOCK, O, D, maxt[i], true, h2, ct);
+  bool a = traverse<false>(nodes, prims, stk, O, D, maxt[i], true, h2, ct);
   anyhit[i] = a ? 1 : 0;
 }
 
@@ -933,11 +950,11 @@ extern "C" hipError_t ptk_launch_resolve(const KParams* P, hipStream_t s) {
 
 extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prims, const float* o, const float* d,
                                            const float* maxt, int64_t n, int32_t* hit, float* t, int32_t* prim,
-                                           int32_t* anyhit, hipStream_t s) {
+                                           int32_t* anyhit, int* spill, hipStream_t s) {
   int grid = (int)((n + PT_BLOCK - 1) / PT_BLOCK);
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL(ptk::intersect_kernel, dim3(grid), dim3(PT_BLOCK), 0, s, nodes, prims, o, d, maxt, n, hit, t,
-                     prim, anyhit);
+                     prim, anyhit, spill);
   return hipGetLastError();
 }
 

@@ -102,12 +102,6 @@ def proxy_path(levels: int, cache_dir: Optional[str] = None) -> str:
     return dst
 
 
-if __name__ == "__main__":
-    import sys
-    for lv in (int(a) for a in sys.argv[1:] or ["1"]):
-        print(proxy_path(lv))
-
-
 def synthetic_envmap(width: int = 512, height: int = 256, seed: int = 7) -> np.ndarray:
     """Deterministic lat-long HDR sky (float32, (height, width, 3), row 0 = +y,
     the reference's EnvironmentLight convention theta = (y+0.5)/h*pi): a
@@ -128,3 +122,106 @@ def synthetic_envmap(width: int = 512, height: int = 256, seed: int = 7) -> np.n
     noise = 1.0 + 0.08 * rng.standard_normal((height, width, 1))
     env = (sky + ground) * noise + sun
     return np.ascontiguousarray(np.maximum(env, 0.0).astype(np.float32))
+
+
+_GLASS_EXTRA = """      <extra>
+        <technique profile="CMU462">
+          <glass>
+            <reflectance>1 1 1</reflectance>
+            <transmittance>1 1 1</transmittance>
+            <roughness>0</roughness>
+            <ior>1.45</ior>
+          </glass>
+        </technique>
+      </extra>
+"""
+
+_CHROME_EFFECT = """    <effect id="chrome-effect">
+      <profile_COMMON>
+        <technique sid="common">
+          <phong>
+            <diffuse>
+              <color sid="diffuse">0.8 0.8 0.8 1</color>
+            </diffuse>
+          </phong>
+        </technique>
+      </profile_COMMON>
+      <extra>
+        <technique profile="CMU462">
+          <mirror>
+            <reflectance>1 1 1</reflectance>
+          </mirror>
+        </technique>
+      </extra>
+    </effect>
+"""
+
+_MIRROR_SPHERE_GEOM = """    <geometry id="MirrorSphere-data" name="MirrorSphere">
+      <extra>
+        <technique profile="CMU462">
+          <sphere>
+            <radius>.25</radius>
+          </sphere>
+        </technique>
+      </extra>
+    </geometry>
+"""
+
+_MIRROR_SPHERE_NODE = """      <node id="MirrorSphere" name="MirrorSphere" type="NODE">
+        <matrix sid="transform">1 0 0 0.65 0 1 0 0.25 0 0 1 0.45 0 0 0 1</matrix>
+        <instance_geometry url="#MirrorSphere-data">
+          <bind_material>
+            <technique_common>
+              <instance_material symbol="chrome" target="#chrome"/>
+            </technique_common>
+          </bind_material>
+        </instance_geometry>
+      </node>
+"""
+
+
+def make_c5(levels: int, dst: str) -> str:
+    """C5 proxy: CBbunny_sub<levels> with the bunny's
+    material switched to <glass> (ior 1.45, the commented template of
+    CBspheres_lambertian.dae) and one <mirror> sphere (r = 0.25, resting on
+    the floor beside the bunny, in CBspheres.dae's chrome syntax)."""
+    txt = open(proxy_path(levels)).read()
+    e0 = txt.index('<effect id="Default-effect">')
+    e1 = txt.index("</effect>", e0)
+    txt = txt[:e1] + _GLASS_EXTRA + "    " + txt[e1:]
+    le = txt.index("</library_effects>")
+    txt = txt[:le] + _CHROME_EFFECT + "  " + txt[le:]
+    lm = txt.index("</library_materials>")
+    txt = txt[:lm] + '  <material id="chrome" name="chrome">\n      <instance_effect url="#chrome-effect"/>\n    </material>\n  ' + txt[lm:]
+    lg = txt.index("</library_geometries>")
+    txt = txt[:lg] + _MIRROR_SPHERE_GEOM + "  " + txt[lg:]
+    vs = txt.index("</visual_scene>")
+    txt = txt[:vs] + _MIRROR_SPHERE_NODE + "    " + txt[vs:]
+    with open(dst, "w") as f:
+        f.write(txt)
+    return dst
+
+
+def c5_path(levels: int = 2, cache_dir: Optional[str] = None) -> str:
+    cache_dir = cache_dir or os.path.join(ROOT, "_scenes")
+    dst = os.path.join(cache_dir, f"CBbunny_sub{levels}_c5.dae")
+    if not os.path.exists(dst) or os.path.getmtime(dst) < os.path.getmtime(__file__):
+        make_c5(levels, dst)
+    return dst
+
+
+def c5_envmap_path(cache_dir: Optional[str] = None) -> str:
+    """The C5 environment map: synthetic_envmap(512, 256, seed=7) as a ZIP OpenEXR."""
+    from . import image_io
+    cache_dir = cache_dir or os.path.join(ROOT, "_scenes")
+    dst = os.path.join(cache_dir, "c5_sky_512x256.exr")
+    if not os.path.exists(dst) or os.path.getmtime(dst) < os.path.getmtime(__file__):
+        os.makedirs(cache_dir, exist_ok=True)
+        image_io.write_exr(dst, synthetic_envmap(512, 256, seed=7), "zip")
+    return dst
+
+
+if __name__ == "__main__":
+    import sys
+    for lv in (int(a) for a in sys.argv[1:] or ["1"]):
+        print(proxy_path(lv))

@@ -200,6 +200,66 @@ def test_hip_oversize_leaf_split_matches_reference_bvh(name):
     assert frac >= 0.995 and rel_mean <= 1e-3, (frac, rel_mean)
 
 
+def _deep_chain_scene(n=96):
+    """n parallel squares-as-triangles stacked along z, under a CHAIN BVH
+    (node k: left = leaf {prim k}, right = node k+1).  Rays travelling -z
+    enter the chain's far end first, so near-first traversal pushes every
+    leaf: the worst-case stack (> PT_STACK) spills to global memory."""
+    base = ptdump.read(golden("c1_default_64x64.scene.ptd"))
+    d = dict(base)
+    z = np.linspace(-0.5, 0.5, n)
+    geom = np.zeros((n, 9))
+    for k in range(n):
+        geom[k] = [-1, -1, z[k], 1, -1, z[k], -1, 1, z[k]]   # covers x + y <= 0 of [-1,1]^2
+    norms = np.tile([0, 0, 1.0], (n, 3))
+    d["prim_type"] = np.ones(n, np.int32)
+    d["prim_bsdf"] = np.zeros(n, np.int32)
+    d["prim_orig"] = np.arange(n, dtype=np.int32)
+    d["prim_geom"] = geom.reshape(-1)
+    d["prim_norm"] = norms.reshape(-1)
+    bb, info = [], []
+    for k in range(n - 1):   # internal node k at index 2k, leaf k at 2k+1, next internal at 2k+2
+        lo = [-1, -1, z[k]]
+        hi = [1, 1, z[-1]]
+        bb.append(lo + hi)
+        info.append([k, n - k, 2 * k + 1, 2 * k + 2])
+        bb.append([-1, -1, z[k], 1, 1, z[k]])
+        info.append([k, 1, -1, -1])
+    bb.append([-1, -1, z[-1], 1, 1, z[-1]])
+    info.append([n - 1, 1, -1, -1])
+    d["node_bb"] = np.array(bb, np.float64).reshape(-1)
+    d["node_info"] = np.array(info, np.int64).reshape(-1)
+    return d
+
+
+def test_hip_deep_bvh_stack_spill_vs_restatement(restate, tmp_path):
+    from dsgpuraytracing_amd.pathtracer import Device
+    d = _deep_chain_scene()
+    path = str(tmp_path / "deep.ptd")
+    ptdump.write(path, d)
+    rng = np.random.default_rng(5)
+    m = 4096
+    o = np.stack([rng.uniform(-0.99, 0.99, m), rng.uniform(-0.99, 0.99, m), np.full(m, 2.0)], 1)
+    dr = np.stack([rng.uniform(-0.05, 0.05, m), rng.uniform(-0.05, 0.05, m), -np.ones(m)], 1)
+    dr /= np.linalg.norm(dr, axis=1, keepdims=True)
+    maxt = rng.uniform(1.0, 3.0, m)
+    dev = Device(0)
+    sc = Scene(native.SceneArrays(d))
+    dev.upload_scene(sc)
+    hit, t, prim, anyh = dev.intersect(o, dr, maxt)
+    dev.set_camera(sc.camera)
+    dev.set_params(64, 64, 2, 4, 1, 1)
+    dev.render_tiles([(0, 0, 64, 64)], np.zeros((64, 64, 3), np.float32))  # the render path with spill on
+    st = dev.stats()
+    assert st["bvh_stack"] > 32
+    rh, rt, rp, _, ra = restate.intersect(path, o.reshape(-1), dr.reshape(-1), maxt)
+    assert hit.mean() > 0.3 and np.array_equal(hit, rh)
+    both = hit == 1
+    assert np.array_equal(prim[both], rp[both])
+    assert np.allclose(t[both], rt[both], rtol=1e-5)
+    assert np.array_equal(anyh, ra)
+
+
 def test_hip_stats_counters():
     _, st = gpu_render("c1_default_64x64", 64, 64, 2, stats=True)
     assert st["counters_valid"] == 1
