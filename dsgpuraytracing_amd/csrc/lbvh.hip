@@ -1,0 +1,410 @@
+// lbvh.hip — GPU BVH build (linear BVH) for gfx950.
+//
+// Replaces the reference's PARALLEL_BUILD_BVH path, CUDAPathTracer::buildBVH
+// (cuda_src/setup.cu:478-686) with its kernels computeMorton / generateLeafNode /
+// generateInternalNode / buildBoundingBox / treeCollapse (cuda_src/kernel.cu:
+// 358-493) and helpers morton3D / delta / determineRange / findSplit /
+// propogateBBox (cuda_src/helper.cu:73-91, 354-458):
+//   1. 30-bit Morton code of each primitive's box centre in the scene box
+//      (the reference's quirks kept: NaN or a coordinate outside [0, 1) -> 0);
+//   2. stable key/value radix sort of the codes (thrust::sort_by_key there,
+//      hipCUB's onesweep radix sort here);
+//   3. Karras 2012 radix tree over (code << 32 | index) keys;
+//   4. bottom-up boxes, the second child to arrive completing its parent
+//      (agent-scope acquire/release: the per-XCD L2s are not coherent);
+//   5. subtrees of <= LEAF_NUMBER = 4 primitives collapse into leaves.
+// Then, MI355X-specific: the binary tree is emitted both as the 64-B binary
+// nodes of the reference-count launch and, breadth-first two levels at a time,
+// as the 128-B BVH4 nodes the renderer traverses (children allocated after
+// their parent, so references only point forward); primitives and normals are
+// gathered into sorted order; the worst-case traversal stack is computed on the
+// way down.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+#include "pt_device.h"
+
+namespace lbvh {
+
+constexpr int kLeafNumber = 4;  // kernel.cu:14 LEAF_NUMBER
+
+__device__ __forceinline__ uint32_t expand_bits(uint32_t v) {
+  v = (v * 0x00010001u) & 0xFF0000FFu;
+  v = (v * 0x00000101u) & 0x0F00F00Fu;
+  v = (v * 0x00000011u) & 0xC30C30C3u;
+  v = (v * 0x00000005u) & 0x49249249u;
+  return v;
+}
+
+__device__ __forceinline__ uint32_t morton3d(float x, float y, float z) {
+  x = fminf(fmaxf(x * 1024.0f, 0.0f), 1023.0f);
+  y = fminf(fmaxf(y * 1024.0f, 0.0f), 1023.0f);
+  z = fminf(fmaxf(z * 1024.0f, 0.0f), 1023.0f);
+  return expand_bits((uint32_t)x) * 4 + expand_bits((uint32_t)y) * 2 + expand_bits((uint32_t)z);
+}
+
+// Box of one primitive in the float layout (v0, e1, e2) / (c, r), widened by
+// one ulp each way: v0 + e is rounded, the triangle the renderer tests is not.
+__device__ __forceinline__ void prim_box(const DPrim& p, float lo[3], float hi[3]) {
+  const float v0[3] = {p.v0.x, p.v0.y, p.v0.z};
+  if (__float_as_int(p.v0.w) & 1) {
+    const float e1[3] = {p.e1.x, p.e1.y, p.e1.z}, e2[3] = {p.e2.x, p.e2.y, p.e2.z};
+    for (int i = 0; i < 3; ++i) {
+      lo[i] = nextafterf(v0[i] + fminf(fminf(0.0f, e1[i]), e2[i]), -INFINITY);
+      hi[i] = nextafterf(v0[i] + fmaxf(fmaxf(0.0f, e1[i]), e2[i]), INFINITY);
+    }
+  } else {
+    for (int i = 0; i < 3; ++i) {
+      lo[i] = nextafterf(v0[i] - p.e1.x, -INFINITY);
+      hi[i] = nextafterf(v0[i] + p.e1.x, INFINITY);
+    }
+  }
+}
+
+struct Params {
+  int n;
+  const DPrim* prims;   // input order
+  float smin[3], sext[3];
+  uint32_t* keys;       // sorted Morton codes
+  int* ids;             // sorted primitive ids
+  int* child;           // 2 per internal node: >= 0 internal index, < 0: ~leaf index
+  int* parent;          // parent of internal node i (n-1 entries), then of leaf j (n entries)
+  int* start;           // first sorted primitive of internal node i
+  int* range;           // primitive count of internal node i
+  float* box;           // 6 per internal node (lo xyz, hi xyz)
+  int* flag;            // arrivals per internal node
+};
+
+__global__ void k_morton(Params P) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.n) return;
+  const DPrim p = P.prims[i];
+  float c[3];
+  if (__float_as_int(p.v0.w) & 1) {  // triangle: centre of its box (kernel.cu:366-374)
+    const float v0[3] = {p.v0.x, p.v0.y, p.v0.z};
+    const float e1[3] = {p.e1.x, p.e1.y, p.e1.z}, e2[3] = {p.e2.x, p.e2.y, p.e2.z};
+    for (int k = 0; k < 3; ++k)
+      c[k] = v0[k] + 0.5f * (fminf(fminf(0.0f, e1[k]), e2[k]) + fmaxf(fmaxf(0.0f, e1[k]), e2[k]));
+  } else {
+    c[0] = p.v0.x;
+    c[1] = p.v0.y;
+    c[2] = p.v0.z;
+  }
+  for (int k = 0; k < 3; ++k) {
+    c[k] = (c[k] - P.smin[k]) / P.sext[k];
+    if (c[k] != c[k]) c[k] = 0.0f;
+    if (c[k] < 0.0f || c[k] >= 1.0f) c[k] = 0.0f;
+  }
+  P.keys[i] = morton3d(c[0], c[1], c[2]);
+  P.ids[i] = i;
+}
+
+__device__ __forceinline__ int delta(const Params& P, int i, int j) {
+  if (i < 0 || i >= P.n || j < 0 || j >= P.n) return -1;
+  const uint64_t a = ((uint64_t)P.keys[i] << 32) | (uint32_t)i;
+  const uint64_t b = ((uint64_t)P.keys[j] << 32) | (uint32_t)j;
+  return __clzll((long long)(a ^ b));
+}
+
+// Karras 2012: range and split of internal node i (helper.cu:371-435).
+__global__ void k_internal(Params P) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.n - 1) return;
+  const int d = (delta(P, i, i + 1) - delta(P, i, i - 1)) >= 0 ? 1 : -1;
+  const int dmin = delta(P, i, i - d);
+  int lmax = 2;
+  while (delta(P, i, i + lmax * d) > dmin) lmax <<= 1;
+  int l = 0;
+  for (int t = lmax >> 1; t >= 1; t >>= 1)
+    if (delta(P, i, i + (l + t) * d) > dmin) l += t;
+  const int j = i + l * d;
+  const int first = min(i, j), last = max(i, j);
+  const int common = delta(P, first, last);
+  int split = first, step = last - first;
+  do {
+    step = (step + 1) >> 1;
+    const int ns = split + step;
+    if (ns < last && delta(P, first, ns) > common) split = ns;
+  } while (step > 1);
+  const int a = split == first ? ~split : split;
+  const int b = split + 1 == last ? ~(split + 1) : split + 1;
+  P.child[2 * i] = a;
+  P.child[2 * i + 1] = b;
+  P.parent[a >= 0 ? a : (P.n - 1) + ~a] = i;
+  P.parent[b >= 0 ? b : (P.n - 1) + ~b] = i;
+  P.start[i] = first;
+  P.range[i] = last - first + 1;
+  P.flag[i] = 0;
+  if (i == 0) P.parent[0] = -1;
+}
+
+__device__ __forceinline__ void child_box(const Params& P, int c, float lo[3], float hi[3]) {
+  if (c < 0) {
+    prim_box(P.prims[P.ids[~c]], lo, hi);
+  } else {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = __hip_atomic_load(&P.box[6 * c + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      hi[k] = __hip_atomic_load(&P.box[6 * c + 3 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Bottom-up boxes (propogateBBox, helper.cu:437-458): one thread per leaf
+// climbs until it is the first to reach a node.
+__global__ void k_boxes(Params P) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= P.n || P.n < 2) return;
+  int node = P.parent[(P.n - 1) + j];
+  while (node >= 0) {
+    if (__hip_atomic_fetch_add(&P.flag[node], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+    float la[3], ha[3], lb[3], hb[3];
+    child_box(P, P.child[2 * node], la, ha);
+    child_box(P, P.child[2 * node + 1], lb, hb);
+    for (int k = 0; k < 3; ++k) {
+      __hip_atomic_store(&P.box[6 * node + k], fminf(la[k], lb[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&P.box[6 * node + 3 + k], fmaxf(ha[k], hb[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    node = P.parent[node];
+  }
+}
+
+// Children of binary node c as the renderer sees them: a collapsed subtree
+// (range <= LEAF_NUMBER, treeCollapse kernel.cu:475-485) or a real leaf is a
+// leaf cursor, otherwise the internal index.
+__device__ __forceinline__ int as_ref(const Params& P, int c) {
+  if (c < 0) return ~((~c) << 3);  // one primitive: count 1
+  if (P.range[c] <= kLeafNumber) return ~((P.start[c] << 3) | (P.range[c] - 1));
+  return c;
+}
+
+__device__ __forceinline__ void ref_box(const Params& P, int c, float lo[3], float hi[3]) { child_box(P, c, lo, hi); }
+
+// Binary nodes for the reference-count launch (node index = Karras index).
+__global__ void k_emit_bin(Params P, DNode2* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.n - 1) return;
+  float l0[3], h0[3], l1[3], h1[3];
+  const int c0 = P.child[2 * i], c1 = P.child[2 * i + 1];
+  ref_box(P, c0, l0, h0);
+  ref_box(P, c1, l1, h1);
+  DNode2 d;
+  d.a = make_float4(l0[0], h0[0], l0[1], h0[1]);
+  d.b = make_float4(l1[0], h1[0], l1[1], h1[1]);
+  d.c = make_float4(l0[2], h0[2], l1[2], h1[2]);
+  d.e = make_int4(as_ref(P, c0), as_ref(P, c1), 0, 0);
+  out[i] = d;
+}
+
+struct Item {
+  int bin;    // internal binary node (not collapsed)
+  int idx;    // its BVH4 node index
+  int stack;  // worst-case stack entries on entering it
+};
+
+// One breadth-first level: each BVH4 node takes up to four children by opening
+// both (non-collapsed internal) children of its binary node.
+__global__ void k_bfs(Params P, const Item* __restrict__ in, int n_in, Item* out, int* n_out, int* n_nodes,
+                      int* max_stack, DNode* nodes) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_in) return;
+  const Item it = in[t];
+  int kids[4];
+  int nk = 0;
+  for (int s = 0; s < 2; ++s) {
+    const int c = P.child[2 * it.bin + s];
+    if (c >= 0 && P.range[c] > kLeafNumber) {
+      kids[nk++] = P.child[2 * c];
+      kids[nk++] = P.child[2 * c + 1];
+    } else {
+      kids[nk++] = c;
+    }
+  }
+  const int below = it.stack + nk - 1;
+  atomicMax(max_stack, below);
+  float lo[3][4], hi[3][4];
+  int ref[4];
+  for (int k = 0; k < 4; ++k) {
+    if (k < nk) {
+      float l[3], h[3];
+      ref_box(P, kids[k], l, h);
+      for (int a = 0; a < 3; ++a) {
+        lo[a][k] = l[a];
+        hi[a][k] = h[a];
+      }
+      int r = as_ref(P, kids[k]);
+      if (r >= 0) {  // internal: allocate its BVH4 node (after this one: forward reference)
+        const int idx = atomicAdd(n_nodes, 1);
+        out[atomicAdd(n_out, 1)] = Item{kids[k], idx, below};
+        r = idx;
+      }
+      ref[k] = r;
+    } else {  // empty slot: box at +inf
+      for (int a = 0; a < 3; ++a) lo[a][k] = hi[a][k] = __int_as_float(0x7f800000);
+      ref[k] = 0;
+    }
+  }
+  DNode d;
+  d.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
+  d.hix = make_float4(hi[0][0], hi[0][1], hi[0][2], hi[0][3]);
+  d.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
+  d.hiy = make_float4(hi[1][0], hi[1][1], hi[1][2], hi[1][3]);
+  d.loz = make_float4(lo[2][0], lo[2][1], lo[2][2], lo[2][3]);
+  d.hiz = make_float4(hi[2][0], hi[2][1], hi[2][2], hi[2][3]);
+  d.ref = make_int4(ref[0], ref[1], ref[2], ref[3]);
+  d.pad = make_int4(0, 0, 0, 0);
+  nodes[it.idx] = d;
+}
+
+// Primitives, vertex normals and the sorted -> input id map in sorted order.
+__global__ void k_gather(Params P, const float* __restrict__ norms_in, DPrim* prims_out, float* norms_out,
+                         int* prim_map) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.n) return;
+  const int s = P.ids[i];
+  prims_out[i] = P.prims[s];
+  for (int k = 0; k < 9; ++k) norms_out[9 * (size_t)i + k] = norms_in[9 * (size_t)s + k];
+  prim_map[i] = s;
+}
+
+}  // namespace lbvh
+
+#define LB_CHK(x)                   \
+  do {                              \
+    hipError_t e_ = (x);            \
+    if (e_ != hipSuccess) return e_; \
+  } while (0)
+
+extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t s) {
+  using namespace lbvh;
+  const int n = in->n;
+  *out = LbvhOut{};
+  Params P{};
+  P.n = n;
+  P.prims = in->prims;
+  for (int k = 0; k < 3; ++k) {
+    P.smin[k] = in->scene_min[k];
+    P.sext[k] = in->scene_extent[k];
+  }
+  // scratch
+  uint32_t *keys_a = nullptr, *keys_b = nullptr;
+  int *ids_a = nullptr, *ids_b = nullptr, *ints = nullptr;
+  float* box = nullptr;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  const size_t ni = (size_t)(n > 1 ? n - 1 : 1);
+  LB_CHK(hipMalloc(&keys_a, (size_t)n * 4));
+  LB_CHK(hipMalloc(&keys_b, (size_t)n * 4));
+  LB_CHK(hipMalloc(&ids_a, (size_t)n * 4));
+  LB_CHK(hipMalloc(&ids_b, (size_t)n * 4));
+  LB_CHK(hipMalloc(&ints, (ni * 2 + ni + n + ni + ni + ni + 4) * 4));
+  LB_CHK(hipMalloc(&box, ni * 6 * 4));
+  const int B = 256;
+  const int gn = (n + B - 1) / B, gi = (int)((ni + B - 1) / B);
+  P.keys = keys_a;
+  P.ids = ids_a;
+  hipLaunchKernelGGL(k_morton, dim3(gn), dim3(B), 0, s, P);
+  LB_CHK(hipGetLastError());
+  LB_CHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys_a, keys_b, ids_a, ids_b, n, 0, 30, s));
+  LB_CHK(hipMalloc(&tmp, tmp_bytes));
+  LB_CHK(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys_a, keys_b, ids_a, ids_b, n, 0, 30, s));
+  P.keys = keys_b;
+  P.ids = ids_b;
+  P.child = ints;
+  P.parent = P.child + 2 * ni;
+  P.start = P.parent + ni + n;
+  P.range = P.start + ni;
+  P.flag = P.range + ni;
+  int* counters = P.flag + ni;  // n_nodes, n_out, max_stack, spare
+  P.box = box;
+  LB_CHK(hipMemsetAsync(counters, 0, 16, s));
+  // outputs
+  LB_CHK(hipMalloc(&out->prims, (size_t)n * sizeof(DPrim)));
+  LB_CHK(hipMalloc(&out->norms, (size_t)n * 9 * 4));
+  LB_CHK(hipMalloc(&out->prim_map, (size_t)n * 4));
+  LB_CHK(hipMalloc(&out->nodes4, (size_t)(ni + 1) * sizeof(DNode)));
+  LB_CHK(hipMalloc(&out->nodes2, ni * sizeof(DNode2)));
+  hipLaunchKernelGGL(k_gather, dim3(gn), dim3(B), 0, s, P, in->norms, out->prims, out->norms, out->prim_map);
+  LB_CHK(hipGetLastError());
+  if (n <= kLeafNumber) {  // a single leaf: one BVH4 node, one child, as the host path
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = in->scene_min[k];
+      hi[k] = in->scene_min[k] + in->scene_extent[k];
+    }
+    DNode d{};
+    float inf = INFINITY;
+    d.lox = make_float4(lo[0], inf, inf, inf);
+    d.hix = make_float4(hi[0], inf, inf, inf);
+    d.loy = make_float4(lo[1], inf, inf, inf);
+    d.hiy = make_float4(hi[1], inf, inf, inf);
+    d.loz = make_float4(lo[2], inf, inf, inf);
+    d.hiz = make_float4(hi[2], inf, inf, inf);
+    d.ref = make_int4(~((0 << 3) | (n - 1)), 0, 0, 0);
+    LB_CHK(hipMemcpyAsync(out->nodes4, &d, sizeof(d), hipMemcpyHostToDevice, s));
+    DNode2 b{};
+    b.a = make_float4(lo[0], hi[0], lo[1], hi[1]);
+    b.b = make_float4(inf, inf, inf, inf);
+    b.c = make_float4(lo[2], hi[2], inf, inf);
+    b.e = make_int4(~((0 << 3) | (n - 1)), 0, 0, 0);
+    LB_CHK(hipMemcpyAsync(out->nodes2, &b, sizeof(b), hipMemcpyHostToDevice, s));
+    LB_CHK(hipStreamSynchronize(s));
+    out->n4 = 1;
+    out->n2 = 1;
+    out->max_stack = 1;
+    for (int k = 0; k < 3; ++k) {
+      out->root_lo[k] = lo[k];
+      out->root_hi[k] = hi[k];
+    }
+  } else {
+    hipLaunchKernelGGL(k_internal, dim3(gi), dim3(B), 0, s, P);
+    LB_CHK(hipGetLastError());
+    hipLaunchKernelGGL(k_boxes, dim3(gn), dim3(B), 0, s, P);
+    LB_CHK(hipGetLastError());
+    hipLaunchKernelGGL(k_emit_bin, dim3(gi), dim3(B), 0, s, P, out->nodes2);
+    LB_CHK(hipGetLastError());
+    // breadth-first BVH4 emission from the root (binary node 0 -> BVH4 node 0)
+    Item *fa = nullptr, *fb = nullptr;
+    LB_CHK(hipMalloc(&fa, (ni + 1) * sizeof(Item)));
+    LB_CHK(hipMalloc(&fb, (ni + 1) * sizeof(Item)));
+    Item root{0, 0, 0};
+    int one = 1;
+    LB_CHK(hipMemcpyAsync(fa, &root, sizeof(root), hipMemcpyHostToDevice, s));
+    LB_CHK(hipMemcpyAsync(counters, &one, 4, hipMemcpyHostToDevice, s));  // n_nodes = 1 (the root)
+    int n_in = 1;
+    while (n_in > 0) {  // one launch per two binary levels
+      LB_CHK(hipMemsetAsync(counters + 1, 0, 4, s));
+      hipLaunchKernelGGL(k_bfs, dim3((n_in + B - 1) / B), dim3(B), 0, s, P, fa, n_in, fb, counters + 1, counters,
+                         counters + 2, out->nodes4);
+      LB_CHK(hipGetLastError());
+      LB_CHK(hipMemcpyAsync(&n_in, counters + 1, 4, hipMemcpyDeviceToHost, s));
+      LB_CHK(hipStreamSynchronize(s));
+      Item* t = fa;
+      fa = fb;
+      fb = t;
+    }
+    int cnt[3] = {0, 0, 0};
+    LB_CHK(hipMemcpyAsync(cnt, counters, 12, hipMemcpyDeviceToHost, s));
+    float rb[6];
+    LB_CHK(hipMemcpyAsync(rb, box, 24, hipMemcpyDeviceToHost, s));
+    LB_CHK(hipStreamSynchronize(s));
+    out->n4 = cnt[0];
+    out->n2 = (int)ni;
+    out->max_stack = cnt[2];
+    for (int k = 0; k < 3; ++k) {
+      out->root_lo[k] = rb[k];
+      out->root_hi[k] = rb[3 + k];
+    }
+    (void)hipFree(fa);
+    (void)hipFree(fb);
+  }
+  (void)hipFree(keys_a);
+  (void)hipFree(keys_b);
+  (void)hipFree(ids_a);
+  (void)hipFree(ids_b);
+  (void)hipFree(ints);
+  (void)hipFree(box);
+  (void)hipFree(tmp);
+  return hipSuccess;
+}

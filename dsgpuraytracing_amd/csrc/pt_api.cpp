@@ -58,6 +58,11 @@ struct DevBuf {
     p = nullptr;
     n = 0;
   }
+  void adopt(T* q, size_t count) {  // take ownership of a hipMalloc'd array
+    release();
+    p = q;
+    n = count;
+  }
 };
 
 float round_down(double x) {
@@ -122,6 +127,7 @@ struct pt_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   DevBuf<DNode> nodes;
   DevBuf<DNode2> nodes2;  // binary tree for PT_FLAG_REF_COUNTS
+  DevBuf<int> prim_map;   // GPU-built BVH: sorted primitive -> uploaded index (else empty)
   DevBuf<float4> env_tex;          // environment map RGB (w*h, .w unused)
   DevBuf<float> env_ptheta, env_pphi, env_pdf;  // EnvironmentLight tables
   int env_w = 0, env_h = 0;
@@ -193,6 +199,7 @@ int pt_destroy(pt_ctx* c) {
   (void)hipSetDevice(c->device);
   c->nodes.release();
   c->nodes2.release();
+  c->prim_map.release();
   c->env_tex.release();
   c->env_ptheta.release();
   c->env_pphi.release();
@@ -217,45 +224,9 @@ int pt_destroy(pt_ctx* c) {
   return PT_OK;
 }
 
-int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
-  if (!c || !s) return fail(PT_E_INVALID, "pt_upload_scene: NULL argument");
-  if (s->n_prims <= 0 || s->n_nodes <= 0 || !s->prim_type || !s->prim_bsdf || !s->prim_geom || !s->prim_norm ||
-      !s->nodes)
-    return fail(PT_E_INVALID, "pt_upload_scene: empty scene");
-  if (s->n_bsdfs <= 0 || !s->bsdfs) return fail(PT_E_INVALID, "pt_upload_scene: no BSDFs");
-  if (s->n_lights < 0 || (s->n_lights > 0 && !s->lights)) return fail(PT_E_INVALID, "pt_upload_scene: bad lights");
-  if (s->n_prims > (int64_t)0x3fffffff) return fail(PT_E_INVALID, "pt_upload_scene: too many primitives");
-  HIPCHK(hipSetDevice(c->device));
-
-  // ---- primitives (already in BVH order)
-  std::vector<DPrim> prims((size_t)s->n_prims);
-  std::vector<float> norms((size_t)s->n_prims * 9);
-  for (int64_t i = 0; i < s->n_prims; ++i) {
-    const double* g = s->prim_geom + 9 * i;
-    const double* n = s->prim_norm + 9 * i;
-    int b = s->prim_bsdf[i];
-    if (b < 0 || b >= s->n_bsdfs) return fail(PT_E_INVALID, "pt_upload_scene: primitive BSDF index out of range");
-    DPrim& P = prims[(size_t)i];
-    if (s->prim_type[i] == PT_PRIM_TRIANGLE) {
-      int meta = (b << 1) | 1;
-      float mf;
-      std::memcpy(&mf, &meta, 4);
-      P.v0 = make_float4((float)g[0], (float)g[1], (float)g[2], mf);
-      P.e1 = make_float4((float)(g[3] - g[0]), (float)(g[4] - g[1]), (float)(g[5] - g[2]), 0.f);
-      P.e2 = make_float4((float)(g[6] - g[0]), (float)(g[7] - g[1]), (float)(g[8] - g[2]), 0.f);
-      for (int k = 0; k < 9; ++k) norms[9 * i + k] = (float)n[k];
-    } else if (s->prim_type[i] == PT_PRIM_SPHERE) {
-      int meta = (b << 1);
-      float mf;
-      std::memcpy(&mf, &meta, 4);
-      P.v0 = make_float4((float)g[0], (float)g[1], (float)g[2], mf);
-      P.e1 = make_float4((float)g[3], (float)(g[3] * g[3]), 0.f, 0.f);
-      P.e2 = make_float4(0.f, 0.f, 0.f, 0.f);
-    } else {
-      return fail(PT_E_INVALID, "pt_upload_scene: unknown primitive type");
-    }
-  }
-
+// Reference BVH (pt_scene.nodes) -> BVH4 nodes (dn), binary nodes (d2) and
+// the worst-case traversal stack.
+static int build_host_bvh(const pt_scene* s, std::vector<DNode>& dn, std::vector<DNode2>& d2, int& max_stack) {
   // ---- BVH: internal nodes only, pre-order, child boxes rounded outward;
   // leaves become cursors in their parent's child references.  Leaves of more
   // than 8 primitives are split into small subtrees over primitive boxes.
@@ -381,8 +352,7 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
       out[s2].ref = b2[(size_t)n].ref[s2];
     }
   };
-  std::vector<DNode> dn;
-  int max_stack = 0;
+  max_stack = 0;
   {
     struct Item4 { int b2node; int64_t parent; int slot; int stack; };
     std::vector<Item4> st = {{0, -1, 0, 0}};
@@ -444,8 +414,101 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
   if (max_stack > PT_STACK_MAX)
     return fail(PT_E_INVALID, "pt_upload_scene: BVH needs a deeper traversal stack (" + std::to_string(max_stack) +
                                   " > " + std::to_string(PT_STACK_MAX) + ")");
-  c->bvh_stack = max_stack;
-  c->n_nodes4 = dn.size();
+
+  d2.resize(b2.size());
+  for (size_t i = 0; i < b2.size(); ++i) {
+    const B2& q = b2[i];
+    d2[i].a = make_float4(q.lo[0][0], q.hi[0][0], q.lo[0][1], q.hi[0][1]);
+    d2[i].b = make_float4(q.lo[1][0], q.hi[1][0], q.lo[1][1], q.hi[1][1]);
+    d2[i].c = make_float4(q.lo[0][2], q.hi[0][2], q.lo[1][2], q.hi[1][2]);
+    d2[i].e = make_int4(q.ref[0], q.ref[1], 0, 0);
+  }
+  return PT_OK;
+}
+
+// GPU linear-BVH build over the primitives already in c->prims / c->norms
+// (CUDAPathTracer::buildBVH, cuda_src/setup.cu:478-686; kernels in lbvh.hip).
+static int build_gpu_bvh(pt_ctx* c, const pt_scene* s) {
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int64_t i = 0; i < s->n_prims; ++i) {  // sceneBox.expand(prim->get_bbox()) (setup.cu:482-487)
+    const double* g = s->prim_geom + 9 * i;
+    for (int k = 0; k < 3; ++k) {
+      if (s->prim_type[i] == PT_PRIM_TRIANGLE) {
+        lo[k] = std::min({lo[k], g[k], g[3 + k], g[6 + k]});
+        hi[k] = std::max({hi[k], g[k], g[3 + k], g[6 + k]});
+      } else {
+        lo[k] = std::min(lo[k], g[k] - std::fabs(g[3]));
+        hi[k] = std::max(hi[k], g[k] + std::fabs(g[3]));
+      }
+    }
+  }
+  LbvhIn in{};
+  in.n = (int)s->n_prims;
+  in.prims = c->prims.p;
+  in.norms = c->norms.p;
+  for (int k = 0; k < 3; ++k) {
+    in.scene_min[k] = round_down(lo[k]);
+    in.scene_extent[k] = (float)(hi[k] - lo[k]);
+  }
+  LbvhOut out{};
+  HIPCHK(ptk_build_lbvh(&in, &out, c->stream));
+  c->prims.adopt(out.prims, (size_t)in.n);
+  c->norms.adopt(out.norms, (size_t)in.n * 9);
+  c->prim_map.adopt(out.prim_map, (size_t)in.n);
+  c->nodes.adopt(out.nodes4, (size_t)out.n4);
+  c->nodes2.adopt(out.nodes2, (size_t)std::max(1, out.n2));
+  if (out.max_stack > PT_STACK_MAX)
+    return fail(PT_E_INVALID, "pt_upload_scene_lbvh: BVH needs a deeper traversal stack (" +
+                                  std::to_string(out.max_stack) + " > " + std::to_string(PT_STACK_MAX) + ")");
+  c->bvh_stack = out.max_stack;
+  c->n_nodes4 = (size_t)out.n4;
+  for (int k = 0; k < 3; ++k) {
+    c->root_lo[k] = out.root_lo[k];
+    c->root_hi[k] = out.root_hi[k];
+    c->root_lo_d[k] = out.root_lo[k];
+    c->root_hi_d[k] = out.root_hi[k];
+  }
+  return PT_OK;
+}
+
+static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
+  if (!c || !s) return fail(PT_E_INVALID, "pt_upload_scene: NULL argument");
+  if (s->n_prims <= 0 || !s->prim_type || !s->prim_bsdf || !s->prim_geom || !s->prim_norm ||
+      (!gpu_bvh && (s->n_nodes <= 0 || !s->nodes)))
+    return fail(PT_E_INVALID, "pt_upload_scene: empty scene");
+  if (s->n_bsdfs <= 0 || !s->bsdfs) return fail(PT_E_INVALID, "pt_upload_scene: no BSDFs");
+  if (s->n_lights < 0 || (s->n_lights > 0 && !s->lights)) return fail(PT_E_INVALID, "pt_upload_scene: bad lights");
+  if (s->n_prims > (int64_t)0x3fffffff) return fail(PT_E_INVALID, "pt_upload_scene: too many primitives");
+  HIPCHK(hipSetDevice(c->device));
+
+  // ---- primitives (already in BVH order)
+  std::vector<DPrim> prims((size_t)s->n_prims);
+  std::vector<float> norms((size_t)s->n_prims * 9);
+  for (int64_t i = 0; i < s->n_prims; ++i) {
+    const double* g = s->prim_geom + 9 * i;
+    const double* n = s->prim_norm + 9 * i;
+    int b = s->prim_bsdf[i];
+    if (b < 0 || b >= s->n_bsdfs) return fail(PT_E_INVALID, "pt_upload_scene: primitive BSDF index out of range");
+    DPrim& P = prims[(size_t)i];
+    if (s->prim_type[i] == PT_PRIM_TRIANGLE) {
+      int meta = (b << 1) | 1;
+      float mf;
+      std::memcpy(&mf, &meta, 4);
+      P.v0 = make_float4((float)g[0], (float)g[1], (float)g[2], mf);
+      P.e1 = make_float4((float)(g[3] - g[0]), (float)(g[4] - g[1]), (float)(g[5] - g[2]), 0.f);
+      P.e2 = make_float4((float)(g[6] - g[0]), (float)(g[7] - g[1]), (float)(g[8] - g[2]), 0.f);
+      for (int k = 0; k < 9; ++k) norms[9 * i + k] = (float)n[k];
+    } else if (s->prim_type[i] == PT_PRIM_SPHERE) {
+      int meta = (b << 1);
+      float mf;
+      std::memcpy(&mf, &meta, 4);
+      P.v0 = make_float4((float)g[0], (float)g[1], (float)g[2], mf);
+      P.e1 = make_float4((float)g[3], (float)(g[3] * g[3]), 0.f, 0.f);
+      P.e2 = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      return fail(PT_E_INVALID, "pt_upload_scene: unknown primitive type");
+    }
+  }
 
   std::vector<DBsdf> bs((size_t)s->n_bsdfs);
   for (int i = 0; i < s->n_bsdfs; ++i) {
@@ -487,24 +550,36 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
   EnvTables env;
   if (n_env) build_env_tables(s->env_rgb, s->env_width, s->env_height, env);
 
-  std::vector<DNode2> d2(b2.size());
-  for (size_t i = 0; i < b2.size(); ++i) {
-    const B2& q = b2[i];
-    d2[i].a = make_float4(q.lo[0][0], q.hi[0][0], q.lo[0][1], q.hi[0][1]);
-    d2[i].b = make_float4(q.lo[1][0], q.hi[1][0], q.lo[1][1], q.hi[1][1]);
-    d2[i].c = make_float4(q.lo[0][2], q.hi[0][2], q.lo[1][2], q.hi[1][2]);
-    d2[i].e = make_int4(q.ref[0], q.ref[1], 0, 0);
-  }
-  HIPCHK(c->nodes2.reserve(d2.size()));
-  HIPCHK(hipMemcpy(c->nodes2.p, d2.data(), d2.size() * sizeof(DNode2), hipMemcpyHostToDevice));
-  HIPCHK(c->nodes.reserve(dn.size()));
   HIPCHK(c->prims.reserve(prims.size()));
   HIPCHK(c->norms.reserve(norms.size()));
   HIPCHK(c->bsdfs.reserve(bs.size()));
   HIPCHK(c->lights.reserve(std::max<size_t>(1, ls.size())));
-  HIPCHK(hipMemcpy(c->nodes.p, dn.data(), dn.size() * sizeof(DNode), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(c->prims.p, prims.data(), prims.size() * sizeof(DPrim), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(c->norms.p, norms.data(), norms.size() * sizeof(float), hipMemcpyHostToDevice));
+  c->prim_map.release();
+  if (!gpu_bvh) {
+    std::vector<DNode> dn;
+    std::vector<DNode2> d2;
+    int max_stack = 0;
+    int rc = build_host_bvh(s, dn, d2, max_stack);
+    if (rc) return rc;
+    HIPCHK(c->nodes2.reserve(d2.size()));
+    HIPCHK(hipMemcpy(c->nodes2.p, d2.data(), d2.size() * sizeof(DNode2), hipMemcpyHostToDevice));
+    HIPCHK(c->nodes.reserve(dn.size()));
+    HIPCHK(hipMemcpy(c->nodes.p, dn.data(), dn.size() * sizeof(DNode), hipMemcpyHostToDevice));
+    c->bvh_stack = max_stack;
+    c->n_nodes4 = dn.size();
+    const pt_bvh_node* N = s->nodes;
+    for (int k = 0; k < 3; ++k) {
+      c->root_lo[k] = round_down(N[0].bb_min[k]);
+      c->root_hi[k] = round_up(N[0].bb_max[k]);
+      c->root_lo_d[k] = N[0].bb_min[k];
+      c->root_hi_d[k] = N[0].bb_max[k];
+    }
+  } else {
+    int rc = build_gpu_bvh(c, s);
+    if (rc) return rc;
+  }
   HIPCHK(hipMemcpy(c->bsdfs.p, bs.data(), bs.size() * sizeof(DBsdf), hipMemcpyHostToDevice));
   if (!ls.empty()) HIPCHK(hipMemcpy(c->lights.p, ls.data(), ls.size() * sizeof(DLight), hipMemcpyHostToDevice));
   c->env_w = n_env ? s->env_width : 0;
@@ -522,15 +597,13 @@ int pt_upload_scene(pt_ctx* c, const pt_scene* s) {
   c->n_lights = (int)ls.size();
   c->n_bsdfs = (int)bs.size();
   c->n_prims = s->n_prims;
-  for (int k = 0; k < 3; ++k) {
-    c->root_lo[k] = round_down(N[0].bb_min[k]);
-    c->root_hi[k] = round_up(N[0].bb_max[k]);
-    c->root_lo_d[k] = N[0].bb_min[k];
-    c->root_hi_d[k] = N[0].bb_max[k];
-  }
   c->have_scene = true;
   return PT_OK;
 }
+
+int pt_upload_scene(pt_ctx* c, const pt_scene* s) { return upload_impl(c, s, false); }
+
+int pt_upload_scene_lbvh(pt_ctx* c, const pt_scene* s) { return upload_impl(c, s, true); }
 
 int pt_set_camera(pt_ctx* c, const pt_camera* cam) {
   if (!c || !cam) return fail(PT_E_INVALID, "pt_set_camera: NULL argument");
@@ -857,7 +930,7 @@ int pt_intersect(pt_ctx* c, int64_t n, const double* o, const double* d, const d
     spill = c->spill.p;
   }
   HIPCHK(ptk_launch_intersect(c->nodes.p, c->prims.p, c->q_f.p, c->q_f.p + 3 * n, c->q_f.p + 6 * n, n, dh, dt, dp, da,
-                              spill, c->stream));
+                              spill, c->prim_map.p, c->stream));
   std::vector<int32_t> ib((size_t)n * 3);
   std::vector<float> tb((size_t)n);
   HIPCHK(hipMemcpyAsync(ib.data(), c->q_i.p, ib.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));

@@ -118,9 +118,30 @@ struct KParams {
   int cull_x0, cull_y0, cull_x1, cull_y1;  // pixels outside [x0,x1]x[y0,y1] see no geometry
 };
 
+// GPU BVH build (lbvh.hip).  Inputs in upload order; outputs hipMalloc'd by
+// the builder (the caller owns and frees them).
+struct LbvhIn {
+  int n;
+  const DPrim* prims;    // device, input order
+  const float* norms;    // device, 9 per primitive
+  float scene_min[3], scene_extent[3];  // scene box (rounded outward)
+};
+struct LbvhOut {
+  DPrim* prims;          // sorted order
+  float* norms;
+  int* prim_map;         // sorted index -> input index
+  DNode* nodes4;
+  int n4;
+  DNode2* nodes2;
+  int n2;
+  int max_stack;         // worst-case traversal stack of nodes4
+  float root_lo[3], root_hi[3];
+};
+extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t s);
+
 extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, bool ref_counts, hipStream_t s);
 extern "C" hipError_t ptk_launch_resolve(const KParams* P, hipStream_t s);
 extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prims, const float* o, const float* d,
                                            const float* maxt, int64_t n, int32_t* hit, float* t, int32_t* prim,
-                                           int32_t* anyhit, int* spill, hipStream_t s);
+                                           int32_t* anyhit, int* spill, const int* prim_map, hipStream_t s);
 extern "C" hipError_t ptk_render_occupancy(int* blocks_per_cu, bool stats);

@@ -898,7 +898,7 @@ __global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __rest
                                                            const DPrim* __restrict__ prims, const float* __restrict__ o,
                                                            const float* __restrict__ d, const float* __restrict__ maxt,
                                                            int64_t n, int32_t* hit, float* t, int32_t* prim,
-                                                           int32_t* anyhit, int* spill) {
+                                                           int32_t* anyhit, int* spill, const int* prim_map) {
   __shared__ int s_stack[PT_STACK * PT_BLOCK];
   int64_t i = (int64_t)blockIdx.x * PT_BLOCK + threadIdx.x;
   const Stack stk{s_stack + threadIdx.x, spill ? spill + i : nullptr, gridDim.x * PT_BLOCK};
@@ -913,7 +913,7 @@ __global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __rest
   bool f = traverse<false>(nodes, prims, stk, O, D, 3.0e38f, false, h, ct);
   hit[i] = f ? 1 : 0;
   t[i] = f ? h.t : -1.0f;
-  prim[i] = f ? h.prim : -1;
+  prim[i] = f ? (prim_map ? prim_map[h.prim] : h.prim) : -1;
   Hit h2;
   bool a = traverse<false>(nodes, prims, stk, O, D, maxt[i], true, h2, ct);
   anyhit[i] = a ? 1 : 0;
@@ -950,11 +950,11 @@ extern "C" hipError_t ptk_launch_resolve(const KParams* P, hipStream_t s) {
 
 extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prims, const float* o, const float* d,
                                            const float* maxt, int64_t n, int32_t* hit, float* t, int32_t* prim,
-                                           int32_t* anyhit, int* spill, hipStream_t s) {
+                                           int32_t* anyhit, int* spill, const int* prim_map, hipStream_t s) {
   int grid = (int)((n + PT_BLOCK - 1) / PT_BLOCK);
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL(ptk::intersect_kernel, dim3(grid), dim3(PT_BLOCK), 0, s, nodes, prims, o, d, maxt, n, hit, t,
-                     prim, anyhit, spill);
+                     prim, anyhit, spill, prim_map);
   return hipGetLastError();
 }
 

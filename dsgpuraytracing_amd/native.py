@@ -97,6 +97,7 @@ _SIGS = {
     "pt_create": (c_int32, [c_int32, POINTER(c_void_p)]),
     "pt_destroy": (c_int32, [c_void_p]),
     "pt_upload_scene": (c_int32, [c_void_p, POINTER(pt_scene)]),
+    "pt_upload_scene_lbvh": (c_int32, [c_void_p, POINTER(pt_scene)]),
     "pt_set_camera": (c_int32, [c_void_p, POINTER(pt_camera)]),
     "pt_set_params": (c_int32, [c_void_p, POINTER(pt_params)]),
     "pt_render_tiles": (c_int32, [c_void_p, POINTER(pt_tile), c_int32, c_void_p, c_uint32]),

@@ -63,8 +63,11 @@ class Device:
         except Exception:
             pass
 
-    def upload_scene(self, scene: "Scene"):
-        check(self._lib.pt_upload_scene(self.handle, ctypes.byref(scene.arrays.scene)))
+    def upload_scene(self, scene: "Scene", gpu_bvh: bool = False):
+        """gpu_bvh: build a linear BVH on the device (pt_upload_scene_lbvh, the
+        reference's PARALLEL_BUILD_BVH path) instead of using the scene's BVH."""
+        fn = self._lib.pt_upload_scene_lbvh if gpu_bvh else self._lib.pt_upload_scene
+        check(fn(self.handle, ctypes.byref(scene.arrays.scene)))
         self._scene_keepalive = scene
 
     def set_camera(self, cam: native.pt_camera):
@@ -170,9 +173,14 @@ def to_color(hdr: np.ndarray) -> np.ndarray:
 class PathTracer:
     def __init__(self, ns_aa: int = 1, max_ray_depth: int = 4, ns_area_light: int = 1, ns_diff: int = 1,
                  ns_glsy: int = 1, ns_refr: int = 1, num_threads: int = 1, envmap=None, device: int = 0,
-                 seed: int = 1):
-        if envmap is not None:
-            raise NotImplementedError("environment lights are not on the HIP path yet (SURVEY §8(f) rank 3)")
+                 seed: int = 1, gpu_bvh: bool = False):
+        # envmap: an OpenEXR path or a float (h, w, 3) lat-long array; like the
+        # reference (pathtracer.cpp:42-46, 88-90) it becomes an EnvironmentLight
+        # appended to the scene's lights in set_scene.
+        if isinstance(envmap, str):
+            from . import scene_loader
+            envmap = scene_loader.load_exr(envmap)
+        self.envmap = None if envmap is None else np.ascontiguousarray(envmap, dtype=np.float32)
         self.state = State.INIT
         self.ns_aa = int(ns_aa)
         self.max_ray_depth = int(max_ray_depth)
@@ -186,6 +194,7 @@ class PathTracer:
         self.sampleBuffer = np.zeros((0, 0, 3), np.float32)
         self.frameBuffer = np.zeros((0, 0, 4), np.uint8)
         self._device_index = device
+        self.gpu_bvh = bool(gpu_bvh)  # build the BVH on the GPU (PARALLEL_BUILD_BVH, setup.cu:188-189)
         self._dev: Optional[Device] = None
         self.last_stats: dict = {}
 
@@ -201,8 +210,18 @@ class PathTracer:
     def set_scene(self, scene: Scene):
         if self.state != State.INIT:
             return
+        if self.envmap is not None and "env_rgb" not in scene.arrays.d:
+            d = dict(scene.arrays.d)
+            h, w, _ = self.envmap.shape
+            d["light_type"] = np.append(d["light_type"], np.int32(native.PT_LIGHT_ENVIRONMENT)).astype(np.int32)
+            d["light_rad"] = np.append(d["light_rad"], np.zeros(3, np.float32))
+            d["light_geom"] = np.append(d["light_geom"], np.zeros(12))
+            d["light_area"] = np.append(d["light_area"], np.float32(0))
+            d["env_shape"] = np.array([h, w], np.int64)
+            d["env_rgb"] = self.envmap.reshape(-1)
+            scene = Scene(native.SceneArrays(d))
         self.scene = scene
-        self._device().upload_scene(scene)
+        self._device().upload_scene(scene, gpu_bvh=self.gpu_bvh)
         if self.has_valid_configuration():
             self.state = State.READY
 

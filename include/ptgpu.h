@@ -7,6 +7,10 @@
  *                               (cuda_src/setup.h:90-148, setup.cu:92-115)
  *   pt_upload_scene             CUDAPathTracer::init -> loadPrimitives/loadLights/
  *                               loadBVH (setup.cu:181-201, 249-476, 689-774)
+ *   pt_upload_scene_lbvh        the same with the BVH built on the GPU: the reference's
+ *                               PARALLEL_BUILD_BVH path CUDAPathTracer::buildBVH
+ *                               (setup.cu:188-189, 478-686; kernel.cu:358-493) —
+ *                               scene.nodes is ignored (may be NULL)
  *   pt_set_camera               CUDAPathTracer::loadCamera (setup.cu:221-247);
  *                               camera semantics of Camera::generate_ray
  *                               (src/camera.cpp:113-129)
@@ -188,6 +192,11 @@ typedef struct pt_stats {
 int pt_create(int device, pt_ctx** out);
 int pt_destroy(pt_ctx* ctx);
 int pt_upload_scene(pt_ctx* ctx, const pt_scene* scene);
+/* Uploads the scene and builds a linear BVH on the device (Morton codes,
+ * radix sort, Karras tree, bottom-up boxes, leaves of <= 4 primitives, then
+ * the 4-wide layout).  Primitive indices reported by pt_intersect stay those
+ * of the uploaded arrays. */
+int pt_upload_scene_lbvh(pt_ctx* ctx, const pt_scene* scene);
 int pt_set_camera(pt_ctx* ctx, const pt_camera* cam);
 int pt_set_params(pt_ctx* ctx, const pt_params* params);
 /* Renders the listed tiles into a host framebuffer of width*height*3 floats;
