@@ -121,6 +121,7 @@ def main():
     ap.add_argument("--scene-dump", default=None, help="PTDUMP scene instead of the native .dae loader")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--lbvh", action="store_true", help="build the BVH on the GPU (pt_upload_scene_lbvh)")
     args = ap.parse_args()
     global W, H, SPP
     wl = WORKLOADS[args.workload]
@@ -152,7 +153,9 @@ def main():
         scene = Scene.from_dae(dae, W, H, envmap=envmap)
         dump_path = None
     dev = Device(local)
-    dev.upload_scene(scene)
+    t_up = time.perf_counter()
+    dev.upload_scene(scene, gpu_bvh=args.lbvh)
+    t_up = time.perf_counter() - t_up
     dev.set_camera(scene.camera)
     dev.set_params(W, H, SPP, DEPTH, NSL, SEED)
     t_load = time.perf_counter() - t_load
@@ -223,7 +226,9 @@ def main():
             "config": {"workload": wl["desc"] + ", default camera",
                        "width": W, "height": H, "spp": SPP, "max_ray_depth": DEPTH, "ns_area_light": NSL,
                        "parallelism": f"tiles{world}" if world > 1 else "single",
-                       "render_time_s": round(elapsed / frames, 4), "scene_load_s": round(t_load, 3)},
+                       "render_time_s": round(elapsed / frames, 4), "scene_load_s": round(t_load, 3),
+                       "bvh": "gpu-lbvh" if args.lbvh else "reference-sah (host)",
+                       "upload_s": round(t_up, 4)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": measured_traffic(args.workload),
                          "kernel": "render_kernel<false>", "kernel_ms": round(avg_ms, 3),

@@ -167,12 +167,13 @@ class SceneArrays:
         nbb = d["node_bb"].reshape(-1, 6)
         ninfo = d["node_info"].reshape(-1, 4)
         nn = nbb.shape[0]
-        self.nodes = (pt_bvh_node * nn)()
-        for i in range(nn):
-            n = self.nodes[i]
-            n.bb_min[:] = nbb[i, :3].tolist()
-            n.bb_max[:] = nbb[i, 3:].tolist()
-            n.start, n.range, n.left, n.right = (int(v) for v in ninfo[i])
+        # pt_bvh_node = 6 doubles + 4 int64 (80 B): one structured array, no per-node Python
+        rec = np.zeros(nn, dtype=np.dtype([("bb", "<f8", 6), ("info", "<i8", 4)]))
+        assert rec.dtype.itemsize == ctypes.sizeof(pt_bvh_node)
+        rec["bb"] = nbb
+        rec["info"] = ninfo
+        self._node_rec = rec
+        self.nodes = ctypes.cast(rec.ctypes.data, POINTER(pt_bvh_node)) if nn else (pt_bvh_node * 1)()
         bt = d["bsdf_type"]
         bp = d["bsdf_params"].reshape(-1, 12)
         self.bsdfs = (pt_bsdf * len(bt))()
