@@ -84,7 +84,18 @@ float round_up(double x) {
 struct EnvTables {
   std::vector<float4> tex;
   std::vector<float> p_theta, p_phi, p_theta_phi;
+  std::vector<int> g_theta, g_phi;  // guide tables (PT_ENV_GUIDE buckets)
 };
+
+// g[k] = lower_bound(a, k/G * a[n-1]), k = 0..G
+static void build_guide(const float* a, int n, int* g) {
+  const float total = a[n - 1];
+  for (int k = 0; k <= PT_ENV_GUIDE; ++k) {
+    const float v = (float)((double)k / PT_ENV_GUIDE) * total;
+    g[k] = (int)(std::lower_bound(a, a + n, v) - a);
+    if (g[k] > n - 1) g[k] = n - 1;
+  }
+}
 #pragma clang fp contract(off)
 void build_env_tables(const float* rgb, int w, int h, EnvTables& t) {
   const double kPi = 3.14159265358979323;  // CMU462 PI
@@ -116,6 +127,10 @@ void build_env_tables(const float* rgb, int w, int h, EnvTables& t) {
     if (y > 0) t.p_theta[y] += t.p_theta[y - 1];
     for (int x = 1; x < w; x++) t.p_phi[(size_t)y * w + x] += t.p_phi[(size_t)y * w + x - 1];
   }
+  t.g_theta.resize(PT_ENV_GUIDE + 1);
+  build_guide(t.p_theta.data(), h, t.g_theta.data());
+  t.g_phi.resize((size_t)h * (PT_ENV_GUIDE + 1));
+  for (int y = 0; y < h; y++) build_guide(&t.p_phi[(size_t)y * w], w, &t.g_phi[(size_t)y * (PT_ENV_GUIDE + 1)]);
 }
 #pragma clang fp contract(on)
 
@@ -130,6 +145,7 @@ struct pt_ctx {
   DevBuf<int> prim_map;   // GPU-built BVH: sorted primitive -> uploaded index (else empty)
   DevBuf<float4> env_tex;          // environment map RGB (w*h, .w unused)
   DevBuf<float> env_ptheta, env_pphi, env_pdf;  // EnvironmentLight tables
+  DevBuf<int> env_gtheta, env_gphi;               // their guide tables
   int env_w = 0, env_h = 0;
   DevBuf<DPrim> prims;
   DevBuf<float> norms;
@@ -204,6 +220,8 @@ int pt_destroy(pt_ctx* c) {
   c->env_ptheta.release();
   c->env_pphi.release();
   c->env_pdf.release();
+  c->env_gtheta.release();
+  c->env_gphi.release();
   c->prims.release();
   c->norms.release();
   c->bsdfs.release();
@@ -593,6 +611,10 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
     HIPCHK(hipMemcpy(c->env_ptheta.p, env.p_theta.data(), env.p_theta.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->env_pphi.p, env.p_phi.data(), env.p_phi.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->env_pdf.p, env.p_theta_phi.data(), env.p_theta_phi.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(c->env_gtheta.reserve(env.g_theta.size()));
+    HIPCHK(c->env_gphi.reserve(env.g_phi.size()));
+    HIPCHK(hipMemcpy(c->env_gtheta.p, env.g_theta.data(), env.g_theta.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->env_gphi.p, env.g_phi.data(), env.g_phi.size() * 4, hipMemcpyHostToDevice));
   }
   c->n_lights = (int)ls.size();
   c->n_bsdfs = (int)bs.size();
@@ -732,6 +754,8 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.env_ptheta = c->env_ptheta.p;
   P.env_pphi = c->env_pphi.p;
   P.env_pdf = c->env_pdf.p;
+  P.env_gtheta = c->env_gtheta.p;
+  P.env_gphi = c->env_gphi.p;
   P.tiles = c->tiles.p;
   P.out = out_dev;
   P.work_counter = c->counter.p;
@@ -860,6 +884,7 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags) {
     c->last.wave_wall_sum = (int64_t)v[14];
     c->last.wave_wall_max = (int64_t)v[15];
     c->last.hitshade_clocks = (int64_t)v[16];
+    for (int k = 0; k < 4; ++k) c->last.section_clocks[k] = (int64_t)v[17 + k];
     c->last.counters_valid = 1;
   }
   return PT_OK;

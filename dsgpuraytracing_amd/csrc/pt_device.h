@@ -26,6 +26,9 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #ifndef PT_LEAF_WEIGHT
 #define PT_LEAF_WEIGHT 16  // leaf steps when leaf lanes >= node lanes * 16 / PT_LEAF_WEIGHT
 #endif
+#ifndef PT_ENV_GUIDE
+#define PT_ENV_GUIDE 64  // buckets of the environment-CDF guide tables
+#endif
 #ifndef PT_STACK
 #define PT_STACK 32  // traversal stack entries per lane in LDS (lane-contiguous)
 #endif
@@ -103,6 +106,8 @@ struct KParams {
   const float* env_ptheta;   // EnvironmentLight::pTheta (running sums over rows)
   const float* env_pphi;     // pPhiGivenTheta (running sums within each row)
   const float* env_pdf;      // pThetaPhi
+  const int* env_gtheta;     // guide table of env_ptheta (PT_ENV_GUIDE + 1 entries)
+  const int* env_gphi;       // guide tables of the rows of env_pphi (h x (PT_ENV_GUIDE + 1))
   const int4* tiles;  // (x, y, w, h)
   float* out;         // W*H*3
   float* partial;     // W*H*n_groups*3: each sample group's sum, resolved into `out` in group order

@@ -418,9 +418,16 @@ __device__ __forceinline__ float3 env_dir(const KParams& P, float3 d) {
   return zy1 * (1.0f - b) + zy2 * b;
 }
 
-// First index of the ascending array a[0..n) with a[i] >= v (std::lower_bound).
-__device__ __forceinline__ int lower_bound_f(const float* __restrict__ a, int n, float v) {
-  int lo = 0;
+// lower_bound of v = r * a[n-1] accelerated by a guide table g[0..G] with
+// g[k] = lower_bound(a, k/G * a[n-1]) (built on the host): the answer lies in
+// [g[k-1], g[k+2]] for k = floor(r*G), one bucket of slack either side for
+// rounding; the result is exactly std::lower_bound's.
+__device__ __forceinline__ int guided_lower_bound(const float* __restrict__ a, float v, float r,
+                                                  const int* __restrict__ g, int G) {
+  const int k = min(G - 1, max(0, (int)(r * (float)G)));
+  int lo = g[max(k - 1, 0)];
+  const int hi = g[min(k + 2, G)];
+  int n = hi - lo;  // candidates [lo, hi); hi itself satisfies a[hi] >= v
   while (n > 0) {
     const int half = n >> 1;
     if (a[lo + half] < v) {
@@ -438,14 +445,16 @@ __device__ __forceinline__ int lower_bound_f(const float* __restrict__ a, int n,
 __device__ __forceinline__ void env_sample(const KParams& P, float r1, float r2, float3& wi, float& pdf) {
   const float kPi = 3.14159265358979323f;
   const int w = P.env_w, h = P.env_h;
+  const float u1 = r1;
   r1 *= P.env_ptheta[h - 1];
-  const int t = lower_bound_f(P.env_ptheta, h, r1);
+  const int t = guided_lower_bound(P.env_ptheta, r1, u1, P.env_gtheta, PT_ENV_GUIDE);
   float prev = t > 0 ? P.env_ptheta[t - 1] : 0.0f;
   const float y = (float)t + (r1 - prev) / (P.env_ptheta[t] - prev);
   const float theta = fminf(y / (float)h, 1.0f) * kPi;
   const float* row = P.env_pphi + (size_t)t * w;
+  const float u2 = r2;
   r2 *= row[w - 1];
-  const int q = lower_bound_f(row, w, r2);
+  const int q = guided_lower_bound(row, r2, u2, P.env_gphi + (size_t)t * (PT_ENV_GUIDE + 1), PT_ENV_GUIDE);
   prev = q > 0 ? row[q - 1] : 0.0f;
   const float x = (float)q + (r2 - prev) / (row[q] - prev);
   const float phi = fminf(x / (float)w, 1.0f) * (2.0f * kPi);
@@ -517,6 +526,13 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   uint32_t chunk_next = 0, chunk_end = 0;  // the wave's private range of work slots
   unsigned long long cyc_shade = 0, cyc_trav = 0;  // shader clocks per phase (lane 0)
   unsigned long long cyc_hitshade = 0;              // of which: shading before the refill
+  unsigned long long cyc_sec[4] = {0, 0, 0, 0};     // of which: hit record, NEE, bounce, refill fetch
+#define PT_STAMP(k)                                 \
+  if (STATS) {                                      \
+    unsigned long long t_ = clock64();              \
+    cyc_sec[k] += lane == 0 ? t_ - t_mark : 0ull;   \
+    t_mark = t_;                                    \
+  }
   unsigned long long t_mark = STATS ? clock64() : 0ull;
   const unsigned long long w_start = STATS ? wall_clock64() : 0ull;
 
@@ -574,6 +590,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         ls = 0;
         stage = 0;
       }
+      PT_STAMP(0);
       if (stage < 2) {
         const DBsdf B = bsdfs[bsdf];
         const Frame fr = make_frame(ns);
@@ -641,6 +658,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           if (STATS) n_shadow++;
           break;
         }
+        PT_STAMP(1);
         if (emitted) {
           shadow = true;
           mode = M_TRAV;
@@ -713,6 +731,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           }
         }
       }
+      PT_STAMP(2);
       if (finish) {
         acc = acc + L;
         ++sample;
@@ -783,6 +802,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           chunk_next += cnt;
         }
       }
+      PT_STAMP(3);
       // ---- camera rays: Camera::generate_ray (camera.cpp:113-129) at the
       // jittered pixel position of raytrace_pixel (pathtracer.cpp:571-575)
       while (mode == M_CAMERA) {
@@ -870,6 +890,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       unsigned long long w = wall_clock64() - w_start;
       atomicMax(P.stats + 13, cyc_shade + cyc_hitshade + cyc_trav);
       atomicAdd(P.stats + 16, cyc_hitshade);
+      for (int k = 0; k < 4; ++k) atomicAdd(P.stats + 17 + k, cyc_sec[k]);
       atomicAdd(P.stats + 14, w);
       atomicMax(P.stats + 15, w);
     }

@@ -116,7 +116,9 @@ class Device:
     def stats(self) -> dict:
         s = native.pt_stats()
         check(self._lib.pt_get_stats(self.handle, ctypes.byref(s)))
-        return {k: getattr(s, k) for k, _ in native.pt_stats._fields_}
+        out = {k: getattr(s, k) for k, _ in native.pt_stats._fields_}
+        out["section_clocks"] = list(s.section_clocks)
+        return out
 
 
 class Scene:

@@ -180,9 +180,11 @@ typedef struct pt_stats {
   int64_t wave_wall_max;   /* longest wave lifetime, device wall-clock ticks */
   int64_t leaf_steps;      /* of wave_trav_steps: leaf (primitive) steps */
   int64_t hitshade_clocks; /* of shade_clocks: hit records, NEE and bounces (the rest is refill) */
-  double resolve_ms;
+  double resolve_ms;       /* device time of the sample-group resolve kernel */
   int32_t bvh_stack;       /* worst-case traversal stack entries of the uploaded BVH */
-  int64_t bvh_nodes;       /* 4-wide BVH nodes uploaded */       /* device time of the sample-group resolve kernel */
+  int64_t bvh_nodes;       /* 4-wide BVH nodes uploaded */
+  int64_t section_clocks[4]; /* of shade_clocks: hit record, light sampling, BSDF sampling, queue fetch
+                                (the rest: camera rays) */
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */
