@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "pt_device.h"
 #include "pt_rng.h"
 
@@ -221,16 +223,30 @@ __device__ __forceinline__ bool prim_test(const float4 v0, const float4 e1, cons
 // Per-lane traversal stack: the first PT_STACK entries in LDS (lane-
 // contiguous, conflict-free), deeper ones in a global per-lane spill area that
 // only BVHs with a worst-case depth beyond PT_STACK get (rarely touched).
+// LDS pointers typed as such: a plain int* into __shared__ memory makes the
+// compiler merge the LDS / spill paths into FLAT accesses, which occupy the
+// vector-memory (TA/TD) path the node and primitive fetches need.
+typedef __attribute__((address_space(3))) int lds_int;
+
 struct Stack {
-  int* lds;       // s_stack + lane, stride PT_BLOCK
+  lds_int* lds;   // s_stack + lane, stride PT_BLOCK
   int* spill;     // P.stack_spill + global lane id, stride sstride (may be null)
   uint32_t sstride;
   __device__ __forceinline__ void put(int i, int v) const {
-    if (i < PT_STACK) lds[i * PT_BLOCK] = v;
-    else spill[(size_t)(i - PT_STACK) * sstride] = v;
+    if (i < PT_STACK) {
+      lds[i * PT_BLOCK] = v;
+    } else {
+      spill[(size_t)(i - PT_STACK) * sstride] = v;
+    }
   }
   __device__ __forceinline__ int get(int i) const {
-    return i < PT_STACK ? lds[i * PT_BLOCK] : spill[(size_t)(i - PT_STACK) * sstride];
+    int v;
+    if (i < PT_STACK) {
+      v = lds[i * PT_BLOCK];
+    } else {
+      v = spill[(size_t)(i - PT_STACK) * sstride];
+    }
+    return v;
   }
 };
 
@@ -475,29 +491,51 @@ enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 // BIN: the reference-count variant, traversing the binary tree (P.nodes2).
 // ENV: the scene has an environment light (kept out of the common build: its
 // lookups and sampling cost registers).
-template <bool STATS, bool DBG, bool BIN, bool ENV>
+// GTAB: material/light tables larger than the LDS copies (read from global
+// memory; the common build reads them from LDS through address-space-typed
+// pointers, never through FLAT accesses).
+template <bool STATS, bool DBG, bool BIN, bool ENV, bool GTAB>
 __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel(KParams P) {
   __shared__ int s_stack[PT_STACK * PT_BLOCK];
   const int lane = threadIdx.x & 63;
   const uint32_t gid = blockIdx.x * PT_BLOCK + threadIdx.x;
-  const Stack stk{s_stack + threadIdx.x, P.stack_spill ? P.stack_spill + gid : nullptr, gridDim.x * PT_BLOCK};
+  const Stack stk{(lds_int*)(s_stack + threadIdx.x), P.stack_spill ? P.stack_spill + gid : nullptr,
+                  gridDim.x * PT_BLOCK};
 
   // Material and light tables are read by every shading step: keep small
   // ones in LDS (the usual case); larger ones stay in global memory.
-  __shared__ DBsdf s_bsdf[PT_LDS_BSDFS];
-  __shared__ DLight s_light[PT_LDS_LIGHTS];
-  const DBsdf* bsdfs = P.bsdfs;
-  const DLight* lights = P.lights;
-  if (P.n_bsdfs <= PT_LDS_BSDFS) {
-    const int n = P.n_bsdfs * (int)(sizeof(DBsdf) / 4);
-    for (int k = lane; k < n; k += PT_BLOCK) ((float*)s_bsdf)[k] = ((const float*)P.bsdfs)[k];
-    bsdfs = s_bsdf;
+  __shared__ DBsdf s_bsdf[GTAB ? 1 : PT_LDS_BSDFS];
+  __shared__ DLight s_light[GTAB ? 1 : PT_LDS_LIGHTS];
+  typedef __attribute__((address_space(3))) const float lds_f;
+  if (!GTAB) {
+    const int nb = P.n_bsdfs * (int)(sizeof(DBsdf) / 4);
+    for (int k = lane; k < nb; k += PT_BLOCK) ((float*)s_bsdf)[k] = ((const float*)P.bsdfs)[k];
+    const int nl = P.n_lights * (int)(sizeof(DLight) / 4);
+    for (int k = lane; k < nl; k += PT_BLOCK) ((float*)s_light)[k] = ((const float*)P.lights)[k];
   }
-  if (P.n_lights <= PT_LDS_LIGHTS) {
-    const int n = P.n_lights * (int)(sizeof(DLight) / 4);
-    for (int k = lane; k < n; k += PT_BLOCK) ((float*)s_light)[k] = ((const float*)P.lights)[k];
-    lights = s_light;
-  }
+  // table entries read with address-space-typed (ds_read) loads
+  auto bsdf_at = [&](int i) -> DBsdf {
+    if constexpr (GTAB) {
+      return P.bsdfs[i];
+    } else {
+      DBsdf b;
+      lds_f* src = (lds_f*)s_bsdf + i * (int)(sizeof(DBsdf) / 4);
+#pragma unroll
+      for (int k = 0; k < (int)(sizeof(DBsdf) / 4); ++k) ((float*)&b)[k] = src[k];
+      return b;
+    }
+  };
+  auto light_at = [&](int i) -> DLight {
+    if constexpr (GTAB) {
+      return P.lights[i];
+    } else {
+      DLight l;
+      lds_f* src = (lds_f*)s_light + i * (int)(sizeof(DLight) / 4);
+#pragma unroll
+      for (int k = 0; k < (int)(sizeof(DLight) / 4); ++k) ((float*)&l)[k] = src[k];
+      return l;
+    }
+  };
   __syncthreads();
 
   // ---- per-lane state
@@ -584,7 +622,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if ((meta & 1) && dot(tr.d, ns) > 0.0f) ns = f3(0, 0, 0) - ns;
         ng = normalize(ng);
         wo = normalize(make_frame(ns).to_local(f3(0, 0, 0) - tr.d));
-        if (includeLe) L = L + mul(T, ld3(bsdfs[bsdf].e));
+        if (includeLe) L = L + mul(T, ld3(bsdf_at(bsdf).e));
         if (DBG && pix == P.dbg_pix) printf("  depth %d hit prim %d bsdf %d t=%.9g n=(%.6g %.6g %.6g) T=(%.5g)\n", depth, h.prim, bsdf, h.t, ns.x, ns.y, ns.z, T.x);
         li = 0;
         ls = 0;
@@ -592,12 +630,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       }
       PT_STAMP(0);
       if (stage < 2) {
-        const DBsdf B = bsdfs[bsdf];
+        const DBsdf B = bsdf_at(bsdf);
         const Frame fr = make_frame(ns);
         bool emitted = false;
         // ---- next-event estimation over all lights (pathtracer.cpp:469-523)
         while (li < P.n_lights) {
-          const DLight Lt = lights[li];
+          const DLight Lt = light_at(li);
           const bool delta = Lt.type == 0 || Lt.type == 2;
           const int nls = delta ? 1 : P.ns_area;
           if (ls >= nls) {
@@ -922,7 +960,7 @@ __global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __rest
                                                            int32_t* anyhit, int* spill, const int* prim_map) {
   __shared__ int s_stack[PT_STACK * PT_BLOCK];
   int64_t i = (int64_t)blockIdx.x * PT_BLOCK + threadIdx.x;
-  const Stack stk{s_stack + threadIdx.x, spill ? spill + i : nullptr, gridDim.x * PT_BLOCK};
+  const Stack stk{(lds_int*)(s_stack + threadIdx.x), spill ? spill + i : nullptr, gridDim.x * PT_BLOCK};
   if (i >= n) return;
   float3 O = f3(o[3 * i], o[3 * i + 1], o[3 * i + 2]);
   float3 D = f3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
@@ -943,23 +981,28 @@ __global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __rest
 }  // namespace ptk
 
 // ------------------------------------------------------------------ launchers
-template <bool ENV>
+template <bool ENV, bool GTAB>
 static void launch_render(const KParams* P, int grid, bool stats, bool ref_counts, hipStream_t s) {
   if (ref_counts)
-    hipLaunchKernelGGL((ptk::render_kernel<true, false, true, ENV>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+    hipLaunchKernelGGL((ptk::render_kernel<true, false, true, ENV, GTAB>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
   else if (P->dbg_pix >= 0)
-    hipLaunchKernelGGL((ptk::render_kernel<false, true, false, ENV>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+    hipLaunchKernelGGL((ptk::render_kernel<false, true, false, ENV, GTAB>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
   else if (stats)
-    hipLaunchKernelGGL((ptk::render_kernel<true, false, false, ENV>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+    hipLaunchKernelGGL((ptk::render_kernel<true, false, false, ENV, GTAB>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
   else
-    hipLaunchKernelGGL((ptk::render_kernel<false, false, false, ENV>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+    hipLaunchKernelGGL((ptk::render_kernel<false, false, false, ENV, GTAB>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
 }
 
 extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, bool ref_counts, hipStream_t s) {
-  if (P->env_w > 0)
-    launch_render<true>(P, grid, stats, ref_counts, s);
-  else
-    launch_render<false>(P, grid, stats, ref_counts, s);
+  static const bool force_gtab = std::getenv("PT_FORCE_GLOBAL_TABLES") != nullptr;  // tests
+  const bool gtab = force_gtab || P->n_bsdfs > PT_LDS_BSDFS || P->n_lights > PT_LDS_LIGHTS;
+  if (P->env_w > 0) {
+    if (gtab) launch_render<true, true>(P, grid, stats, ref_counts, s);
+    else launch_render<true, false>(P, grid, stats, ref_counts, s);
+  } else {
+    if (gtab) launch_render<false, true>(P, grid, stats, ref_counts, s);
+    else launch_render<false, false>(P, grid, stats, ref_counts, s);
+  }
   return hipGetLastError();
 }
 
@@ -981,8 +1024,8 @@ extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prim
 
 extern "C" hipError_t ptk_render_occupancy(int* blocks_per_cu, bool stats) {
   if (stats)
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ptk::render_kernel<true, false, false, false>,
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ptk::render_kernel<true, false, false, false, false>,
                                                         PT_BLOCK, 0);
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ptk::render_kernel<false, false, false, false>,
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ptk::render_kernel<false, false, false, false, false>,
                                                       PT_BLOCK, 0);
 }

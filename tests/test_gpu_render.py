@@ -148,6 +148,22 @@ def test_screen_footprint_culling_is_exact(monkeypatch, scene, w, h):
         assert st["culled_samples"] > 0
 
 
+@pytest.mark.parametrize("scene", ["CBspheres_64x64", "c1env_64x64"])
+def test_global_table_variant_is_identical(monkeypatch, scene):
+    """Scenes with more BSDFs/lights than the LDS copies hold use the kernel
+    variant that reads the tables from global memory: same arithmetic, same image."""
+    a, _ = gpu_render(scene, 64, 64, 4, seed=13)
+    monkeypatch.setenv("PT_FORCE_GLOBAL_TABLES", "1")
+    import subprocess, sys, json, os
+    code = ("import numpy as np, sys; sys.path.insert(0, %r); from tests.test_gpu_render import gpu_render; "
+            "a, _ = gpu_render(%r, 64, 64, 4, seed=13); np.save(%r, a)")
+    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"gtab_{scene}.npy")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run([sys.executable, "-c", code % (root, scene, out)], check=True, env=dict(os.environ), cwd=root)
+    b = np.load(out)
+    assert np.array_equal(a, b)
+
+
 def test_hip_ray_queries_vs_reference_kat():
     rays = ptdump.read(golden("c1_rays.ptd"))
     ref = ptdump.read(golden("c1_rays_ref.ptd"))
