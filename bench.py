@@ -90,27 +90,39 @@ def measured_pmc(workload: str):
 def cpu_baseline(scene_dump: str, budget_s: float = 12.0) -> dict:
     """Reference CPU algorithm (oracle/restate.cpp, bit-identical to the
     reference binary at -t 1: glibc rand, one thread) timed on this host on a
-    bounded sample of the same workload: every k-th tile of the 1024x1024 FIFO
-    at the full 64 spp."""
+    bounded, UNIFORM sample of the same workload: every k-th tile of the 32x32
+    tile FIFO at the full spp, k sized from a 16-tile calibration so the sample
+    takes about budget_s (scene load excluded)."""
     from tests.oracle_helpers import Restatement
     rs = Restatement()
     ntx = (W + 31) // 32
     ntiles = ntx * ((H + 31) // 32)
-    # calibrate on one tile, then size the sample to ~budget_s
-    t0 = time.perf_counter()
-    rs.render(scene_dump, W, H, SPP, DEPTH, NSL, SEED, rng_mode=0, tile_begin=ntiles // 2, tile_end=ntiles // 2 + 1)
-    one = max(time.perf_counter() - t0, 1e-3)
-    step = max(1, int(ntiles * one / budget_s))
-    total_t, total_px = 0.0, 0
-    for ti in range(0, ntiles, step):
-        t0 = time.perf_counter()
-        rs.render(scene_dump, W, H, SPP, DEPTH, NSL, SEED, rng_mode=0, tile_begin=ti, tile_end=ti + 1)
-        total_t += time.perf_counter() - t0
-        tx, ty = (ti % ntx) * 32, (ti // ntx) * 32
-        total_px += (min(W, tx + 32) - tx) * (min(H, ty + 32) - ty)
-    return {"value": total_px * SPP / total_t / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": f"every {step}th 32x32 tile of the {W}x{H} frame ({total_px} px) at {SPP} spp, -m 4 -l 1, "
-                      f"oracle/restate.cpp glibc-rand mode (== reference -t 1), {total_t:.1f} s"}
+
+    def tiles_px(begin, stride):
+        px = 0
+        for ti in range(begin, ntiles, stride):
+            tx, ty = (ti % ntx) * 32, (ti // ntx) * 32
+            px += (min(W, tx + 32) - tx) * (min(H, ty + 32) - ty)
+        return px
+
+    import math
+
+    def coprime(k):  # strides sharing a factor with the row length sample columns, not the frame
+        while k > 1 and math.gcd(k, ntx) != 1:
+            k += 1
+        return k
+
+    cal = coprime(max(1, ntiles // 16))
+    _, _, t_cal = rs.render_strided(scene_dump, W, H, SPP, DEPTH, NSL, SEED, rng_mode=0, tile_begin=cal // 2,
+                                    tile_stride=cal)
+    per_tile = max(t_cal, 1e-4) / len(range(cal // 2, ntiles, cal))
+    step = coprime(max(1, int(round(ntiles * per_tile / budget_s))))
+    _, _, secs = rs.render_strided(scene_dump, W, H, SPP, DEPTH, NSL, SEED, rng_mode=0, tile_begin=step // 2,
+                                   tile_stride=step)
+    px = tiles_px(step // 2, step)
+    return {"value": px * SPP / secs / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
+            "sample": f"every {step}th 32x32 tile of the {W}x{H} frame ({px} px, uniform) at {SPP} spp, -m {DEPTH} "
+                      f"-l {NSL}, oracle/restate.cpp glibc-rand mode (== reference -t 1), {secs:.1f} s of rendering"}
 
 
 def main():

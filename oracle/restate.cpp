@@ -29,6 +29,7 @@
 // (g++ -O3, no -march, no -ffast-math): see oracle/Makefile.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -738,11 +739,27 @@ extern "C" {
 // rng_mode 0: glibc rand() after srand(seed), single thread, reference order.
 // rng_mode 1: counter stream, `threads` workers over tiles.
 // stats_out (nullable): rays, shadow rays, node visits, tri tests, sphere tests.
+// rs_render_strided: tiles tile_begin, tile_begin + stride, ... < tile_end
+// (a uniform sample of the frame for the bench's CPU baseline); render_s
+// (nullable) receives the wall time of the render alone (scene load excluded).
+int rs_render_strided(const char* scene_path, int w, int h, int spp, int max_depth, int ns_area_light,
+                      uint32_t seed, int rng_mode, int threads, int tile_begin, int tile_end, int tile_stride,
+                      float* hdr_out, int64_t* stats_out, double* render_s);
+
 int rs_render(const char* scene_path, int w, int h, int spp, int max_depth, int ns_area_light,
               uint32_t seed, int rng_mode, int threads, int tile_begin, int tile_end, float* hdr_out,
               int64_t* stats_out) {
+  return rs_render_strided(scene_path, w, h, spp, max_depth, ns_area_light, seed, rng_mode, threads, tile_begin,
+                           tile_end, 1, hdr_out, stats_out, nullptr);
+}
+
+int rs_render_strided(const char* scene_path, int w, int h, int spp, int max_depth, int ns_area_light,
+                      uint32_t seed, int rng_mode, int threads, int tile_begin, int tile_end, int tile_stride,
+                      float* hdr_out, int64_t* stats_out, double* render_s) {
   rs::Scene S;
   if (!rs::load_scene(scene_path, S)) return -1;
+  if (tile_stride < 1) tile_stride = 1;
+  const auto t_start = std::chrono::steady_clock::now();
   const int T = 32;
   std::vector<std::pair<int, int>> tiles;
   for (int y = 0; y < h; y += T)
@@ -759,7 +776,7 @@ int rs_render(const char* scene_path, int w, int h, int spp, int max_depth, int 
     rs::Rng rng;
     rng.mode = rng_mode;
     for (;;) {
-      int ti = next.fetch_add(1);
+      int ti = next.fetch_add(tile_stride);
       if (ti >= tile_end) break;
       int x0 = tiles[ti].first, y0 = tiles[ti].second;
       int x1 = std::min(x0 + T, w), y1 = std::min(y0 + T, h);
@@ -797,6 +814,7 @@ int rs_render(const char* scene_path, int w, int h, int spp, int max_depth, int 
     for (int i = 0; i < nt; ++i) th.emplace_back(worker, i);
     for (auto& t : th) t.join();
   }
+  if (render_s) *render_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
   if (stats_out) {
     int64_t a[5] = {0, 0, 0, 0, 0};
     for (auto& s : stats) {

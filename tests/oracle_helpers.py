@@ -31,6 +31,9 @@ class Restatement:
         self.lib.rs_render.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 5 + [ctypes.c_uint32] + \
             [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_void_p]
         self.lib.rs_render.restype = ctypes.c_int
+        self.lib.rs_render_strided.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 5 + [ctypes.c_uint32] + \
+            [ctypes.c_int] * 5 + [ctypes.c_void_p] * 3
+        self.lib.rs_render_strided.restype = ctypes.c_int
         self.lib.rs_intersect.argtypes = [ctypes.c_char_p, ctypes.c_int64] + [ctypes.c_void_p] * 8
         self.lib.rs_intersect.restype = ctypes.c_int
         self.lib.rs_rng_draw.argtypes = [ctypes.c_uint32] * 4
@@ -45,6 +48,19 @@ class Restatement:
         if rc != 0:
             raise RuntimeError(f"rs_render failed on {scene_path}")
         return out, st
+
+    def render_strided(self, scene_path, w, h, spp, depth=4, ns_area_light=1, seed=1, rng_mode=0, threads=1,
+                       tile_begin=0, tile_end=-1, tile_stride=1):
+        """Tiles tile_begin, +stride, ... < tile_end; returns (hdr, stats, render seconds)."""
+        out = np.zeros((h, w, 3), np.float32)
+        st = np.zeros(5, np.int64)
+        secs = ctypes.c_double(0.0)
+        rc = self.lib.rs_render_strided(scene_path.encode(), w, h, spp, depth, ns_area_light, seed, rng_mode,
+                                        threads, tile_begin, tile_end, tile_stride, out.ctypes.data,
+                                        st.ctypes.data, ctypes.byref(secs))
+        if rc != 0:
+            raise RuntimeError(f"rs_render_strided failed on {scene_path}")
+        return out, st, secs.value
 
     def intersect(self, scene_path, o, d, maxt):
         n = len(maxt)
