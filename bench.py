@@ -210,6 +210,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    host_ms = None
+    if world == 1:  # the drop-in pt_render_tiles path: output copied to a host buffer (PCIe-inclusive)
+        host = np.zeros((H, W, 3), np.float32)
+        dev.render_tiles(mine_arr, host)
+        t0h = time.perf_counter()
+        for _ in range(2):
+            dev.render_tiles(mine_arr, host)
+        host_ms = (time.perf_counter() - t0h) / 2 * 1e3
     if rank == 0:
         frames = args.steps
         value = W * H * SPP * frames / elapsed / 1e6
@@ -240,7 +248,8 @@ def main():
                        "parallelism": f"tiles{world}" if world > 1 else "single",
                        "render_time_s": round(elapsed / frames, 4), "scene_load_s": round(t_load, 3),
                        "bvh": "gpu-lbvh" if args.lbvh else "reference-sah (host)",
-                       "upload_s": round(t_up, 4)},
+                       "upload_s": round(t_up, 4),
+                       "host_output_ms_per_frame": None if host_ms is None else round(host_ms, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": measured_traffic(args.workload),
                          "kernel": "render_kernel<false>", "kernel_ms": round(avg_ms, 3),

@@ -813,6 +813,9 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     if (w > 0) want = (int64_t)w * c->n_cu;
   }
   P.group_spp = PT_GROUP_SPP;
+  // Small launches (a GPU's share of a sharded frame, single tiles) get
+  // one-sample groups: at least ~16 work slots per lane keep the tail short.
+  if ((int64_t)bl.size() * 64 * ((P.spp + P.group_spp - 1) / P.group_spp) < want * PT_BLOCK * 16) P.group_spp = 1;
   if (const char* g = std::getenv("PT_SAMPLE_GROUP")) {  // tuning knob
     int v = std::atoi(g);
     if (v > 0) P.group_spp = v;
@@ -897,6 +900,19 @@ static int check_ready(pt_ctx* c) {
   return PT_OK;
 }
 
+// True when no pixel belongs to two of the (clipped) tiles.
+static bool tiles_disjoint(const std::vector<int4>& tl, size_t W, size_t H) {
+  std::vector<uint8_t> seen(W * H, 0);
+  for (const int4& t : tl)
+    for (int y = t.y; y < t.y + t.w; ++y)
+      for (int x = t.x; x < t.x + t.z; ++x) {
+        uint8_t& v = seen[(size_t)y * W + (size_t)x];
+        if (v) return false;
+        v = 1;
+      }
+  return true;
+}
+
 int pt_render_tiles(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, float* hdr_out_host, uint32_t flags) {
   int rc = check_ready(c);
   if (rc) return rc;
@@ -907,10 +923,19 @@ int pt_render_tiles(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, float* hdr
   const size_t W = (size_t)c->params.width, H = (size_t)c->params.height;
   HIPCHK(c->frame.reserve(W * H * 3));
   if ((rc = launch(c, tl, c->frame.p, c->stream, flags))) return rc;
-  for (const int4& t : tl) {
-    size_t off = ((size_t)t.y * W + (size_t)t.x) * 3;
-    HIPCHK(hipMemcpy2DAsync(hdr_out_host + off, W * 3 * sizeof(float), c->frame.p + off, W * 3 * sizeof(float),
-                            (size_t)t.z * 3 * sizeof(float), (size_t)t.w, hipMemcpyDeviceToHost, c->stream));
+  // Copy back only the tiles' pixels (the caller's buffer is theirs outside
+  // them); a call whose (clipped, disjoint) tiles cover the whole frame - the
+  // whole-frame batch - is one contiguous copy.
+  int64_t area = 0;
+  for (const int4& t : tl) area += (int64_t)t.z * t.w;
+  if (area == (int64_t)(W * H) && tiles_disjoint(tl, W, H)) {
+    HIPCHK(hipMemcpyAsync(hdr_out_host, c->frame.p, W * H * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  } else {
+    for (const int4& t : tl) {
+      size_t off = ((size_t)t.y * W + (size_t)t.x) * 3;
+      HIPCHK(hipMemcpy2DAsync(hdr_out_host + off, W * 3 * sizeof(float), c->frame.p + off, W * 3 * sizeof(float),
+                              (size_t)t.z * 3 * sizeof(float), (size_t)t.w, hipMemcpyDeviceToHost, c->stream));
+    }
   }
   return finish_stats(c, c->stream, flags);
 }
