@@ -134,6 +134,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--lbvh", action="store_true", help="build the BVH on the GPU (pt_upload_scene_lbvh)")
+    ap.add_argument("--emulate-shard", type=int, default=0,
+                    help="diagnostic: render only rank 0's share of an N-GPU split on this one GPU")
     args = ap.parse_args()
     global W, H, SPP
     wl = WORKLOADS[args.workload]
@@ -177,6 +179,8 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
 
     mine_arr = np.asarray(shard_tiles(tiles, rank, world), dtype=np.int32).reshape(-1, 4)
+    if args.emulate_shard > 1:
+        mine_arr = np.asarray(shard_tiles(tiles, 0, args.emulate_shard), dtype=np.int32).reshape(-1, 4)
 
     def step(stats=False):  # render_sharded deals the same tiles to this rank every step
         render_sharded(lambda mine: dev.render_tiles_device(mine_arr, frame.data_ptr(), stream, stats=stats),
@@ -221,6 +225,8 @@ def main():
     if rank == 0:
         frames = args.steps
         value = W * H * SPP * frames / elapsed / 1e6
+        if args.emulate_shard > 1:
+            value = float(np.sum(mine_arr[:, 2] * mine_arr[:, 3])) * SPP * frames / elapsed / 1e6
         bytes_launch = algorithmic_bytes(st_counts)
         avg_ms = float(np.mean(kernel_ms))
         achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
@@ -261,7 +267,7 @@ def main():
             "launch_counters": {k: st_perf[k] for k in ("node_visits", "tri_tests", "sphere_tests", "wave_trav_steps",
                                                         "leaf_steps", "wave_rounds", "queue_atomics", "shade_clocks",
                                                         "hitshade_clocks", "trav_clocks", "max_wave_clocks",
-                                                        "wave_wall_sum", "wave_wall_max", "section_clocks")},
+                                                        "wave_wall_sum", "wave_wall_max", "section_clocks", "wave_span")},
             "launch": {"grid_blocks": s["grid_blocks"], "block": 64, "blocks_per_cu_query": s["blocks_per_cu"],
                        "bvh_nodes": s["bvh_nodes"], "bvh_stack": s["bvh_stack"]},
             "image_mean": float(img.mean()),

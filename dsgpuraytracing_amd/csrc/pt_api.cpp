@@ -720,7 +720,11 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     c->tiles_host = tl;
   }
   HIPCHK(hipMemsetAsync(c->counter.p, 0, sizeof(uint32_t), s));
-  if (stats) HIPCHK(hipMemsetAsync(c->stats.p, 0, 32 * sizeof(unsigned long long), s));
+  if (stats) {
+    unsigned long long init[32] = {0};
+    init[21] = init[23] = ~0ull;  // atomicMin slots
+    HIPCHK(hipMemcpyAsync(c->stats.p, init, sizeof(init), hipMemcpyHostToDevice, s));
+  }
   KParams P;
   std::memset(&P, 0, sizeof(P));
   for (int k = 0; k < 3; ++k) {
@@ -827,12 +831,12 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   for (;;) {
     P.n_groups = (P.spp + P.group_spp - 1) / P.group_spp;
     int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
-    bool fits = slots + want * PT_CHUNK < (int64_t)UINT32_MAX && npx * P.n_groups * 12 <= (4ll << 30);
+    bool fits = slots + want * PT_CHUNK_MAX < (int64_t)UINT32_MAX && npx * P.n_groups * 12 <= (4ll << 30);
     if (fits || P.n_groups == 1) break;
     P.group_spp *= 2;
   }
   int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
-  if (slots + want * PT_CHUNK >= (int64_t)UINT32_MAX || npx * P.n_groups >= (int64_t)UINT32_MAX)
+  if (slots + want * PT_CHUNK_MAX >= (int64_t)UINT32_MAX || npx * P.n_groups >= (int64_t)UINT32_MAX)
     return fail(PT_E_INVALID, "frame too large for one launch");
   HIPCHK(c->partial.reserve((size_t)(npx * P.n_groups) * 3));
   P.partial = c->partial.p;
@@ -888,6 +892,7 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags) {
     c->last.wave_wall_max = (int64_t)v[15];
     c->last.hitshade_clocks = (int64_t)v[16];
     for (int k = 0; k < 4; ++k) c->last.section_clocks[k] = (int64_t)v[17 + k];
+    for (int k = 0; k < 3; ++k) c->last.wave_span[k] = (int64_t)(v[22 + k] - v[21]);
     c->last.counters_valid = 1;
   }
   return PT_OK;

@@ -8,7 +8,13 @@
 #define PT_BLOCK 64  // one wave64 per workgroup: the persistent queue is per wave
 #endif
 #ifndef PT_CHUNK
-#define PT_CHUNK 64  // work slots (pixels) a wave takes from the queue per atomic
+#define PT_CHUNK 128  // smallest claim of work slots a wave takes from the queue per atomic
+#endif
+#ifndef PT_CHUNK_MAX
+#define PT_CHUNK_MAX 128  // largest claim (guided self-scheduling, see the refill in pt_kernels.hip)
+#endif
+#ifndef PT_CHUNK_DIV
+#define PT_CHUNK_DIV 8u  // a claim is ~1/(PT_CHUNK_DIV * waves) of the slots still unclaimed
 #endif
 static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand");
 #ifndef PT_GROUP_SPP

@@ -562,6 +562,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   uint32_t n_leafit = 0;               // of the traversal steps: leaf steps
   uint32_t n_atomics = 0;              // work-queue atomics (lane 0)
   uint32_t chunk_next = 0, chunk_end = 0;  // the wave's private range of work slots
+  uint32_t seen = 0;                       // queue head after this wave's last claim
   unsigned long long cyc_shade = 0, cyc_trav = 0;  // shader clocks per phase (lane 0)
   unsigned long long cyc_hitshade = 0;              // of which: shading before the refill
   unsigned long long cyc_sec[4] = {0, 0, 0, 0};     // of which: hit record, NEE, bounce, refill fetch
@@ -796,14 +797,20 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       unsigned long long m = __ballot(need);
       if (m != 0ull) {
         // Lanes are served from the wave's private chunk of consecutive slots;
-        // one atomic refills it with PT_CHUNK slots (keeps the queue head off
-        // the critical path: ~1 atomic per PT_CHUNK pixels).
+        // one atomic refills it.  Guided self-scheduling: a chunk is about
+        // 1/(PT_CHUNK_DIV * waves) of the slots still unclaimed (as last seen), between
+        // PT_CHUNK and PT_CHUNK_MAX, so early chunks are large (few atomics on
+        // the one queue head, which sits memory-side since the XCD L2s are
+        // not coherent) and the tail is handed out 64 slots at a time.
         uint32_t cnt = (uint32_t)__popcll(m);
         uint32_t avail = chunk_end - chunk_next;
-        uint32_t nbase = 0;
+        uint32_t nbase = 0, csize = 0;
         if (cnt > avail) {
-          if (lane == 0) nbase = atomicAdd(P.work_counter, (uint32_t)PT_CHUNK);
+          const uint32_t left = seen < total_slots ? total_slots - seen : 0u;
+          csize = min((uint32_t)PT_CHUNK_MAX, max((uint32_t)PT_CHUNK, left / (PT_CHUNK_DIV * gridDim.x))) & ~63u;
+          if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
           nbase = __shfl(nbase, 0);
+          seen = nbase + csize;
           if (STATS) n_atomics += lane == 0;
         }
         if (need) {
@@ -835,7 +842,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         }
         if (cnt > avail) {  // wave-uniform
           chunk_next = nbase + (cnt - avail);
-          chunk_end = nbase + PT_CHUNK;
+          chunk_end = nbase + csize;
         } else {
           chunk_next += cnt;
         }
@@ -928,6 +935,11 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       unsigned long long w = wall_clock64() - w_start;
       atomicMax(P.stats + 13, cyc_shade + cyc_hitshade + cyc_trav);
       atomicAdd(P.stats + 16, cyc_hitshade);
+      const unsigned long long w_end = wall_clock64();  // launch shape: first/last wave start and end
+      atomicMin(P.stats + 21, w_start);
+      atomicMax(P.stats + 22, w_start);
+      atomicMin(P.stats + 23, w_end);
+      atomicMax(P.stats + 24, w_end);
       for (int k = 0; k < 4; ++k) atomicAdd(P.stats + 17 + k, cyc_sec[k]);
       atomicAdd(P.stats + 14, w);
       atomicMax(P.stats + 15, w);

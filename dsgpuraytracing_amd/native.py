@@ -89,7 +89,8 @@ class pt_stats(ctypes.Structure):
                 ("shade_clocks", c_int64), ("trav_clocks", c_int64),
                 ("max_wave_clocks", c_int64), ("wave_wall_sum", c_int64), ("wave_wall_max", c_int64),
                 ("leaf_steps", c_int64), ("hitshade_clocks", c_int64), ("resolve_ms", c_double),
-                ("bvh_stack", c_int32), ("bvh_nodes", c_int64), ("section_clocks", c_int64 * 4)]
+                ("bvh_stack", c_int32), ("bvh_nodes", c_int64), ("section_clocks", c_int64 * 4),
+                ("wave_span", c_int64 * 3)]
 
 
 # Every symbol include/ptgpu.h and include/ptgpu_scene.h declare, with ctypes signatures.

@@ -118,6 +118,7 @@ class Device:
         check(self._lib.pt_get_stats(self.handle, ctypes.byref(s)))
         out = {k: getattr(s, k) for k, _ in native.pt_stats._fields_}
         out["section_clocks"] = list(s.section_clocks)
+        out["wave_span"] = list(s.wave_span)
         return out
 
 

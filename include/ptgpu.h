@@ -185,6 +185,8 @@ typedef struct pt_stats {
   int64_t bvh_nodes;       /* 4-wide BVH nodes uploaded */
   int64_t section_clocks[4]; /* of shade_clocks: hit record, light sampling, BSDF sampling, queue fetch
                                 (the rest: camera rays) */
+  int64_t wave_span[3];    /* wall-clock ticks after the first wave started: last wave start,
+                              first wave end, last wave end (launch ramp and tail) */
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */
