@@ -886,6 +886,11 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     // lanes have finished their ray, so finished lanes are refilled together
     // (coherent shading) while the others keep their traversal state.
     if (__ballot(mode == M_TRAV) == 0ull) break;  // every lane is M_DONE
+    // Once the queue is drained, lanes retire (M_DONE): shade when 3/4 of the
+    // lanes still working are ready, not when `batch` of 64 are, or the tail
+    // would wait for the slowest ray of the wave at every bounce.
+    const int alive = __popcll(__ballot(mode != M_DONE));
+    const int round_batch = min(batch, (3 * alive + 3) / 4);
     if (STATS) {
       n_rounds += lane == 0;
       unsigned long long t = clock64();
@@ -913,7 +918,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       if (done) mode = M_SHADE;
       unsigned long long ready = __ballot(mode == M_SHADE);
       unsigned long long busy = __ballot(mode == M_TRAV);
-      if (busy == 0ull || __popcll(ready) >= batch) break;
+      if (busy == 0ull || __popcll(ready) >= round_batch) break;
     }
     if (STATS) {
       unsigned long long t = clock64();
