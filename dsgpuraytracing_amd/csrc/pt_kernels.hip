@@ -544,13 +544,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   int pix = 0, px = 0, py = 0, sample = 0, s_end = 0;
   uint32_t wslot = 0;  // the work slot (pixel, sample group) this lane renders
   uint32_t rbase = 0, rdim = 0;
-  float3 acc = f3(0, 0, 0);  // pixel sum over samples, in sample order
-  float3 L = f3(0, 0, 0);    // radiance of the current sample
+  float3 acc = f3(0, 0, 0);  // the slot's radiance sum: each path contribution is added as it is found
   float3 T = f3(1, 1, 1);    // path throughput
   int depth = 0;
   bool includeLe = true;
   // shading record of the current path vertex
-  float3 hp = f3(0, 0, 0), ns = f3(0, 0, 1), ng = f3(0, 0, 1), wo = f3(0, 0, 1);
+  float3 hp = f3(0, 0, 0), ns = f3(0, 0, 1), ng = f3(0, 0, 1);
   int bsdf = 0;
   int li = 0, ls = 0;         // NEE cursor: light index, light sample index
   float3 pend = f3(0, 0, 0);  // NEE contribution awaiting its shadow ray
@@ -586,12 +585,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       bool finish = false;  // the sample is complete
       int stage;            // 0: NEE loop, 1: BSDF step, 2: none
       if (shadow) {
-        if (!found) L = L + pend;  // unoccluded (the light sample was already counted)
+        if (!found) acc = acc + pend;  // unoccluded (the light sample was already counted)
         if (DBG && pix == P.dbg_pix) printf("    shadow %s (pend %.6g) prim %d t %.9g\n", found ? "occluded" : "clear", pend.x, tr.hit.prim, tr.hit.t);
         stage = 0;
       } else if (!found) {
         // miss: the environment map if there is one and includeLe (pathtracer.cpp:411-427)
-        if (ENV && includeLe) L = L + mul(T, env_dir(P, tr.d));
+        if (ENV && includeLe) acc = acc + mul(T, env_dir(P, tr.d));
         finish = true;
         stage = 2;
       } else {
@@ -622,8 +621,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         // (sphere.cpp:66-70), which is what tells GlassBSDF a ray is leaving.
         if ((meta & 1) && dot(tr.d, ns) > 0.0f) ns = f3(0, 0, 0) - ns;
         ng = normalize(ng);
-        wo = normalize(make_frame(ns).to_local(f3(0, 0, 0) - tr.d));
-        if (includeLe) L = L + mul(T, ld3(bsdf_at(bsdf).e));
+        if (includeLe) acc = acc + mul(T, ld3(bsdf_at(bsdf).e));
         if (DBG && pix == P.dbg_pix) printf("  depth %d hit prim %d bsdf %d t=%.9g n=(%.6g %.6g %.6g) T=(%.5g)\n", depth, h.prim, bsdf, h.t, ns.x, ns.y, ns.z, T.x);
         li = 0;
         ls = 0;
@@ -633,6 +631,10 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       if (stage < 2) {
         const DBsdf B = bsdf_at(bsdf);
         const Frame fr = make_frame(ns);
+        // w_out (pathtracer.cpp:449-453) is only read by mirror / glass
+        // sampling, which never waits for a shadow ray (f() = 0 there), so it
+        // is rebuilt from the incoming ray in the round of the hit, not kept.
+        const float3 wo = shadow ? f3(0, 0, 1) : normalize(fr.to_local(f3(0, 0, 0) - tr.d));
         bool emitted = false;
         // ---- next-event estimation over all lights (pathtracer.cpp:469-523)
         while (li < P.n_lights) {
@@ -772,7 +774,6 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       }
       PT_STAMP(2);
       if (finish) {
-        acc = acc + L;
         ++sample;
         if (sample < s_end) {
           mode = M_CAMERA;
@@ -864,7 +865,6 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if (STATS) n_cam++;
         if (DBG && pix == P.dbg_pix) printf("pixel (%d,%d) sample %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g)\n", px, py, sample, tr.o.x, tr.o.y, tr.o.z, d.x, d.y, d.z);
         if (box_hit(tr, P.root_lo, P.root_hi)) {
-          L = f3(0, 0, 0);
           T = f3(1, 1, 1);
           depth = 0;
           includeLe = true;
