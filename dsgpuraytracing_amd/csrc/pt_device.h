@@ -36,7 +36,7 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #define PT_ENV_GUIDE 64  // buckets of the environment-CDF guide tables
 #endif
 #ifndef PT_STACK
-#define PT_STACK 32  // traversal stack entries per lane in LDS (lane-contiguous)
+#define PT_STACK 24  // traversal stack entries per lane in LDS (lane-contiguous)
 #endif
 #ifndef PT_STACK_MAX
 #define PT_STACK_MAX 128  // deepest worst-case stack accepted (entries past PT_STACK spill to global memory)

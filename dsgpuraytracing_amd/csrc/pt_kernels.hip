@@ -122,9 +122,8 @@ struct RayState {
 };
 
 struct Hit {
-  float t, u, v;
+  float t;
   int prim;
-  int meta;  // the primitive's (bsdf << 1) | is_triangle, kept from the test
 };
 
 struct Counters {
@@ -132,12 +131,15 @@ struct Counters {
 };
 
 // Resumable stack-based BVH2 traversal state of one lane.
+// The closest hit is (tmax, prim): the shading round rebuilds the barycentrics
+// and reads the material from the primitive record, so no more of the hit is
+// carried through traversal (every persistent value costs a VGPR in all waves).
 struct Trav {
   float3 o, d, inv;
   float tmax;
   int node, sp;
+  int prim;
   bool any, found;
-  Hit hit;
 };
 
 __device__ __forceinline__ void trav_init(Trav& tr, float3 o, float3 d, float tmax, bool any) {
@@ -152,10 +154,23 @@ __device__ __forceinline__ void trav_init(Trav& tr, float3 o, float3 d, float tm
   tr.sp = 0;
   tr.any = any;
   tr.found = false;
-  tr.hit.t = 0.0f;
-  tr.hit.u = tr.hit.v = 0.0f;
-  tr.hit.prim = -1;
-  tr.hit.meta = 0;
+  tr.prim = -1;
+}
+
+// Moller-Trumbore terms of one triangle (u, v, t; det = 0 means parallel).
+// Shared by the traversal test and the shading round's barycentric rebuild,
+// which must agree bit for bit.
+__device__ __forceinline__ float mt_terms(float3 o, float3 d, float3 V0, float3 E1, float3 E2, float& u, float& v,
+                                          float& t) {
+  float3 pv = cross(d, E2);
+  float det = dot(E1, pv);
+  float id = __builtin_amdgcn_rcpf(det);
+  float3 tv = o - V0;
+  u = dot(tv, pv) * id;
+  float3 qv = cross(tv, E1);
+  v = dot(d, qv) * id;
+  t = dot(E2, qv) * id;
+  return det;
 }
 
 // Intersection of one primitive; updates the closest hit in `tr`.  Returns
@@ -168,16 +183,8 @@ __device__ __forceinline__ bool prim_test(const float4 v0, const float4 e1, cons
   float t, u = 0.0f, v = 0.0f;
   if (meta & 1) {  // triangle: Moller-Trumbore; u,v >= 0, u+v <= 1, 0 < t < tmax
     if (STATS) ct.tris++;
-    float3 E1 = f3(e1.x, e1.y, e1.z), E2 = f3(e2.x, e2.y, e2.z);
-    float3 pv = cross(d, E2);
-    float det = dot(E1, pv);
+    const float det = mt_terms(o, d, f3(v0.x, v0.y, v0.z), f3(e1.x, e1.y, e1.z), f3(e2.x, e2.y, e2.z), u, v, t);
     if (det == 0.0f) return false;
-    float id = __builtin_amdgcn_rcpf(det);
-    float3 tv = o - f3(v0.x, v0.y, v0.z);
-    u = dot(tv, pv) * id;
-    float3 qv = cross(tv, E1);
-    v = dot(d, qv) * id;
-    t = dot(E2, qv) * id;
     if (!(u >= 0.0f && v >= 0.0f && u + v <= 1.0f)) return false;
   } else {  // sphere, cancellation-free roots (Haines et al., Ray Tracing Gems ch.7)
     if (STATS) ct.spheres++;
@@ -196,11 +203,7 @@ __device__ __forceinline__ bool prim_test(const float4 v0, const float4 e1, cons
   }
   if (t > 0.0f && t < tr.tmax) {
     tr.tmax = t;
-    tr.hit.t = t;
-    tr.hit.u = u;
-    tr.hit.v = v;
-    tr.hit.prim = pi;
-    tr.hit.meta = meta;
+    tr.prim = pi;
     tr.found = true;
     return tr.any;
   }
@@ -383,7 +386,8 @@ __device__ __forceinline__ bool traverse(const DNode* __restrict__ nodes, const 
   trav_init(tr, o, d, tmax, any);
   while (!trav_step<STATS>(nodes, prims, stk, tr, ct)) {
   }
-  hit = tr.hit;
+  hit.t = tr.tmax;
+  hit.prim = tr.prim;
   return tr.found;
 }
 
@@ -485,8 +489,12 @@ __device__ __forceinline__ void env_sample(const KParams& P, float r1, float r2,
 enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 
 // DBG: diagnostic build that printf-traces the pixel P.dbg_pix (PT_DEBUG_PIXEL=x,y)
+// Occupancy target: 5 waves per SIMD = at most 96 VGPRs (512 / 5, granule 8)
+// and 8 KB of LDS per wave (160 KB / 20 waves per CU; the 24-entry stack is
+// 6 KB).  The traversal is latency-bound, so waves per SIMD pay directly:
+// C3 16.0 / 20.5 / 23.6 / 24.9 Gsamples/s at 2 / 3 / 4 / 5 waves per SIMD.
 #ifndef PT_MIN_WAVES_PER_SIMD
-#define PT_MIN_WAVES_PER_SIMD 4
+#define PT_MIN_WAVES_PER_SIMD 5
 #endif
 // BIN: the reference-count variant, traversing the binary tree (P.nodes2).
 // ENV: the scene has an environment light (kept out of the common build: its
@@ -513,36 +521,27 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     const int nl = P.n_lights * (int)(sizeof(DLight) / 4);
     for (int k = lane; k < nl; k += PT_BLOCK) ((float*)s_light)[k] = ((const float*)P.lights)[k];
   }
-  // table entries read with address-space-typed (ds_read) loads
-  auto bsdf_at = [&](int i) -> DBsdf {
-    if constexpr (GTAB) {
-      return P.bsdfs[i];
-    } else {
-      DBsdf b;
-      lds_f* src = (lds_f*)s_bsdf + i * (int)(sizeof(DBsdf) / 4);
-#pragma unroll
-      for (int k = 0; k < (int)(sizeof(DBsdf) / 4); ++k) ((float*)&b)[k] = src[k];
-      return b;
-    }
+  // Table fields are read where they are used (address-space-typed ds_read
+  // loads in the LDS build), never copied whole into registers: every value
+  // live in the shading code costs a VGPR in all waves.
+  auto bsdf_f = [&](int i, int k) -> float {
+    if constexpr (GTAB) return ((const float*)P.bsdfs)[i * (int)(sizeof(DBsdf) / 4) + k];
+    else return ((lds_f*)s_bsdf)[i * (int)(sizeof(DBsdf) / 4) + k];
   };
-  auto light_at = [&](int i) -> DLight {
-    if constexpr (GTAB) {
-      return P.lights[i];
-    } else {
-      DLight l;
-      lds_f* src = (lds_f*)s_light + i * (int)(sizeof(DLight) / 4);
-#pragma unroll
-      for (int k = 0; k < (int)(sizeof(DLight) / 4); ++k) ((float*)&l)[k] = src[k];
-      return l;
-    }
+  auto light_f = [&](int i, int k) -> float {
+    if constexpr (GTAB) return ((const float*)P.lights)[i * (int)(sizeof(DLight) / 4) + k];
+    else return ((lds_f*)s_light)[i * (int)(sizeof(DLight) / 4) + k];
   };
+#define PT_BSDF3(i, field) f3(bsdf_f(i, offsetof(DBsdf, field) / 4), bsdf_f(i, offsetof(DBsdf, field) / 4 + 1), bsdf_f(i, offsetof(DBsdf, field) / 4 + 2))
+#define PT_LIGHT3(i, field) f3(light_f(i, offsetof(DLight, field) / 4), light_f(i, offsetof(DLight, field) / 4 + 1), light_f(i, offsetof(DLight, field) / 4 + 2))
   __syncthreads();
 
   // ---- per-lane state
   int mode = M_FETCH;
   bool shadow = false;  // the ray in flight is a shadow ray
-  int pix = 0, px = 0, py = 0, sample = 0, s_end = 0;
-  uint32_t wslot = 0;  // the work slot (pixel, sample group) this lane renders
+  // the work slot (pixel, sample group) this lane renders: its pixel and
+  // current sample; the group is sample / group_spp
+  int pix = 0, sample = 0;
   uint32_t rbase = 0, rdim = 0;
   float3 acc = f3(0, 0, 0);  // the slot's radiance sum: each path contribution is added as it is found
   float3 T = f3(1, 1, 1);    // path throughput
@@ -575,6 +574,10 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   const unsigned long long w_start = STATS ? wall_clock64() : 0ull;
 
   const uint32_t n_groups = (uint32_t)P.n_groups;
+  // partial-sum slot of a finished group: (pixel, group of the last sample)
+  auto slot_of = [&](int p, int s_next) -> size_t {
+    return (size_t)p * n_groups + (uint32_t)((s_next - 1) / P.group_spp);
+  };
   const uint32_t total_slots = (uint32_t)P.n_blocks * 64u * n_groups;
   const int batch = P.shade_batch;
 
@@ -586,7 +589,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       int stage;            // 0: NEE loop, 1: BSDF step, 2: none
       if (shadow) {
         if (!found) acc = acc + pend;  // unoccluded (the light sample was already counted)
-        if (DBG && pix == P.dbg_pix) printf("    shadow %s (pend %.6g) prim %d t %.9g\n", found ? "occluded" : "clear", pend.x, tr.hit.prim, tr.hit.t);
+        if (DBG && pix == P.dbg_pix) printf("    shadow %s (pend %.6g) prim %d t %.9g\n", found ? "occluded" : "clear", pend.x, tr.prim, tr.tmax);
         stage = 0;
       } else if (!found) {
         // miss: the environment map if there is one and includeLe (pathtracer.cpp:411-427)
@@ -599,20 +602,21 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         // are rebuilt from the primitive (barycentrics / sphere reprojection),
         // not o + t*d, so their error is relative to the primitive and the
         // 256-ulp origin offset always clears the surface.
-        const Hit h = tr.hit;
-        const int meta = h.meta;
+        const DPrim pr = P.prims[tr.prim];
+        const int meta = __float_as_int(pr.v0.w);  // (bsdf << 1) | is_triangle
         bsdf = meta >> 1;
-        const DPrim pr = P.prims[h.prim];
         if (meta & 1) {
-          const float* nn = P.norms + 9 * (size_t)h.prim;
-          float w0 = 1.0f - h.u - h.v;
-          float3 E1 = f3(pr.e1.x, pr.e1.y, pr.e1.z), E2 = f3(pr.e2.x, pr.e2.y, pr.e2.z);
-          hp = f3(pr.v0.x, pr.v0.y, pr.v0.z) + E1 * h.u + E2 * h.v;
-          ns = ld3(nn) * w0 + ld3(nn + 3) * h.u + ld3(nn + 6) * h.v;
+          const float* nn = P.norms + 9 * (size_t)tr.prim;
+          float3 V0 = f3(pr.v0.x, pr.v0.y, pr.v0.z), E1 = f3(pr.e1.x, pr.e1.y, pr.e1.z), E2 = f3(pr.e2.x, pr.e2.y, pr.e2.z);
+          float hu, hv, ht;
+          mt_terms(tr.o, tr.d, V0, E1, E2, hu, hv, ht);  // the barycentrics of the traversal test
+          float w0 = 1.0f - hu - hv;
+          hp = V0 + E1 * hu + E2 * hv;
+          ns = ld3(nn) * w0 + ld3(nn + 3) * hu + ld3(nn + 6) * hv;
           ng = cross(E1, E2);
         } else {
           float3 C = f3(pr.v0.x, pr.v0.y, pr.v0.z);
-          ns = normalize(tr.o + tr.d * h.t - C);
+          ns = normalize(tr.o + tr.d * tr.tmax - C);
           hp = C + ns * pr.e1.x;
           ng = ns;
         }
@@ -621,25 +625,21 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         // (sphere.cpp:66-70), which is what tells GlassBSDF a ray is leaving.
         if ((meta & 1) && dot(tr.d, ns) > 0.0f) ns = f3(0, 0, 0) - ns;
         ng = normalize(ng);
-        if (includeLe) acc = acc + mul(T, ld3(bsdf_at(bsdf).e));
-        if (DBG && pix == P.dbg_pix) printf("  depth %d hit prim %d bsdf %d t=%.9g n=(%.6g %.6g %.6g) T=(%.5g)\n", depth, h.prim, bsdf, h.t, ns.x, ns.y, ns.z, T.x);
+        if (includeLe) acc = acc + mul(T, PT_BSDF3(bsdf, e));
+        if (DBG && pix == P.dbg_pix) printf("  depth %d hit prim %d bsdf %d t=%.9g n=(%.6g %.6g %.6g) T=(%.5g)\n", depth, tr.prim, bsdf, tr.tmax, ns.x, ns.y, ns.z, T.x);
         li = 0;
         ls = 0;
         stage = 0;
       }
       PT_STAMP(0);
       if (stage < 2) {
-        const DBsdf B = bsdf_at(bsdf);
+        const int btype = __float_as_int(bsdf_f(bsdf, 0));
         const Frame fr = make_frame(ns);
-        // w_out (pathtracer.cpp:449-453) is only read by mirror / glass
-        // sampling, which never waits for a shadow ray (f() = 0 there), so it
-        // is rebuilt from the incoming ray in the round of the hit, not kept.
-        const float3 wo = shadow ? f3(0, 0, 1) : normalize(fr.to_local(f3(0, 0, 0) - tr.d));
         bool emitted = false;
         // ---- next-event estimation over all lights (pathtracer.cpp:469-523)
         while (li < P.n_lights) {
-          const DLight Lt = light_at(li);
-          const bool delta = Lt.type == 0 || Lt.type == 2;
+          const int ltype = __float_as_int(light_f(li, 0));
+          const bool delta = ltype == 0 || ltype == 2;
           const int nls = delta ? 1 : P.ns_area;
           if (ls >= nls) {
             ++li;
@@ -649,47 +649,47 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           float3 wi;
           float dist, pdf;
           bool lit = true;
-          if (ENV && Lt.type == 4) {  // EnvironmentLight::sample_L (environment_light.cpp:117-128)
+          if (ENV && ltype == 4) {  // EnvironmentLight::sample_L (environment_light.cpp:117-128)
             float r1 = ptrng::draw(rbase, rdim++);
             float r2 = ptrng::draw(rbase, rdim++);
             env_sample(P, r1, r2, wi, pdf);
             dist = 3.0e38f;
-          } else if (Lt.type == 3) {  // AreaLight::sample_L (light.cpp:80-92); grid sampler draws y first
+          } else if (ltype == 3) {  // AreaLight::sample_L (light.cpp:80-92); grid sampler draws y first
             float u0 = ptrng::draw(rbase, rdim++);
             float u1 = ptrng::draw(rbase, rdim++);
             float sx = u1 - 0.5f, sy = u0 - 0.5f;
-            float3 dv = ld3(Lt.pos) + ld3(Lt.dimx) * sx + ld3(Lt.dimy) * sy - hp;
-            float cosL = dot(dv, ld3(Lt.dir));
+            float3 dv = PT_LIGHT3(li, pos) + PT_LIGHT3(li, dimx) * sx + PT_LIGHT3(li, dimy) * sy - hp;
+            float cosL = dot(dv, PT_LIGHT3(li, dir));
             float sq = dot(dv, dv);
             dist = fsqrt(sq);
             wi = dv * rcp(dist);
-            pdf = sq * rcp(Lt.area * fabsf(cosL));  // unnormalised d.dir, as the reference
+            pdf = sq * rcp(light_f(li, offsetof(DLight, area) / 4) * fabsf(cosL));  // unnormalised d.dir, as the reference
             lit = cosL < 0.0f;
-          } else if (Lt.type == 1) {  // InfiniteHemisphereLight (light.cpp:34-42)
+          } else if (ltype == 1) {  // InfiniteHemisphereLight (light.cpp:34-42)
             float r1 = ptrng::draw(rbase, rdim++);
             float r2 = ptrng::draw(rbase, rdim++);
             float st = fsqrt(fmaxf(0.0f, 1.0f - r1 * r1));
             wi = f3(st * cos_rev(r2), r1, -st * sin_rev(r2));  // phi = 2 pi r2
             dist = 3.0e38f;
             pdf = 0.15915494309189535f;
-          } else if (Lt.type == 2) {  // PointLight (light.cpp:49-57)
-            float3 dv = ld3(Lt.pos) - hp;
+          } else if (ltype == 2) {  // PointLight (light.cpp:49-57)
+            float3 dv = PT_LIGHT3(li, pos) - hp;
             dist = fsqrt(dot(dv, dv));
             wi = dv * rcp(dist);
             pdf = 1.0f;
           } else {  // DirectionalLight (light.cpp:17-23)
-            wi = ld3(Lt.dir);
+            wi = PT_LIGHT3(li, dir);
             dist = 3.0e38f;
             pdf = 1.0f;
           }
           const float scale = 1.0f / (float)nls;
           ++ls;
           // f() is zero for every BSDF but Diffuse (bsdf.cpp:34-202): nothing to add.
-          if (B.type != 0 || !lit) continue;
+          if (btype != 0 || !lit) continue;
           float cos_t = fmaxf(0.0f, fr.to_local(wi).z);
           if (!(cos_t > 0.0f)) continue;
-          float3 f = ld3(B.a) * 0.31830988618379067f;
-          const float3 Le = (ENV && Lt.type == 4) ? env_dir(P, wi) : ld3(Lt.rad);
+          float3 f = PT_BSDF3(bsdf, a) * 0.31830988618379067f;
+          const float3 Le = (ENV && ltype == 4) ? env_dir(P, wi) : PT_LIGHT3(li, rad);
           pend = mul(mul(T, Le * (cos_t * rcp(pdf))), f) * scale;
           // shadow ray (pathtracer.cpp:497-504): delta lights offset EPS_N along n
           float3 so = delta ? hp + ns * 5e-3f : offset_ray(hp, dot(wi, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng);
@@ -710,19 +710,24 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           float3 wi;
           float pdf = 1.0f;
           float3 f;
-          if (B.type == 0 || B.type == 4) {  // cosine hemisphere (sampler.cpp:44-55)
+          if (btype == 0 || btype == 4) {  // cosine hemisphere (sampler.cpp:44-55)
             float r1 = ptrng::draw(rbase, rdim++);
             float r2 = ptrng::draw(rbase, rdim++);
             float ct = fsqrt(1.0f - r1);  // cos(acos(1 - 2 r1) / 2)
             float stt = fsqrt(r1);
             wi = f3(stt * cos_rev(r2), stt * sin_rev(r2), ct);  // phi = 2 pi r2
             pdf = ct * 0.31830988618379067f;
-            f = B.type == 0 ? ld3(B.a) * 0.31830988618379067f : f3(0, 0, 0);
-          } else if (B.type == 1) {  // MirrorBSDF::sample_f (bsdf.cpp:60-69)
+            f = btype == 0 ? PT_BSDF3(bsdf, a) * 0.31830988618379067f : f3(0, 0, 0);
+          } else if (btype == 1) {  // MirrorBSDF::sample_f (bsdf.cpp:60-69)
+            // w_out (pathtracer.cpp:449-453) is only read by mirror / glass
+            // sampling, which never waits for a shadow ray (f() = 0 there):
+            // tr still holds the incoming ray, so it is rebuilt here, not kept.
+            const float3 wo = normalize(fr.to_local(f3(0, 0, 0) - tr.d));
             wi = f3(-wo.x, -wo.y, wo.z);
-            f = ld3(B.a) * (1.0f / fmaxf(wo.z, 1e-8f));
+            f = PT_BSDF3(bsdf, a) * (1.0f / fmaxf(wo.z, 1e-8f));
           } else {  // Refraction (bsdf.cpp:90-111) / Glass (bsdf.cpp:120-158)
-            float ratio = B.ior;
+            const float3 wo = normalize(fr.to_local(f3(0, 0, 0) - tr.d));
+            float ratio = bsdf_f(bsdf, offsetof(DBsdf, ior) / 4);
             float sgn = 1.0f;
             if (wo.z > 0.0f) {
               sgn = -1.0f;
@@ -731,16 +736,16 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             float cos2 = 1.0f - ratio * ratio * (1.0f - wo.z * wo.z);
             bool tir = cos2 < 0.0f;
             wi = tir ? f3(-wo.x, -wo.y, wo.z) : normalize(f3(-wo.x * ratio, -wo.y * ratio, sgn * fsqrt(cos2)));
-            float ni = B.ior, no = 1.0f;
+            float ni = bsdf_f(bsdf, offsetof(DBsdf, ior) / 4), no = 1.0f;
             if (wo.z < 0.0f) {
               ni = 1.0f;
-              no = B.ior;
+              no = bsdf_f(bsdf, offsetof(DBsdf, ior) / 4);
             }
             float inv_cos = 1.0f / fmaxf(fabsf(wi.z), 1e-8f);
-            if (B.type == 2) {
-              f = tir ? f3(0, 0, 0) : ld3(B.t) * ((no / ni) * (no / ni) * inv_cos);
+            if (btype == 2) {
+              f = tir ? f3(0, 0, 0) : PT_BSDF3(bsdf, t) * ((no / ni) * (no / ni) * inv_cos);
             } else if (tir) {
-              f = ld3(B.t) * inv_cos;  // quirk kept: TIR returns transmittance (bsdf.cpp:129-131)
+              f = PT_BSDF3(bsdf, t) * inv_cos;  // quirk kept: TIR returns transmittance (bsdf.cpp:129-131)
             } else {
               float ci = fabsf(wi.z), co = fabsf(wo.z);
               float r1 = (no * ci - ni * co) / (no * ci + ni * co);
@@ -748,9 +753,9 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
               float Fr = 0.5f * (r1 * r1 + r2 * r2);
               if (ptrng::draw(rbase, rdim++) <= Fr) {
                 wi = f3(-wo.x, -wo.y, wo.z);
-                f = ld3(B.a) * (1.0f / fmaxf(fabsf(wi.z), 1e-8f));
+                f = PT_BSDF3(bsdf, a) * (1.0f / fmaxf(fabsf(wi.z), 1e-8f));
               } else {
-                f = ld3(B.t) * ((no / ni) * (no / ni) * inv_cos);
+                f = PT_BSDF3(bsdf, t) * ((no / ni) * (no / ni) * inv_cos);
               }
             }
           }
@@ -764,7 +769,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             T = mul(T, f * (fabsf(wi.z) * rcp(pdf * (1.0f - pterm))));
             float3 v = normalize(fr.to_world(wi));
             trav_init(tr, offset_ray(hp, dot(v, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng), v, 3.0e38f, false);
-            includeLe = B.type == 1 || B.type == 2 || B.type == 3;
+            includeLe = btype == 1 || btype == 2 || btype == 3;
             ++depth;
             shadow = false;
             mode = M_TRAV;
@@ -775,10 +780,10 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       PT_STAMP(2);
       if (finish) {
         ++sample;
-        if (sample < s_end) {
+        if (sample < P.spp && sample % P.group_spp != 0) {
           mode = M_CAMERA;
         } else {
-          store3(P.partial + 3 * (size_t)wslot, acc);
+          store3(P.partial + 3 * slot_of(pix, sample), acc);
           mode = M_FETCH;
         }
       }
@@ -830,12 +835,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             int4 b = P.blocks[bq >> 6];
             int qx = (int)(bq & 7u), qy = (int)((bq >> 3) & 7u);
             if (qx < b.z && qy < b.w) {
-              px = b.x + qx;
-              py = b.y + qy;
-              pix = px + py * P.W;
+              pix = b.x + qx + (b.y + qy) * P.W;
               sample = (int)g * P.group_spp;
-              s_end = min(P.spp, sample + P.group_spp);
-              wslot = (uint32_t)pix * n_groups + g;
               acc = f3(0, 0, 0);
               mode = M_CAMERA;
             }
@@ -854,6 +855,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       while (mode == M_CAMERA) {
         rbase = ptrng::stream_base(P.seed, (uint32_t)pix, (uint32_t)sample);
         rdim = 0;
+        const int py = pix / P.W, px = pix - py * P.W;
         float ry = ptrng::draw(rbase, rdim++);  // UniformGridSampler2D draws y first
         float rx = ptrng::draw(rbase, rdim++);
         float fx = ((float)px + rx) * P.inv_w;
@@ -874,8 +876,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         }
         // miss: the sample sees the environment (includeLe) or nothing
         if (ENV) acc = acc + env_dir(P, d);
-        if (++sample >= s_end) {
-          store3(P.partial + 3 * (size_t)wslot, acc);
+        if (++sample >= P.spp || sample % P.group_spp == 0) {
+          store3(P.partial + 3 * slot_of(pix, sample), acc);
           mode = M_FETCH;
         }
       }
@@ -983,7 +985,6 @@ __global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __rest
   float3 D = f3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
   Hit h;
   h.t = 0;
-  h.u = h.v = 0;
   h.prim = -1;
   Counters ct = {0, 0, 0};
   bool f = traverse<false>(nodes, prims, stk, O, D, 3.0e38f, false, h, ct);
