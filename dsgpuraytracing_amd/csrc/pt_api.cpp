@@ -195,7 +195,7 @@ int pt_create(int device, pt_ctx** out) {
   HIPCHK(hipEventCreate(&c->ev1));
   HIPCHK(hipEventCreate(&c->ev2));
   HIPCHK(c->counter.reserve(1));
-  HIPCHK(c->stats.reserve(32));
+  HIPCHK(c->stats.reserve(PT_STATS_SLOTS));
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, device));
   // Persistent grid: as many one-wave workgroups as can be resident.  The
@@ -206,6 +206,8 @@ int pt_create(int device, pt_ctx** out) {
   HIPCHK(ptk_render_occupancy(&c->bpc_stats, true));
   c->grid_plain = std::max(8, c->bpc_plain) * c->n_cu;
   c->grid_stats = std::max(8, c->bpc_stats) * c->n_cu;
+  // counters + one trace record per wave of the largest stats grid
+  HIPCHK(c->stats.reserve(PT_STATS_SLOTS + (size_t)PT_WAVE_TRACE * std::max(c->grid_stats, 64 * c->n_cu)));
   *out = c;
   return PT_OK;
 }
@@ -721,8 +723,8 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   }
   HIPCHK(hipMemsetAsync(c->counter.p, 0, sizeof(uint32_t), s));
   if (stats) {
-    unsigned long long init[32] = {0};
-    init[21] = init[23] = ~0ull;  // atomicMin slots
+    unsigned long long init[PT_STATS_SLOTS] = {0};
+    init[21] = init[23] = init[25] = ~0ull;  // atomicMin slots
     HIPCHK(hipMemcpyAsync(c->stats.p, init, sizeof(init), hipMemcpyHostToDevice, s));
   }
   KParams P;
@@ -842,6 +844,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.partial = c->partial.p;
   int64_t max_grid = std::max<int64_t>(1, (slots + PT_BLOCK - 1) / PT_BLOCK);
   int grid = (int)std::min<int64_t>(want, max_grid);
+  if (stats && (size_t)grid * PT_WAVE_TRACE + PT_STATS_SLOTS > c->stats.n) grid = (int)((c->stats.n - PT_STATS_SLOTS) / PT_WAVE_TRACE);
   P.stack_spill = nullptr;
   if (c->bvh_stack > PT_STACK) {  // worst-case depth beyond the LDS stack
     HIPCHK(c->spill.reserve((size_t)(c->bvh_stack - PT_STACK) * grid * PT_BLOCK));
@@ -853,6 +856,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   HIPCHK(ptk_launch_resolve(&P, s));
   HIPCHK(hipEventRecord(c->ev2, s));
   c->last.grid_blocks = grid;
+  c->last.group_spp = P.group_spp;
   c->last.blocks_per_cu = stats ? c->bpc_stats : c->bpc_plain;
   int64_t px = 0;
   for (const int4& t : tl) px += (int64_t)t.z * t.w;
@@ -871,8 +875,8 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags) {
   HIPCHK(hipEventElapsedTime(&ms, c->ev1, c->ev2));
   c->last.resolve_ms = ms;
   if (flags & (PT_FLAG_STATS | PT_FLAG_REF_COUNTS)) {
-    unsigned long long v[32] = {0};
-    HIPCHK(hipMemcpy(v, c->stats.p, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    unsigned long long v[PT_STATS_SLOTS] = {0};
+    HIPCHK(hipMemcpy(v, c->stats.p, sizeof(v), hipMemcpyDeviceToHost));
     c->last.camera_rays = (int64_t)v[0];
     c->last.bounce_rays = (int64_t)v[1];
     c->last.shadow_rays = (int64_t)v[2];
@@ -893,6 +897,7 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags) {
     c->last.hitshade_clocks = (int64_t)v[16];
     for (int k = 0; k < 4; ++k) c->last.section_clocks[k] = (int64_t)v[17 + k];
     for (int k = 0; k < 3; ++k) c->last.wave_span[k] = (int64_t)(v[22 + k] - v[21]);
+    for (int k = 0; k < 2; ++k) c->last.wave_span[3 + k] = v[25 + k] ? (int64_t)(v[25 + k] - v[21]) : -1;
     c->last.counters_valid = 1;
   }
   return PT_OK;
@@ -1003,6 +1008,19 @@ int pt_intersect(pt_ctx* c, int64_t n, const double* o, const double* d, const d
 int pt_get_stats(pt_ctx* c, pt_stats* out) {
   if (!c || !out) return fail(PT_E_INVALID, "pt_get_stats: NULL argument");
   *out = c->last;
+  return PT_OK;
+}
+
+int pt_get_wave_trace(pt_ctx* c, int64_t* out, int64_t cap, int64_t* n_waves) {
+  if (!c || !n_waves) return fail(PT_E_INVALID, "pt_get_wave_trace: NULL argument");
+  if (!c->last.counters_valid) return fail(PT_E_INVALID, "pt_get_wave_trace: the last launch had no counters");
+  const int64_t n = c->last.grid_blocks;
+  *n_waves = n;
+  if (!out) return PT_OK;
+  if (cap < n * PT_WAVE_TRACE) return fail(PT_E_INVALID, "pt_get_wave_trace: buffer too small");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpy(out, c->stats.p + PT_STATS_SLOTS, (size_t)n * PT_WAVE_TRACE * sizeof(int64_t),
+                   hipMemcpyDeviceToHost));
   return PT_OK;
 }
 

@@ -35,6 +35,8 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #ifndef PT_ENV_GUIDE
 #define PT_ENV_GUIDE 64  // buckets of the environment-CDF guide tables
 #endif
+#define PT_STATS_SLOTS 32  // launch counters; per-wave trace records (PT_WAVE_TRACE u64 each) follow
+#define PT_WAVE_TRACE 9
 #ifndef PT_STACK
 #define PT_STACK 24  // traversal stack entries per lane in LDS (lane-contiguous)
 #endif

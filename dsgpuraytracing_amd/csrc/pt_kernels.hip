@@ -9,7 +9,7 @@
 // Design (MI355X-first, not a translation):
 //  * one persistent megakernel, one wave64 per workgroup; a lane owns one
 //    (pixel, sample group) work slot at a time, renders its samples in order
-//    and stores their sum; resolve_kernel sums a pixel's groups in group order
+//    and stores their sum; resolve_kernel sums a pixel's groups in a fixed order
 //    (deterministic, no float atomics, independent of tile->GPU assignment);
 //  * the recursion of trace_ray becomes an iterative throughput loop driven by a
 //    per-lane state machine that owns exactly ONE ray (extension or shadow);
@@ -572,6 +572,16 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   }
   unsigned long long t_mark = STATS ? clock64() : 0ull;
   const unsigned long long w_start = STATS ? wall_clock64() : 0ull;
+  unsigned long long w_empty = 0ull;  // when this wave first found the queue empty
+  unsigned long long slot_t0 = 0ull, slot_lat_sum = 0ull, slot_lat_max = 0ull;  // work-slot latency (wall ticks)
+  // per ray: traversal iterations it stepped in / sat out, traversal phases it spanned
+  uint32_t r_steps = 0, r_idle = 0, r_rounds = 0, ray_steps_max = 0, ray_idle_max = 0, ray_rounds_max = 0;
+#define PT_SLOT_DONE()                                           \
+  if (STATS) {                                                   \
+    const unsigned long long d_ = wall_clock64() - slot_t0;     \
+    slot_lat_sum += d_;                                          \
+    slot_lat_max = d_ > slot_lat_max ? d_ : slot_lat_max;        \
+  }
 
   const uint32_t n_groups = (uint32_t)P.n_groups;
   // partial-sum slot of a finished group: (pixel, group of the last sample)
@@ -784,6 +794,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           mode = M_CAMERA;
         } else {
           store3(P.partial + 3 * slot_of(pix, sample), acc);
+          PT_SLOT_DONE();
           mode = M_FETCH;
         }
       }
@@ -824,6 +835,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           uint32_t slot = rank < avail ? chunk_next + rank : nbase + (rank - avail);
           if (slot >= total_slots) {
             mode = M_DONE;
+            if (STATS && w_empty == 0ull) w_empty = wall_clock64();
           } else {
             // slot = (block * 64 + pixel-in-block) * n_groups + group: the
             // groups of one pixel sit on neighbouring lanes (coherent rays).
@@ -838,6 +850,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
               pix = b.x + qx + (b.y + qy) * P.W;
               sample = (int)g * P.group_spp;
               acc = f3(0, 0, 0);
+              if (STATS) slot_t0 = wall_clock64();
               mode = M_CAMERA;
             }
           }
@@ -878,6 +891,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if (ENV) acc = acc + env_dir(P, d);
         if (++sample >= P.spp || sample % P.group_spp == 0) {
           store3(P.partial + 3 * slot_of(pix, sample), acc);
+          PT_SLOT_DONE();
           mode = M_FETCH;
         }
       }
@@ -899,6 +913,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       cyc_shade += lane == 0 ? t - t_mark : 0ull;
       t_mark = t;
     }
+    if (STATS) r_rounds += mode == M_TRAV;
     for (;;) {
       if (STATS) n_titer += lane == 0;
       // one kind of step per iteration: leaf steps once enough lanes wait on
@@ -908,7 +923,13 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       const int n_leaf = __popcll(__ballot(at_leaf));
       const int n_node = __popcll(__ballot(trav && !at_leaf));
       bool done = false;
-      if (n_leaf > 0 && (n_node == 0 || n_leaf * P.leaf_weight >= n_node * 16)) {
+      const bool leaf_iter = n_leaf > 0 && (n_node == 0 || n_leaf * P.leaf_weight >= n_node * 16);
+      if (STATS && trav) {
+        const bool stepped = leaf_iter == at_leaf;
+        r_steps += stepped;
+        r_idle += !stepped;
+      }
+      if (leaf_iter) {
         if (at_leaf) done = leaf_step<STATS>(P.prims, stk, tr, ct);
         if (STATS) n_leafit += lane == 0;
       } else {
@@ -918,6 +939,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         }
       }
       if (done) mode = M_SHADE;
+      if (STATS && done) {
+        ray_steps_max = max(ray_steps_max, r_steps);
+        ray_idle_max = max(ray_idle_max, r_idle);
+        ray_rounds_max = max(ray_rounds_max, r_rounds);
+        r_steps = r_idle = r_rounds = 0;
+      }
       unsigned long long ready = __ballot(mode == M_SHADE);
       unsigned long long busy = __ballot(mode == M_TRAV);
       if (busy == 0ull || __popcll(ready) >= round_batch) break;
@@ -938,6 +965,21 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       if (lane == 0) atomicAdd(P.stats + k, s);
     }
     // load balance: the slowest wave bounds the launch
+    w_empty = w_empty ? w_empty : ~0ull;
+    for (int off = 32; off > 0; off >>= 1) {
+      const unsigned long long o = __shfl_xor(w_empty, off);
+      w_empty = o < w_empty ? o : w_empty;
+    }
+    uint32_t slots_done = n_cam;  // camera samples this wave started
+    for (int off = 32; off > 0; off >>= 1) {
+      slots_done += __shfl_xor(slots_done, off);
+      slot_lat_sum += __shfl_xor(slot_lat_sum, off);
+      const unsigned long long o = __shfl_xor(slot_lat_max, off);
+      slot_lat_max = o > slot_lat_max ? o : slot_lat_max;
+      ray_steps_max = max(ray_steps_max, (uint32_t)__shfl_xor((int)ray_steps_max, off));
+      ray_idle_max = max(ray_idle_max, (uint32_t)__shfl_xor((int)ray_idle_max, off));
+      ray_rounds_max = max(ray_rounds_max, (uint32_t)__shfl_xor((int)ray_rounds_max, off));
+    }
     if (lane == 0) {
       unsigned long long w = wall_clock64() - w_start;
       atomicMax(P.stats + 13, cyc_shade + cyc_hitshade + cyc_trav);
@@ -947,26 +989,61 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       atomicMax(P.stats + 22, w_start);
       atomicMin(P.stats + 23, w_end);
       atomicMax(P.stats + 24, w_end);
+      if (w_empty != ~0ull) {
+        atomicMin(P.stats + 25, w_empty);
+        atomicMax(P.stats + 26, w_empty);
+      }
       for (int k = 0; k < 4; ++k) atomicAdd(P.stats + 17 + k, cyc_sec[k]);
       atomicAdd(P.stats + 14, w);
       atomicMax(P.stats + 15, w);
+      // per-wave trace (pt_get_wave_trace): start, first empty queue, end,
+      // (XCC id << 32 | HW_ID), camera samples
+      unsigned long long* tw = P.stats + PT_STATS_SLOTS + PT_WAVE_TRACE * (size_t)blockIdx.x;
+      tw[0] = w_start;
+      tw[1] = w_empty;
+      tw[2] = w_end;
+      tw[3] = ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32) |
+              (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+      tw[4] = slots_done;
+      tw[5] = slot_lat_sum;
+      tw[6] = slot_lat_max;
+      tw[7] = ((unsigned long long)ray_steps_max << 32) | ray_idle_max;
+      tw[8] = ray_rounds_max;
     }
   }
 }
 
-// Sums each pixel's sample groups in group order (so the sum is a fixed
-// function of the pixel, independent of scheduling) and writes the pixel's
-// average, SampleBuffer-style (pathtracer.cpp:577-581).  One lane per pixel.
+// Lanes that resolve one pixel: the pixel's groups are read as one coalesced
+// run (the per-pixel partials are n_groups * 12 B contiguous).
+__host__ __device__ __forceinline__ int resolve_team(int n_groups) {
+  int k = 1;
+  while (k < n_groups && k < 64) k <<= 1;
+  return k;
+}
+
+// Sums each pixel's sample groups in a fixed order (so the sum is a fixed
+// function of the pixel, independent of scheduling and of the tile -> GPU
+// assignment) and writes the pixel's average, SampleBuffer-style
+// (pathtracer.cpp:577-581).  A team of k lanes (power of two) per pixel: lane
+// j sums groups j, j+k, j+2k, ... in order, then the team adds its k partial
+// sums by a fixed butterfly.  One lane per pixel read 12-B words n_groups * 12
+// B apart (C5: 3 KB stride, 1.4 TB/s); the team reads contiguous runs.
 __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
-  const uint32_t tq = blockIdx.x * 256u + threadIdx.x;
-  if (tq >= (uint32_t)P.n_tiles * 1024u) return;
-  int2 xy = tile_pixel(P.tiles[tq >> 10], tq & 1023u);
-  if (xy.x < 0) return;
+  const int k = resolve_team(P.n_groups);
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t tq = t / (uint32_t)k;  // pixel slot (k is a power of two: a shift)
+  const int j = (int)(t & (uint32_t)(k - 1));
+  const bool live = tq < (uint32_t)P.n_tiles * 1024u;
+  int2 xy = live ? tile_pixel(P.tiles[tq >> 10], tq & 1023u) : make_int2(-1, -1);
   float3 acc = f3(0, 0, 0);
-  if (!culled(P, xy.x, xy.y)) {
+  if (xy.x >= 0 && !culled(P, xy.x, xy.y)) {
     const float* p = P.partial + 3 * ((size_t)xy.x + (size_t)xy.y * (size_t)P.W) * (size_t)P.n_groups;
-    for (int g = 0; g < P.n_groups; ++g) acc = acc + ld3(p + 3 * g);
+    for (int g = j; g < P.n_groups; g += k) acc = acc + ld3(p + 3 * g);
   }
+  // team lanes are consecutive, aligned, and all reach the shuffles
+  for (int off = 1; off < k; off <<= 1)
+    acc = acc + f3(__shfl_xor(acc.x, off), __shfl_xor(acc.y, off), __shfl_xor(acc.z, off));
+  if (xy.x < 0 || j != 0) return;
   const float inv_spp = (float)(1.0 / (double)P.spp);
   store3(P.out + 3 * ((size_t)xy.x + (size_t)xy.y * (size_t)P.W), acc * inv_spp);
 }
@@ -1025,7 +1102,7 @@ extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, 
 }
 
 extern "C" hipError_t ptk_launch_resolve(const KParams* P, hipStream_t s) {
-  int grid = (int)(((int64_t)P->n_tiles * 1024 + 255) / 256);
+  int grid = (int)(((int64_t)P->n_tiles * 1024 * ptk::resolve_team(P->n_groups) + 255) / 256);
   hipLaunchKernelGGL(ptk::resolve_kernel, dim3(grid), dim3(256), 0, s, *P);
   return hipGetLastError();
 }

@@ -90,7 +90,7 @@ class pt_stats(ctypes.Structure):
                 ("max_wave_clocks", c_int64), ("wave_wall_sum", c_int64), ("wave_wall_max", c_int64),
                 ("leaf_steps", c_int64), ("hitshade_clocks", c_int64), ("resolve_ms", c_double),
                 ("bvh_stack", c_int32), ("bvh_nodes", c_int64), ("section_clocks", c_int64 * 4),
-                ("wave_span", c_int64 * 3)]
+                ("wave_span", c_int64 * 5), ("group_spp", c_int32)]
 
 
 # Every symbol include/ptgpu.h and include/ptgpu_scene.h declare, with ctypes signatures.
@@ -106,6 +106,7 @@ _SIGS = {
     "pt_intersect": (c_int32, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
     "pt_get_stats": (c_int32, [c_void_p, POINTER(pt_stats)]),
+    "pt_get_wave_trace": (c_int32, [c_void_p, c_void_p, c_int64, POINTER(c_int64)]),
     "pt_last_error": (c_char_p, []),
     # include/ptgpu_scene.h (bound with full types in scene_loader.py)
     "pt_host_scene_load": (c_int32, [c_char_p, c_int32, c_int32, c_char_p, POINTER(c_void_p)]),

@@ -121,6 +121,18 @@ class Device:
         out["wave_span"] = list(s.wave_span)
         return out
 
+    def wave_trace(self) -> np.ndarray:
+        """Per-wave records of the last stats launch (pt_get_wave_trace):
+        int64 (waves, 7) = start, first empty-queue time (-1: never), end,
+        (XCC id << 32 | HW_ID), camera samples started, sum and max of the
+        work-slot latencies (wall-clock ticks, 100 MHz), per-ray maxima of
+        traversal iterations stepped (<< 32) | idle, and of traversal phases."""
+        n = ctypes.c_int64(0)
+        check(self._lib.pt_get_wave_trace(self.handle, None, 0, ctypes.byref(n)))
+        buf = np.zeros((n.value, 9), np.int64)
+        check(self._lib.pt_get_wave_trace(self.handle, buf.ctypes.data, buf.size, ctypes.byref(n)))
+        return buf
+
 
 class Scene:
     """A flattened scene (what BVHAccel + the lights hand to the GPU seam)."""

@@ -185,8 +185,10 @@ typedef struct pt_stats {
   int64_t bvh_nodes;       /* 4-wide BVH nodes uploaded */
   int64_t section_clocks[4]; /* of shade_clocks: hit record, light sampling, BSDF sampling, queue fetch
                                 (the rest: camera rays) */
-  int64_t wave_span[3];    /* wall-clock ticks after the first wave started: last wave start,
-                              first wave end, last wave end (launch ramp and tail) */
+  int64_t wave_span[5];    /* wall-clock ticks after the first wave started: last wave start,
+                              first wave end, last wave end, first and last time a wave found
+                              the work queue empty (launch ramp, queue drain and tail) */
+  int32_t group_spp;       /* samples per work slot (pixel, sample group) of the last launch */
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */
@@ -218,6 +220,14 @@ int pt_render_tiles_device(pt_ctx* ctx, const pt_tile* tiles, int32_t n_tiles, f
 int pt_intersect(pt_ctx* ctx, int64_t n, const double* o, const double* d, const double* max_t,
                  int32_t* hit, float* t, int32_t* prim, int32_t* any_hit);
 int pt_get_stats(pt_ctx* ctx, pt_stats* out);
+/* Diagnostics (no reference counterpart): after a PT_FLAG_STATS launch, one
+ * record of 9 int64 per wave -- device wall-clock start, first time the wave
+ * found the work queue empty (~0 if never), end, (XCC id << 32 | HW_ID), the
+ * camera samples it started, the sum and maximum of its work slots'
+ * latencies (claim to partial-sum store, wall-clock ticks), the most
+ * traversal iterations one ray stepped in (<< 32) | sat out, and the most
+ * traversal phases one ray spanned.  out == NULL: only *n_waves is set. */
+int pt_get_wave_trace(pt_ctx* ctx, int64_t* out, int64_t cap, int64_t* n_waves);
 const char* pt_last_error(void);
 
 #ifdef __cplusplus
