@@ -262,7 +262,8 @@ __device__ __forceinline__ bool trav_pop(const Stack& stk, Trav& tr) {
 
 __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb) {
   const bool sw = db < da;
-  const float td = sw ? db : da, tr = sw ? rb : ra;
+  const float td = sw ? db : da;
+  const int tr = sw ? rb : ra;  // references stay integers (leaf cursors exceed 2^24)
   db = sw ? da : db;
   rb = sw ? ra : rb;
   da = td;
@@ -301,11 +302,22 @@ __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, const
   cswap(d1, r1, d3, r3);
   cswap(d1, r1, d2, r2);
   if (d0 == kMiss) return trav_pop(stk, tr);
-  // push the farther hits (farthest first), continue with the nearest
+  // push the farther hits (farthest first), continue with the nearest.  The
+  // hits are a sorted prefix, so with room for three entries every candidate
+  // is written and the top only advances past hits (no branches).
   int sp = tr.sp;
-  if (d3 != kMiss) stk.put(sp++, r3);
-  if (d2 != kMiss) stk.put(sp++, r2);
-  if (d1 != kMiss) stk.put(sp++, r1);
+  if (sp + 3 <= PT_STACK) {
+    stk.lds[sp * PT_BLOCK] = r3;
+    sp += d3 != kMiss;
+    stk.lds[sp * PT_BLOCK] = r2;
+    sp += d2 != kMiss;
+    stk.lds[sp * PT_BLOCK] = r1;
+    sp += d1 != kMiss;
+  } else {
+    if (d3 != kMiss) stk.put(sp++, r3);
+    if (d2 != kMiss) stk.put(sp++, r2);
+    if (d1 != kMiss) stk.put(sp++, r1);
+  }
   tr.sp = sp;
   tr.node = r0;
   return false;

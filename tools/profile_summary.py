@@ -17,7 +17,9 @@ import os
 import shutil
 import sys
 
-KERNEL = "render_kernel<false, false, false>"
+# render_kernel<STATS, DBG, BIN, ENV, GTAB>: the timed launch of each workload
+KERNELS = {"c5": "render_kernel<false, false, false, true, false>"}
+KERNEL = "render_kernel<false, false, false, false, false>"
 
 
 def _pmc(path):
@@ -31,7 +33,9 @@ def _pmc(path):
 
 
 def main():
+    global KERNEL
     workload, out = sys.argv[1], sys.argv[2]
+    KERNEL = KERNELS.get(workload, KERNEL)
     prof = sys.argv[3] if len(sys.argv) > 3 else "gpurun_out/prof"
     os.makedirs(out, exist_ok=True)
     ks = os.path.join(prof, "kt", "kt_kernel_stats.csv")
