@@ -11,11 +11,11 @@ reference's "Primary (M ray/s)" column); scene load / BVH build / upload are
 outside the timed region, as in the reference's timers.
 
 N > 1 (one process per GPU, torchrun): ranks render interleaved 32x32 tiles
-(tile_id mod N) into a zeroed device frame and the frames are summed onto rank 0
-with one RCCL reduce over xGMI (non-owners add +0.0, so the image is
+(tile_id mod N) into packed tile buffers (PT_FLAG_PACKED) that one RCCL gather
+over xGMI brings to rank 0, which scatters them into the frame (the image is
 bit-identical to the 1-GPU image).  The frame is fixed and split across the
 GPUs, so "scaling" is "strong"; value = all pixels*spp of the frame / max-rank
-time.  The reduce is inside the timed region.
+time.  The gather and the scatter are inside the timed region.
 """
 from __future__ import annotations
 
@@ -135,7 +135,8 @@ def main():
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--lbvh", action="store_true", help="build the BVH on the GPU (pt_upload_scene_lbvh)")
     ap.add_argument("--emulate-shard", type=int, default=0,
-                    help="diagnostic: render only rank 0's share of an N-GPU split on this one GPU")
+                    help="diagnostic: render only one rank's share of an N-GPU split on this one GPU")
+    ap.add_argument("--emulate-rank", type=int, default=0, help="the rank --emulate-shard renders")
     args = ap.parse_args()
     global W, H, SPP
     wl = WORKLOADS[args.workload]
@@ -144,7 +145,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from dsgpuraytracing_amd.dist import init_from_env, render_sharded, shard_tiles
+    from dsgpuraytracing_amd.dist import TileExchange, init_from_env, shard_tiles
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     rank, world, local = init_from_env("nccl")
@@ -180,35 +181,39 @@ def main():
 
     mine_arr = np.asarray(shard_tiles(tiles, rank, world), dtype=np.int32).reshape(-1, 4)
     if args.emulate_shard > 1:
-        mine_arr = np.asarray(shard_tiles(tiles, 0, args.emulate_shard), dtype=np.int32).reshape(-1, 4)
+        mine_arr = np.asarray(shard_tiles(tiles, args.emulate_rank, args.emulate_shard),
+                              dtype=np.int32).reshape(-1, 4)
+    ex = TileExchange(tiles, W, H, rank, world, frame.device) if world > 1 else None
+    if ex is not None:
+        mine_arr = np.asarray(ex.mine, dtype=np.int32).reshape(-1, 4)
 
-    def step(stats=False):  # render_sharded deals the same tiles to this rank every step
-        render_sharded(lambda mine: dev.render_tiles_device(mine_arr, frame.data_ptr(), stream, stats=stats),
-                       frame, tiles, rank, world)
-        return dev.stats()
+    def step(stats=False):
+        if ex is None:  # one GPU: the whole tile FIFO straight into the frame
+            dev.render_tiles_device(mine_arr, frame.data_ptr(), stream, stats=stats)
+        else:  # this rank's tiles into its packed buffer, then one gather onto rank 0
+            dev.render_tiles_device(mine_arr, ex.packed.data_ptr(), stream, stats=stats, packed=True)
+            ex.exchange(frame)
+        return dev.stats() if stats else None
 
     # counters for the roofline's algorithmic bytes: the reference's binary BVH
     # (SURVEY.md §8(d) cost model); and the launch's own counters (4-wide BVH)
     st_counts = step(stats="ref")
     st_perf = step(stats=True)
     for _ in range(args.warmup):
-        frame.zero_()
         step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms, resolve_ms = [], []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        if world > 1:
-            frame.zero_()  # the reduce sums whole frames: non-owned tiles must be +0.0
-        s = step()
-        kernel_ms.append(s["last_ms"])
-        resolve_ms.append(s["resolve_ms"])
+    for _ in range(args.steps):  # asynchronous: nothing waits on the GPU inside a step
+        step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # HIP events recorded around every launch on its stream (the timed ones)
+    kernel_ms, resolve_ms = dev.launch_times(args.steps)
+    s = dev.stats()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -139,7 +139,13 @@ void build_env_tables(const float* rgb, int w, int h, EnvTables& t) {
 struct pt_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  // launch timing: a ring of (render start, render end, resolve end) event
+  // triples so device renders need not synchronise (pt_get_launch_times)
+  static constexpr int kRing = 256;
+  hipEvent_t ev[kRing][3] = {};
+  int64_t n_launches = 0;   // launches recorded so far (ring slot = index % kRing)
+  bool times_pending = false;  // c->last's times belong to a launch not yet synchronised
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;  // the current launch's triple
   DevBuf<DNode> nodes;
   DevBuf<DNode2> nodes2;  // binary tree for PT_FLAG_REF_COUNTS
   DevBuf<int> prim_map;   // GPU-built BVH: sorted primitive -> uploaded index (else empty)
@@ -191,9 +197,8 @@ int pt_create(int device, pt_ctx** out) {
   pt_ctx* c = new pt_ctx();
   c->device = device;
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIPCHK(hipEventCreate(&c->ev0));
-  HIPCHK(hipEventCreate(&c->ev1));
-  HIPCHK(hipEventCreate(&c->ev2));
+  for (auto& tri : c->ev)
+    for (auto& e : tri) HIPCHK(hipEventCreate(&e));
   HIPCHK(c->counter.reserve(1));
   HIPCHK(c->stats.reserve(PT_STATS_SLOTS));
   hipDeviceProp_t prop;
@@ -236,9 +241,9 @@ int pt_destroy(pt_ctx* c) {
   c->stats.release();
   c->q_f.release();
   c->q_i.release();
-  if (c->ev0) (void)hipEventDestroy(c->ev0);
-  if (c->ev1) (void)hipEventDestroy(c->ev1);
-  if (c->ev2) (void)hipEventDestroy(c->ev2);
+  for (auto& tri : c->ev)
+    for (auto& e : tri)
+      if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return PT_OK;
@@ -712,6 +717,7 @@ static void screen_footprint(const pt_ctx* c, KParams& P) {
 static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStream_t s, uint32_t flags) {
   const bool stats = (flags & (PT_FLAG_STATS | PT_FLAG_REF_COUNTS)) != 0;
   std::memset(&c->last, 0, sizeof(c->last));
+  c->times_pending = false;
   if (tl.empty()) return PT_OK;
   // the tile list rarely changes between frames: upload it only when it does
   if (tl.size() != c->tiles_host.size() ||
@@ -764,6 +770,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.env_gphi = c->env_gphi.p;
   P.tiles = c->tiles.p;
   P.out = out_dev;
+  P.packed = (flags & PT_FLAG_PACKED) ? 1 : 0;
   P.work_counter = c->counter.p;
   P.stats = c->stats.p;
   P.dbg_pix = -1;
@@ -850,6 +857,13 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     HIPCHK(c->spill.reserve((size_t)(c->bvh_stack - PT_STACK) * grid * PT_BLOCK));
     P.stack_spill = c->spill.p;
   }
+  {
+    hipEvent_t* tri = c->ev[c->n_launches % pt_ctx::kRing];
+    c->ev0 = tri[0];
+    c->ev1 = tri[1];
+    c->ev2 = tri[2];
+    ++c->n_launches;
+  }
   HIPCHK(hipEventRecord(c->ev0, s));
   HIPCHK(ptk_launch_render(&P, grid, stats, (flags & PT_FLAG_REF_COUNTS) != 0, s));
   HIPCHK(hipEventRecord(c->ev1, s));
@@ -867,14 +881,30 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   return PT_OK;
 }
 
-static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags) {
-  HIPCHK(hipStreamSynchronize(s));
+// The last launch's kernel / resolve times (waits for its events).
+static int settle_times(pt_ctx* c) {
+  if (!c->times_pending) return PT_OK;
+  HIPCHK(hipEventSynchronize(c->ev2));
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   c->last.last_ms = ms;
   HIPCHK(hipEventElapsedTime(&ms, c->ev1, c->ev2));
   c->last.resolve_ms = ms;
-  if (flags & (PT_FLAG_STATS | PT_FLAG_REF_COUNTS)) {
+  c->times_pending = false;
+  return PT_OK;
+}
+
+// After a launch: counters (and times) of a stats launch now; a plain device
+// launch stays asynchronous, its times are read when asked for.
+static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags, bool sync) {
+  if (c->last.grid_blocks == 0) return PT_OK;  // nothing was launched
+  c->times_pending = true;
+  const bool counters = (flags & (PT_FLAG_STATS | PT_FLAG_REF_COUNTS)) != 0;
+  if (!sync && !counters) return PT_OK;
+  HIPCHK(hipStreamSynchronize(s));
+  int rc = settle_times(c);
+  if (rc) return rc;
+  if (counters) {
     unsigned long long v[PT_STATS_SLOTS] = {0};
     HIPCHK(hipMemcpy(v, c->stats.p, sizeof(v), hipMemcpyDeviceToHost));
     c->last.camera_rays = (int64_t)v[0];
@@ -927,6 +957,7 @@ int pt_render_tiles(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, float* hdr
   int rc = check_ready(c);
   if (rc) return rc;
   if (n_tiles < 0 || (n_tiles > 0 && (!tiles || !hdr_out_host))) return fail(PT_E_INVALID, "pt_render_tiles: bad args");
+  if (flags & PT_FLAG_PACKED) return fail(PT_E_INVALID, "pt_render_tiles: PT_FLAG_PACKED is for pt_render_tiles_device");
   HIPCHK(hipSetDevice(c->device));
   std::vector<int4> tl;
   if ((rc = build_tiles(c, tiles, n_tiles, tl))) return rc;
@@ -947,7 +978,7 @@ int pt_render_tiles(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, float* hdr
                               (size_t)t.z * 3 * sizeof(float), (size_t)t.w, hipMemcpyDeviceToHost, c->stream));
     }
   }
-  return finish_stats(c, c->stream, flags);
+  return finish_stats(c, c->stream, flags, true);
 }
 
 int pt_render_tiles_device(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, float* hdr_out_dev, void* stream,
@@ -959,9 +990,17 @@ int pt_render_tiles_device(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, flo
   HIPCHK(hipSetDevice(c->device));
   std::vector<int4> tl;
   if ((rc = build_tiles(c, tiles, n_tiles, tl))) return rc;
+  if (flags & PT_FLAG_PACKED) {  // tile i -> packed slot i: no clipping or splitting may renumber tiles
+    const int W = c->params.width, H = c->params.height;
+    for (int32_t i = 0; i < n_tiles; ++i) {
+      const pt_tile& t = tiles[i];
+      if (t.w < 1 || t.h < 1 || t.w > 32 || t.h > 32 || t.x < 0 || t.y < 0 || t.x + t.w > W || t.y + t.h > H)
+        return fail(PT_E_INVALID, "pt_render_tiles_device: PT_FLAG_PACKED needs tiles of 1..32 x 1..32 inside the frame");
+    }
+  }
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   if ((rc = launch(c, tl, hdr_out_dev, s, flags))) return rc;
-  return finish_stats(c, s, flags);
+  return finish_stats(c, s, flags, false);
 }
 
 int pt_intersect(pt_ctx* c, int64_t n, const double* o, const double* d, const double* max_t, int32_t* hit, float* t,
@@ -1007,7 +1046,29 @@ int pt_intersect(pt_ctx* c, int64_t n, const double* o, const double* d, const d
 
 int pt_get_stats(pt_ctx* c, pt_stats* out) {
   if (!c || !out) return fail(PT_E_INVALID, "pt_get_stats: NULL argument");
+  int rc = settle_times(c);
+  if (rc) return rc;
   *out = c->last;
+  return PT_OK;
+}
+
+int pt_get_launch_times(pt_ctx* c, float* kernel_ms, float* resolve_ms, int32_t cap, int32_t* n) {
+  if (!c || !n || cap < 0 || (cap > 0 && !kernel_ms)) return fail(PT_E_INVALID, "pt_get_launch_times: bad args");
+  int64_t k = std::min<int64_t>({(int64_t)cap, c->n_launches, (int64_t)pt_ctx::kRing});
+  *n = (int32_t)k;
+  if (k == 0) return PT_OK;
+  HIPCHK(hipSetDevice(c->device));
+  for (int64_t i = 0; i < k; ++i) {
+    hipEvent_t* tri = c->ev[(c->n_launches - k + i) % pt_ctx::kRing];
+    HIPCHK(hipEventSynchronize(tri[2]));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, tri[0], tri[1]));
+    kernel_ms[i] = ms;
+    if (resolve_ms) {
+      HIPCHK(hipEventElapsedTime(&ms, tri[1], tri[2]));
+      resolve_ms[i] = ms;
+    }
+  }
   return PT_OK;
 }
 

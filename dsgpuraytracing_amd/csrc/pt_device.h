@@ -117,7 +117,8 @@ struct KParams {
   const int* env_gtheta;     // guide table of env_ptheta (PT_ENV_GUIDE + 1 entries)
   const int* env_gphi;       // guide tables of the rows of env_pphi (h x (PT_ENV_GUIDE + 1))
   const int4* tiles;  // (x, y, w, h)
-  float* out;         // W*H*3
+  float* out;         // W*H*3, or n_tiles*1024*3 when packed
+  int packed;         // PT_FLAG_PACKED: tile i's pixel (x, y) -> out[3 * (i*1024 + (y-ty)*32 + (x-tx))]
   float* partial;     // W*H*n_groups*3: each sample group's sum, resolved into `out` in group order
   const int4* blocks;  // (x, y, w<=8, h<=8): footprint-clipped pixel blocks of the tiles
   int n_blocks;

@@ -1046,7 +1046,8 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
   const uint32_t tq = t / (uint32_t)k;  // pixel slot (k is a power of two: a shift)
   const int j = (int)(t & (uint32_t)(k - 1));
   const bool live = tq < (uint32_t)P.n_tiles * 1024u;
-  int2 xy = live ? tile_pixel(P.tiles[tq >> 10], tq & 1023u) : make_int2(-1, -1);
+  const int4 tile = live ? P.tiles[tq >> 10] : make_int4(0, 0, 0, 0);
+  int2 xy = live ? tile_pixel(tile, tq & 1023u) : make_int2(-1, -1);
   float3 acc = f3(0, 0, 0);
   if (xy.x >= 0 && !culled(P, xy.x, xy.y)) {
     const float* p = P.partial + 3 * ((size_t)xy.x + (size_t)xy.y * (size_t)P.W) * (size_t)P.n_groups;
@@ -1057,7 +1058,9 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
     acc = acc + f3(__shfl_xor(acc.x, off), __shfl_xor(acc.y, off), __shfl_xor(acc.z, off));
   if (xy.x < 0 || j != 0) return;
   const float inv_spp = (float)(1.0 / (double)P.spp);
-  store3(P.out + 3 * ((size_t)xy.x + (size_t)xy.y * (size_t)P.W), acc * inv_spp);
+  const size_t o = P.packed ? (size_t)(tq & ~1023u) + (size_t)((xy.y - tile.y) * 32 + (xy.x - tile.x))
+                            : (size_t)xy.x + (size_t)xy.y * (size_t)P.W;
+  store3(P.out + 3 * o, acc * inv_spp);
 }
 
 // Batched BVHAccel::intersect queries, one lane per ray.

@@ -5,39 +5,133 @@ independent and the scene is read-only, so the frame shards with no data-path
 collective:
   * every rank holds the whole scene (replicated, <= a few hundred MB);
   * the reference's 32x32 tile FIFO (pathtracer.cpp:209-214) is dealt
-    round-robin, tile_id mod world_size (interleaving balances the empty
-    margins of the default Cornell-box framing);
-  * each rank renders its tiles into a zero-initialised full frame on its GPU;
-  * ONE exchange at the end: a sum-reduce of the frames onto rank 0 (RCCL over
-    xGMI with the "nccl" backend; gloo on CPU for tests).  Non-owners add +0.0,
-    so the assembled image is bit-identical to the 1-GPU image: the counter RNG
-    keys every sample by (seed, pixel, sample), not by rank or schedule.
+    diagonally, (column + row) mod world_size: interleaving balances the empty
+    margins of the default Cornell-box framing, and unlike tile_id mod N it
+    does not deal whole tile columns when the row length is a multiple of N
+    (C3 on 8 GPUs: slowest rank 1.20x the mean with mod, 1.06x with diag,
+    tools/shard_balance.py);
+  * each rank renders its tiles into a PACKED buffer (PT_FLAG_PACKED: slot i
+    = its i-th tile, 32x32 row-major), padded to ceil(n_tiles / world) slots;
+  * ONE exchange at the end: a gather of the packed buffers onto rank 0 (RCCL
+    over xGMI with the "nccl" backend, gloo on CPU for tests) -- each rank
+    sends only its own tiles (1/world of the frame; 1.6 MB per rank at 1024^2
+    on 8 GPUs, all seven links into the root in parallel), not a whole frame --
+    then rank 0 scatters the tiles into the frame.  The counter RNG keys
+    every sample by (seed, pixel, sample), not by rank or schedule, so the
+    assembled image is bit-identical to the 1-GPU image.
 """
 from __future__ import annotations
 
 from typing import Callable, List, Sequence, Tuple
 
+import numpy as np
+
 Tile = Tuple[int, int, int, int]
+TILE = 32
 
 
-def shard_tiles(tiles: Sequence[Tile], rank: int, world: int) -> List[Tile]:
+def tile_owner(tile: Tile, index: int, world: int, deal: str = "mod") -> int:
+    """Rank that renders `tile` (FIFO position `index`).  "mod": tile_id mod
+    world; "diag": (column + row) mod world, so a rank's tiles also spread
+    over every column when the row length is a multiple of world (plain mod
+    then deals whole columns); "diag3": (column + 3*row) mod world."""
+    col, row = tile[0] // TILE, tile[1] // TILE
+    if deal == "mod":
+        return index % world
+    if deal == "diag":
+        return (col + row) % world
+    if deal == "diag3":
+        return (col + 3 * row) % world
+    raise ValueError(f"unknown tile deal {deal!r}")
+
+
+def shard_tiles(tiles: Sequence[Tile], rank: int, world: int, deal: str = "mod") -> List[Tile]:
     if world < 1 or not 0 <= rank < world:
         raise ValueError(f"bad rank/world {rank}/{world}")
-    return list(tiles[rank::world])
+    if deal == "mod":
+        return list(tiles[rank::world])
+    return [t for i, t in enumerate(tiles) if tile_owner(t, i, world, deal) == rank]
 
 
-def render_sharded(render_tiles: Callable[[List[Tile]], None], frame, tiles: Sequence[Tile], rank: int,
-                   world: int, dst: int = 0, group=None):
-    """Render this rank's share of `tiles` into `frame` (zeroed by the caller,
-    a torch tensor on this rank's device) and sum-reduce the frames onto `dst`.
-    `render_tiles(list_of_tiles)` writes those tiles' pixels into `frame`."""
-    import torch.distributed as dist
+def packed_index(tiles: Sequence[Tile], width: int, slot0: int = 0):
+    """(packed pixel index, frame pixel index) pairs of every pixel of `tiles`
+    in the PT_FLAG_PACKED layout (tile i -> slots [(slot0+i)*1024, +1024),
+    pixel (x, y) at (y-ty)*32 + (x-tx)); frame index x + y*width."""
+    src, dst = [], []
+    for i, (tx, ty, tw, th) in enumerate(tiles):
+        ly, lx = np.meshgrid(np.arange(th), np.arange(tw), indexing="ij")
+        src.append(((slot0 + i) * TILE * TILE + ly * TILE + lx).ravel())
+        dst.append(((ty + ly) * width + tx + lx).ravel())
+    if not src:
+        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+    return np.concatenate(src).astype(np.int64), np.concatenate(dst).astype(np.int64)
 
-    mine = shard_tiles(tiles, rank, world)
-    render_tiles(mine)
-    if world > 1:
-        dist.reduce(frame, dst=dst, group=group)
-    return frame
+
+class TileExchange:
+    """Packed-tile gather of a sharded frame onto `dst`.
+
+    `render_packed(mine, packed)` renders this rank's tiles `mine` into
+    `packed` (a (slots, 1024, 3) float32 tensor on this rank's device, slot i =
+    mine[i]); `exchange(frame)` gathers every rank's packed tiles onto `dst`
+    and writes them into `frame` ((H, W, 3) float32 on `dst`'s device).  The
+    index maps are built once: a frame's tile deal does not change between
+    steps."""
+
+    def __init__(self, tiles: Sequence[Tile], width: int, height: int, rank: int, world: int, device,
+                 dst: int = 0, group=None, deal: str = "diag"):
+        import torch
+
+        self.rank, self.world, self.dst, self.group = rank, world, dst, group
+        self.width, self.height = width, height
+        # the FIFO's edge tiles overhang the frame (raytrace_tile clamps them,
+        # pathtracer.cpp:594-595); packed slots hold the clamped tiles
+        tiles = [(x, y, min(w, width - x), min(h, height - y)) for (x, y, w, h) in tiles]
+        self.deal = deal
+        self.mine = shard_tiles(tiles, rank, world, deal)
+        self.slots = max(len(shard_tiles(tiles, r, world, deal)) for r in range(world))
+        self.packed = torch.zeros((max(self.slots, 1), TILE * TILE, 3), dtype=torch.float32, device=device)
+        self.recv = None
+        if rank == dst:
+            self.recv = torch.zeros((world, max(self.slots, 1), TILE * TILE, 3), dtype=torch.float32, device=device)
+            src, dstix = [], []
+            for r in range(world):
+                s, d = packed_index(shard_tiles(tiles, r, world, deal), width, slot0=r * max(self.slots, 1))
+                src.append(s)
+                dstix.append(d)
+            self.src = torch.from_numpy(np.concatenate(src)).to(device)
+            self.dstix = torch.from_numpy(np.concatenate(dstix)).to(device)
+
+    def gather(self):
+        """Every rank's packed tiles into `recv[rank]` on `dst` (one collective)."""
+        import torch.distributed as dist
+
+        if self.world > 1:
+            gl = list(self.recv.unbind(0)) if self.rank == self.dst else None
+            dist.gather(self.packed, gather_list=gl, dst=self.dst, group=self.group)
+        else:
+            self.recv[0].copy_(self.packed)
+
+    def scatter(self, frame):
+        """On `dst`: the gathered tiles into their frame pixels."""
+        if self.rank == self.dst:
+            frame.view(-1, 3).index_copy_(0, self.dstix, self.recv.view(-1, 3).index_select(0, self.src))
+        return frame
+
+    def exchange(self, frame):
+        self.gather()
+        return self.scatter(frame)
+
+
+def render_sharded(render_packed: Callable[[List[Tile], object], None], frame, tiles: Sequence[Tile], rank: int,
+                   world: int, dst: int = 0, group=None, exchange: TileExchange | None = None):
+    """Render this rank's share of `tiles` and assemble the frame on `dst`.
+    `render_packed(mine, packed)` writes tile mine[i]'s pixels into packed[i]
+    (PT_FLAG_PACKED layout).  Pass a TileExchange to reuse its buffers and
+    index maps across frames."""
+    h, w = frame.shape[0], frame.shape[1]
+    ex = exchange or TileExchange(tiles, w, h, rank, world, frame.device, dst=dst, group=group)
+    render_packed(ex.mine, ex.packed)
+    return ex.exchange(frame)
 
 
 def init_from_env(backend: str):

@@ -24,6 +24,7 @@ PT_E_IO = -5
 PT_LIGHT_ENVIRONMENT = 4
 PT_FLAG_STATS = 1
 PT_FLAG_REF_COUNTS = 2
+PT_FLAG_PACKED = 4
 
 PRIM_SPHERE, PRIM_TRIANGLE = 0, 1
 BSDF_DIFFUSE, BSDF_MIRROR, BSDF_REFRACTION, BSDF_GLASS, BSDF_EMISSION = range(5)
@@ -106,6 +107,7 @@ _SIGS = {
     "pt_intersect": (c_int32, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
     "pt_get_stats": (c_int32, [c_void_p, POINTER(pt_stats)]),
+    "pt_get_launch_times": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, POINTER(c_int32)]),
     "pt_get_wave_trace": (c_int32, [c_void_p, c_void_p, c_int64, POINTER(c_int64)]),
     "pt_last_error": (c_char_p, []),
     # include/ptgpu_scene.h (bound with full types in scene_loader.py)

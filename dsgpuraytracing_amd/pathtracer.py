@@ -94,9 +94,11 @@ class Device:
         flags = _flags(stats)
         check(self._lib.pt_render_tiles(self.handle, arr, len(keep), out.ctypes.data, flags))
 
-    def render_tiles_device(self, tiles, out_ptr: int, stream: int = 0, stats: bool = False):
+    def render_tiles_device(self, tiles, out_ptr: int, stream: int = 0, stats: bool = False, packed: bool = False):
+        """packed=True: out_ptr holds len(tiles)*32*32*3 floats, tile i's pixel
+        (x, y) at [(i*1024 + (y-ty)*32 + (x-tx))*3] (PT_FLAG_PACKED)."""
         keep, arr = self._tiles(tiles)
-        flags = _flags(stats)
+        flags = _flags(stats) | (native.PT_FLAG_PACKED if packed else 0)
         check(self._lib.pt_render_tiles_device(self.handle, arr, len(keep), ctypes.c_void_p(out_ptr),
                                                ctypes.c_void_p(stream or None), flags))
 
@@ -120,6 +122,16 @@ class Device:
         out["section_clocks"] = list(s.section_clocks)
         out["wave_span"] = list(s.wave_span)
         return out
+
+    def launch_times(self, n: int = 256):
+        """(kernel_ms, resolve_ms) arrays of the last <= n renders, oldest
+        first, from HIP events recorded around each launch on its stream
+        (pt_get_launch_times; waits for them)."""
+        k = np.zeros(n, np.float32)
+        r = np.zeros(n, np.float32)
+        got = ctypes.c_int32(0)
+        check(self._lib.pt_get_launch_times(self.handle, k.ctypes.data, r.ctypes.data, n, ctypes.byref(got)))
+        return k[:got.value].copy(), r[:got.value].copy()
 
     def wave_trace(self) -> np.ndarray:
         """Per-wave records of the last stats launch (pt_get_wave_trace):

@@ -195,6 +195,11 @@ typedef struct pt_stats {
 #define PT_FLAG_REF_COUNTS 2u /* as PT_FLAG_STATS, but traverse the reference's binary BVH so node_visits
                                  and primitive tests follow SURVEY.md §8(d)'s reference-layout cost model */
 
+#define PT_FLAG_PACKED 4u /* pt_render_tiles_device only: hdr_out_dev holds n_tiles*32*32*3 floats and
+                             tile i's pixel (x, y) goes to [(i*1024 + (y-tile.y)*32 + (x-tile.x))*3]
+                             (every tile 1..32 x 1..32 and inside the frame); the multi-GPU exchange
+                             gathers these packed tiles instead of whole frames */
+
 int pt_create(int device, pt_ctx** out);
 int pt_destroy(pt_ctx* ctx);
 int pt_upload_scene(pt_ctx* ctx, const pt_scene* scene);
@@ -211,7 +216,10 @@ int pt_render_tiles(pt_ctx* ctx, const pt_tile* tiles, int32_t n_tiles, float* h
                     uint32_t flags);
 /* Same, into a device framebuffer (width*height*3 floats) on `stream`
  * (hipStream_t, NULL = the context's stream).  Returns after the kernel is
- * queued; synchronise on the stream before reading. */
+ * queued, without waiting for it (a PT_FLAG_STATS / PT_FLAG_REF_COUNTS call
+ * waits, to read its counters); synchronise on the stream before reading.
+ * Replaces CUDAPathTracer::startRayTracingPT (cuda_src/setup.cu:815-827)
+ * minus its host copy-back. */
 int pt_render_tiles_device(pt_ctx* ctx, const pt_tile* tiles, int32_t n_tiles, float* hdr_out_dev,
                            void* stream, uint32_t flags);
 /* Batched BVHAccel::intersect.  Rays: origin o[3n], direction d[3n] (normalised),
@@ -219,7 +227,13 @@ int pt_render_tiles_device(pt_ctx* ctx, const pt_tile* tiles, int32_t n_tiles, f
  * t, primitive index (BVH order), and the any-hit flag within (0, max_t). */
 int pt_intersect(pt_ctx* ctx, int64_t n, const double* o, const double* d, const double* max_t,
                  int32_t* hit, float* t, int32_t* prim, int32_t* any_hit);
+/* Statistics of the last render (waits for its kernel-time events). */
 int pt_get_stats(pt_ctx* ctx, pt_stats* out);
+/* Kernel and resolve times in ms of the last min(cap, launches, 256) renders,
+ * oldest first (waits for them); *n = how many were written.  resolve_ms may
+ * be NULL.  No reference counterpart (its timers are host wall-clock,
+ * application.cpp:776-780): the HIP-event view of the same launches. */
+int pt_get_launch_times(pt_ctx* ctx, float* kernel_ms, float* resolve_ms, int32_t cap, int32_t* n);
 /* Diagnostics (no reference counterpart): after a PT_FLAG_STATS launch, one
  * record of 9 int64 per wave -- device wall-clock start, first time the wave
  * found the work queue empty (~0 if never), end, (XCC id << 32 | HW_ID), the

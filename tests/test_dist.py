@@ -1,4 +1,4 @@
-"""Multi-process tile sharding + framebuffer reduce (gloo, CPU): the assembled
+"""Multi-process tile sharding + packed-tile gather (gloo, CPU): the assembled
 image must be bit-identical to a single-process render for any world size.
 The per-rank renderer here is the oracle restatement in counter-RNG mode (the
 HIP path uses the same RNG keys; tests/test_gpu_render.py checks HIP tiles
@@ -15,7 +15,7 @@ import torch.multiprocessing as mp
 from dsgpuraytracing_amd.dist import render_sharded, shard_tiles
 from dsgpuraytracing_amd.pathtracer import tile_fifo
 
-W = H = 96
+W, H = 96, 80  # ragged last tile row
 SPP = 2
 
 
@@ -37,11 +37,12 @@ def _worker(rank, world, port, out_path):
     frame = torch.zeros((H, W, 3), dtype=torch.float32)
     ntx = (W + 31) // 32
 
-    def render(tiles):
-        for (x, y, _, _) in tiles:
+    def render(tiles, packed):  # the PT_FLAG_PACKED layout: tile i at packed[i], 32 px per row
+        for i, (x, y, tw, th) in enumerate(tiles):
             idx = (y // 32) * ntx + x // 32
             img, _ = rs.render(scene, W, H, SPP, rng_mode=1, tile_begin=idx, tile_end=idx + 1)
-            frame.add_(torch.from_numpy(img))
+            slot = packed[i].view(32, 32, 3)
+            slot[:th, :tw] = torch.from_numpy(img[y:y + th, x:x + tw])
 
     render_sharded(render, frame, tile_fifo(W, H), rank, world)
     if rank == 0:
@@ -60,13 +61,25 @@ def test_sharded_render_bit_identical(tmp_path, restate, world):
     assert np.array_equal(got, ref)
 
 
-def test_shard_tiles_partition():
+@pytest.mark.parametrize("deal", ["mod", "diag", "diag3"])
+def test_shard_tiles_partition(deal):
     tiles = tile_fifo(1920, 1080)
     for world in (1, 2, 4, 8):
-        shards = [shard_tiles(tiles, r, world) for r in range(world)]
+        shards = [shard_tiles(tiles, r, world, deal) for r in range(world)]
         flat = sorted(t for s in shards for t in s)
         assert flat == sorted(tiles)
         sizes = [len(s) for s in shards]
-        assert max(sizes) - min(sizes) <= 1
+        assert max(sizes) - min(sizes) <= (1 if deal == "mod" else 34)  # diag: <= one tile per row
     with pytest.raises(ValueError):
         shard_tiles(tiles, 2, 2)
+
+
+def test_packed_index_layout():
+    from dsgpuraytracing_amd.dist import packed_index
+    tiles = [(0, 0, 32, 32), (32, 64, 8, 16)]
+    src, dst = packed_index(tiles, 40)
+    assert len(src) == 32 * 32 + 8 * 16
+    # tile 1's pixel (33, 65) -> slot 1, local (1, 1)
+    k = int(np.nonzero(dst == 65 * 40 + 33)[0][0])
+    assert src[k] == 1024 + 1 * 32 + 1
+    assert len(set(dst.tolist())) == len(dst)
