@@ -785,6 +785,11 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     int v = std::atoi(lw);
     if (v >= 1) P.leaf_weight = v;
   }
+  P.drain_div = 0;
+  if (const char* dd = std::getenv("PT_DRAIN_DIV")) {  // tuning knob
+    int v = std::atoi(dd);
+    if (v >= 0 && v <= 64) P.drain_div = v;
+  }
   if (const char* sb = std::getenv("PT_SHADE_BATCH")) {  // tuning knob
     int v = std::atoi(sb);
     if (v >= 1 && v <= 64) P.shade_batch = v;

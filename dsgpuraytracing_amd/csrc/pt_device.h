@@ -128,6 +128,7 @@ struct KParams {
   int dbg_pix;                // diagnostic printf trace of one pixel (-1: off)
   int shade_batch;            // leave the traversal phase once this many lanes finished their ray
   int leaf_weight;            // leaf steps run when leaf_weight * leaf lanes >= 16 * node lanes
+  int drain_div;              // queue drained: shade once alive/drain_div lanes are ready (0: 3/4 rule)
   float root_lo[3], root_hi[3];  // scene bounds (root box, rounded outward)
   int cull_x0, cull_y0, cull_x1, cull_y1;  // pixels outside [x0,x1]x[y0,y1] see no geometry
 };

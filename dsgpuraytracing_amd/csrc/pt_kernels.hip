@@ -497,6 +497,10 @@ __device__ __forceinline__ void env_sample(const KParams& P, float r1, float r2,
   wi = f3(-st * sp, ct, st * cp);
 }
 
+#ifndef PT_DRAIN_NO_ATOMIC
+#define PT_DRAIN_NO_ATOMIC 1
+#endif
+
 // Lane modes of the persistent kernel.
 enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 
@@ -835,12 +839,21 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         uint32_t avail = chunk_end - chunk_next;
         uint32_t nbase = 0, csize = 0;
         if (cnt > avail) {
-          const uint32_t left = seen < total_slots ? total_slots - seen : 0u;
-          csize = min((uint32_t)PT_CHUNK_MAX, max((uint32_t)PT_CHUNK, left / (PT_CHUNK_DIV * gridDim.x))) & ~63u;
-          if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
-          nbase = __shfl(nbase, 0);
-          seen = nbase + csize;
-          if (STATS) n_atomics += lane == 0;
+          if (PT_DRAIN_NO_ATOMIC && seen >= total_slots) {
+            // This wave already saw the queue drained: every further claim
+            // would fail.  No atomic -- in the drain, one per wave per round
+            // on the single queue head (memory-side, serialised, slower from
+            // the XCDs far from its channel) stalled every round of the
+            // remaining paths (C3: the XCDs' median drain 380 vs 680 us).
+            nbase = total_slots;
+          } else {
+            const uint32_t left = total_slots - seen;
+            csize = min((uint32_t)PT_CHUNK_MAX, max((uint32_t)PT_CHUNK, left / (PT_CHUNK_DIV * gridDim.x))) & ~63u;
+            if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
+            nbase = __shfl(nbase, 0);
+            seen = nbase + csize;
+            if (STATS) n_atomics += lane == 0;
+          }
         }
         if (need) {
           uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
@@ -870,6 +883,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if (cnt > avail) {  // wave-uniform
           chunk_next = nbase + (cnt - avail);
           chunk_end = nbase + csize;
+          if (csize == 0) chunk_next = chunk_end = total_slots;  // drained: nothing left to hand out
         } else {
           chunk_next += cnt;
         }
@@ -918,7 +932,9 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     // lanes still working are ready, not when `batch` of 64 are, or the tail
     // would wait for the slowest ray of the wave at every bounce.
     const int alive = __popcll(__ballot(mode != M_DONE));
-    const int round_batch = min(batch, (3 * alive + 3) / 4);
+    int round_batch = min(batch, (3 * alive + 3) / 4);
+    if (P.drain_div > 0 && seen >= total_slots)  // the queue is drained: latency, not throughput
+      round_batch = max(1, alive / P.drain_div);
     if (STATS) {
       n_rounds += lane == 0;
       unsigned long long t = clock64();

@@ -124,10 +124,14 @@ _lib = None
 
 
 def lib():
-    """Load libptgpu.so (once).  Raises NativeLibraryError if it is absent."""
-    global _lib
+    """Load libptgpu.so (once).  Raises NativeLibraryError if it is absent.
+    PT_LIB=<path> loads another build of the same library instead (A/B
+    experiments, tools/ab.sh); it is never a fallback."""
+    global _lib, LIB_PATH
     if _lib is not None:
         return _lib
+    if os.environ.get("PT_LIB"):
+        LIB_PATH = os.path.abspath(os.environ["PT_LIB"])
     if not os.path.exists(LIB_PATH):
         raise NativeLibraryError(
             f"{LIB_PATH} is missing: build it with `python -m dsgpuraytracing_amd.build` "

@@ -29,6 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--share", type=int, default=0, help="N: rank 0's share of an N-GPU split (packed output)")
     args = ap.parse_args()
     import torch
 
@@ -53,8 +54,14 @@ def main():
     tiles = np.asarray(tile_fifo(w, h), dtype=np.int32).reshape(-1, 4)
     frame = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda:0")
     stream = torch.cuda.current_stream().cuda_stream
+    out_ptr, packed = frame.data_ptr(), False
+    if args.share > 1:
+        from dsgpuraytracing_amd.dist import TileExchange
+        ex = TileExchange(tile_fifo(w, h), w, h, 0, args.share, frame.device)
+        tiles = np.asarray(ex.mine, np.int32)
+        out_ptr, packed = ex.packed.data_ptr(), True
     for _ in range(2):
-        dev.render_tiles_device(tiles, frame.data_ptr(), stream, stats=True)
+        dev.render_tiles_device(tiles, out_ptr, stream, stats=True, packed=packed)
     torch.cuda.synchronize()
     st = dev.stats()
     tr = dev.wave_trace()
