@@ -116,6 +116,15 @@ __device__ __forceinline__ Frame make_frame(float3 n) {
   return f;
 }
 
+// Materialises loaded values in VGPRs at this point (an empty asm that
+// "modifies" them): the loads must be issued before it and cannot be sunk
+// into later branches.
+// PT_LOAD_FENCE bit 0: node steps, bit 1: leaf steps.
+#ifndef PT_LOAD_FENCE
+#define PT_LOAD_FENCE 3
+#endif
+#define PT_FENCE4(v) asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w))
+
 struct RayState {
   float3 o, d;
   float tmax;
@@ -270,13 +279,17 @@ __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb) {
   ra = tr;
 }
 
-template <bool STATS>
+template <bool STATS, bool FENCE = (PT_LOAD_FENCE & 1) != 0>
 __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, const Stack& stk, Trav& tr,
                                           Counters& ct) {
   const float kRobust = PT_ROBUST;
   const DNode* nd = nodes + tr.node;
-  const float4 lx = nd->lox, hx = nd->hix, ly = nd->loy, hy = nd->hiy, lz = nd->loz, hz = nd->hiz;
-  const int4 rf = nd->ref;
+  float4 lx = nd->lox, hx = nd->hix, ly = nd->loy, hy = nd->hiy, lz = nd->loz, hz = nd->hiz;
+  int4 rf = nd->ref;
+  if (FENCE) {  // all seven loads issued before the first wait (see leaf_step)
+    PT_FENCE4(hz);
+    PT_FENCE4(rf);
+  }
   if (STATS) ct.nodes++;
   const float3 o = tr.o, inv = tr.inv;
   const float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
@@ -373,8 +386,16 @@ __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const
   const int n = leaf_count(tr.node);
   const bool two = n >= 2;
   const int pb = two ? pa + 1 : pa;
-  const float4 a0 = prims[pa].v0, a1 = prims[pa].e1, a2 = prims[pa].e2;
-  const float4 b0 = prims[pb].v0, b1 = prims[pb].e1, b2 = prims[pb].e2;
+  float4 a0 = prims[pa].v0, a1 = prims[pa].e1, a2 = prims[pa].e2;
+  float4 b0 = prims[pb].v0, b1 = prims[pb].e1, b2 = prims[pb].e2;
+  // One memory round trip per leaf step: without the fence the compiler sinks
+  // the first primitive's e2 load into the triangle branch (a second
+  // dependent L2 trip).  The fence makes the last-issued loads' values live
+  // here, so every load is issued before the one wait.
+  if (PT_LOAD_FENCE & 2) {
+    PT_FENCE4(a2);
+    PT_FENCE4(b2);
+  }
   if (prim_test<STATS>(a0, a1, a2, pa, tr, ct)) return true;
   if (two && prim_test<STATS>(b0, b1, b2, pb, tr, ct)) return true;
   if (n > 2) {
@@ -963,7 +984,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       } else {
         if (trav && !at_leaf) {
           if constexpr (BIN) done = node_step2<STATS>(P.nodes2, stk, tr, ct);
-          else done = node_step<STATS>(P.nodes, stk, tr, ct);
+          // (the ENV build spills registers with the node fence: without)
+          else done = node_step<STATS, (PT_LOAD_FENCE & 1) != 0 && !ENV>(P.nodes, stk, tr, ct);
         }
       }
       if (done) mode = M_SHADE;
