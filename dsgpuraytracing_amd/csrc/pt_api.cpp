@@ -199,7 +199,7 @@ int pt_create(int device, pt_ctx** out) {
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   for (auto& tri : c->ev)
     for (auto& e : tri) HIPCHK(hipEventCreate(&e));
-  HIPCHK(c->counter.reserve(1));
+  HIPCHK(c->counter.reserve(PT_QUEUE_WORDS));  // work-queue heads, one 128-B line each
   HIPCHK(c->stats.reserve(PT_STATS_SLOTS));
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, device));
@@ -727,7 +727,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     HIPCHK(hipMemcpyAsync(c->tiles.p, tl.data(), tl.size() * sizeof(int4), hipMemcpyHostToDevice, s));
     c->tiles_host = tl;
   }
-  HIPCHK(hipMemsetAsync(c->counter.p, 0, sizeof(uint32_t), s));
+  HIPCHK(hipMemsetAsync(c->counter.p, 0, PT_QUEUE_WORDS * sizeof(uint32_t), s));
   if (stats) {
     unsigned long long init[PT_STATS_SLOTS] = {0};
     init[21] = init[23] = init[25] = ~0ull;  // atomicMin slots

@@ -17,6 +17,11 @@
 #define PT_CHUNK_DIV 8u  // a claim is ~1/(PT_CHUNK_DIV * waves) of the slots still unclaimed
 #endif
 static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand");
+#ifndef PT_XCD_QUEUES
+#define PT_XCD_QUEUES 1  // work queues (8: one per XCD, banded; measured slower on C3)
+#endif
+#define PT_QUEUE_WORDS (32 * 8)  // queue heads 128 B apart (room for 8)
+static_assert(PT_XCD_QUEUES >= 1 && PT_XCD_QUEUES <= 8, "at most 8 queues");
 #ifndef PT_GROUP_SPP
 #define PT_GROUP_SPP 2  // default samples per work slot
 #endif

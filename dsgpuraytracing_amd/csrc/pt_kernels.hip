@@ -124,6 +124,9 @@ __device__ __forceinline__ Frame make_frame(float3 n) {
 #define PT_LOAD_FENCE 3
 #endif
 #define PT_FENCE4(v) asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w))
+#ifndef PT_HIT_FENCE
+#define PT_HIT_FENCE 1
+#endif
 
 struct RayState {
   float3 o, d;
@@ -598,6 +601,10 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   uint32_t n_atomics = 0;              // work-queue atomics (lane 0)
   uint32_t chunk_next = 0, chunk_end = 0;  // the wave's private range of work slots
   uint32_t seen = 0;                       // queue head after this wave's last claim
+#if PT_XCD_QUEUES > 1
+  // the wave's current queue (its XCD's first) and how many it found exhausted
+  uint32_t qcur = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) % PT_XCD_QUEUES, qtried = 0;
+#endif
   unsigned long long cyc_shade = 0, cyc_trav = 0;  // shader clocks per phase (lane 0)
   unsigned long long cyc_hitshade = 0;              // of which: shading before the refill
   unsigned long long cyc_sec[4] = {0, 0, 0, 0};     // of which: hit record, NEE, bounce, refill fetch
@@ -626,6 +633,11 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     return (size_t)p * n_groups + (uint32_t)((s_next - 1) / P.group_spp);
   };
   const uint32_t total_slots = (uint32_t)P.n_blocks * 64u * n_groups;
+  // first slot of queue part q (part PT_XCD_QUEUES ends at total_slots)
+  auto q_start = [&](uint32_t q) -> uint32_t {
+    return (uint32_t)(((uint64_t)total_slots * q) / PT_XCD_QUEUES);
+  };
+  (void)q_start;
   const int batch = P.shade_batch;
 
   for (;;) {
@@ -649,11 +661,21 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         // are rebuilt from the primitive (barycentrics / sphere reprojection),
         // not o + t*d, so their error is relative to the primitive and the
         // 256-ulp origin offset always clears the surface.
-        const DPrim pr = P.prims[tr.prim];
+        DPrim pr = P.prims[tr.prim];
+#if PT_HIT_FENCE
+        // the whole record and the vertex normals in one memory round trip
+        // (unfenced, the e1/e2 and normal loads wait behind the meta branch)
+        float nnv[9];
+        for (int k = 0; k < 9; ++k) nnv[k] = P.norms[9 * (size_t)tr.prim + k];
+        PT_FENCE4(pr.e2);
+        asm volatile("" : "+v"(nnv[8]));
+        const float* nn = nnv;
+#else
+        const float* nn = P.norms + 9 * (size_t)tr.prim;
+#endif
         const int meta = __float_as_int(pr.v0.w);  // (bsdf << 1) | is_triangle
         bsdf = meta >> 1;
         if (meta & 1) {
-          const float* nn = P.norms + 9 * (size_t)tr.prim;
           float3 V0 = f3(pr.v0.x, pr.v0.y, pr.v0.z), E1 = f3(pr.e1.x, pr.e1.y, pr.e1.z), E2 = f3(pr.e2.x, pr.e2.y, pr.e2.z);
           float hu, hv, ht;
           mt_terms(tr.o, tr.d, V0, E1, E2, hu, hv, ht);  // the barycentrics of the traversal test
@@ -859,6 +881,62 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         uint32_t cnt = (uint32_t)__popcll(m);
         uint32_t avail = chunk_end - chunk_next;
         uint32_t nbase = 0, csize = 0;
+#if PT_XCD_QUEUES > 1
+        // Per-XCD queues: the slot range is split into PT_XCD_QUEUES
+        // contiguous parts (horizontal bands of the footprint), and a wave
+        // claims from the part of its own XCD first, so each XCD's L2 holds
+        // the geometry its band sees; an exhausted part sends the wave to the
+        // next one (stealing), and the wave retires once all were exhausted.
+        uint32_t limit = chunk_end;  // first slot past the chunk handed out now
+        if (cnt > avail) {
+          if (qtried >= PT_XCD_QUEUES) {
+            nbase = limit = total_slots;
+          } else {
+            const uint32_t q_lo = q_start(qcur), q_hi = q_start(qcur + 1);
+            csize = PT_CHUNK;
+            uint32_t old = 0;
+            if (lane == 0) old = atomicAdd(P.work_counter + 32 * qcur, csize);
+            old = __builtin_amdgcn_readfirstlane(__shfl(old, 0));  // wave-uniform: an SGPR
+            if (STATS) n_atomics += lane == 0;
+            nbase = q_lo + min(old, q_hi - q_lo);
+            limit = q_lo + min(old + csize, q_hi - q_lo);
+            if (old + csize >= q_hi - q_lo) {  // this part is exhausted after this chunk
+              qcur = qcur + 1 == PT_XCD_QUEUES ? 0u : qcur + 1;
+              ++qtried;
+            }
+          }
+        }
+        if (need) {
+          uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+          uint32_t slot = rank < avail ? chunk_next + rank : nbase + (rank - avail);
+          if (rank >= avail && slot >= limit) {
+            // nothing for this lane in this claim: it retries from the next
+            // part, or retires when every part was exhausted
+            if (qtried >= PT_XCD_QUEUES) {
+              mode = M_DONE;
+              if (STATS && w_empty == 0ull) w_empty = wall_clock64();
+            }
+          } else {
+            uint32_t bq = slot / n_groups;
+            uint32_t g = slot - bq * n_groups;
+            int4 b = P.blocks[bq >> 6];
+            int qx = (int)(bq & 7u), qy = (int)((bq >> 3) & 7u);
+            if (qx < b.z && qy < b.w) {
+              pix = b.x + qx + (b.y + qy) * P.W;
+              sample = (int)g * P.group_spp;
+              acc = f3(0, 0, 0);
+              if (STATS) slot_t0 = wall_clock64();
+              mode = M_CAMERA;
+            }
+          }
+        }
+        if (cnt > avail) {  // wave-uniform
+          chunk_next = min(nbase + (cnt - avail), limit);
+          chunk_end = limit;
+        } else {
+          chunk_next += cnt;
+        }
+#else
         if (cnt > avail) {
           if (PT_DRAIN_NO_ATOMIC && seen >= total_slots) {
             // This wave already saw the queue drained: every further claim
@@ -871,7 +949,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             const uint32_t left = total_slots - seen;
             csize = min((uint32_t)PT_CHUNK_MAX, max((uint32_t)PT_CHUNK, left / (PT_CHUNK_DIV * gridDim.x))) & ~63u;
             if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
-            nbase = __shfl(nbase, 0);
+            nbase = __builtin_amdgcn_readfirstlane(__shfl(nbase, 0));  // wave-uniform: an SGPR
             seen = nbase + csize;
             if (STATS) n_atomics += lane == 0;
           }
@@ -908,6 +986,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         } else {
           chunk_next += cnt;
         }
+#endif
       }
       PT_STAMP(3);
       // ---- camera rays: Camera::generate_ray (camera.cpp:113-129) at the
