@@ -272,7 +272,8 @@ def main():
             "launch_counters": {k: st_perf[k] for k in ("node_visits", "tri_tests", "sphere_tests", "wave_trav_steps",
                                                         "leaf_steps", "wave_rounds", "queue_atomics", "shade_clocks",
                                                         "hitshade_clocks", "trav_clocks", "max_wave_clocks",
-                                                        "wave_wall_sum", "wave_wall_max", "section_clocks", "wave_span")},
+                                                        "wave_wall_sum", "wave_wall_max", "section_clocks", "wave_span",
+                                                        "lane_iters")},
             "launch": {"grid_blocks": s["grid_blocks"], "block": 64, "blocks_per_cu_query": s["blocks_per_cu"],
                        "bvh_nodes": s["bvh_nodes"], "bvh_stack": s["bvh_stack"]},
             "image_mean": float(img.mean()),

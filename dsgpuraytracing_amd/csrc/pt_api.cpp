@@ -931,6 +931,7 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags, bool sync) {
     c->last.wave_wall_max = (int64_t)v[15];
     c->last.hitshade_clocks = (int64_t)v[16];
     for (int k = 0; k < 4; ++k) c->last.section_clocks[k] = (int64_t)v[17 + k];
+    for (int k = 0; k < 4; ++k) c->last.lane_iters[k] = (int64_t)v[27 + k];
     for (int k = 0; k < 3; ++k) c->last.wave_span[k] = (int64_t)(v[22 + k] - v[21]);
     for (int k = 0; k < 2; ++k) c->last.wave_span[3 + k] = v[25 + k] ? (int64_t)(v[25 + k] - v[21]) : -1;
     c->last.counters_valid = 1;

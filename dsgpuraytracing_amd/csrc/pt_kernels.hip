@@ -298,6 +298,8 @@ __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, const
   const float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
   const float kMiss = 3.0e38f;
   float d[4];
+  // (v_pk_fma_f32 over the SoA child pairs measured -2%: the broadcast
+  // operand pairs cost registers and moves)
   const float* LX = &lx.x; const float* HX = &hx.x; const float* LY = &ly.x;
   const float* HY = &hy.x; const float* LZ = &lz.x; const float* HZ = &hz.x;
 #pragma unroll
@@ -598,6 +600,9 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   uint32_t n_cam = 0, n_bounce = 0, n_shadow = 0, n_hits = 0;
   uint32_t n_titer = 0, n_rounds = 0;  // wave-level traversal steps / shading rounds (lane 0)
   uint32_t n_leafit = 0;               // of the traversal steps: leaf steps
+  // traversal lane-iterations: at the other step kind, finished and waiting
+  // for the shading round, retired, stepping a leaf
+  uint32_t l_other = 0, l_ready = 0, l_dead = 0, l_leaf = 0;
   uint32_t n_atomics = 0;              // work-queue atomics (lane 0)
   uint32_t chunk_next = 0, chunk_end = 0;  // the wave's private range of work slots
   uint32_t seen = 0;                       // queue head after this wave's last claim
@@ -1057,6 +1062,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         r_steps += stepped;
         r_idle += !stepped;
       }
+      if (STATS) {  // what each lane does in this iteration (SIMD efficiency)
+        l_other += trav && leaf_iter != at_leaf;
+        l_ready += mode == M_SHADE;
+        l_dead += mode == M_DONE;
+        l_leaf += at_leaf && leaf_iter;
+      }
       if (leaf_iter) {
         if (at_leaf) done = leaf_step<STATS>(P.prims, stk, tr, ct);
         if (STATS) n_leafit += lane == 0;
@@ -1092,6 +1103,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       unsigned long long s = v[k];
       for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
       if (lane == 0) atomicAdd(P.stats + k, s);
+    }
+    const uint32_t li[4] = {l_other, l_ready, l_dead, l_leaf};
+    for (int k = 0; k < 4; ++k) {
+      unsigned long long s = li[k];
+      for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
+      if (lane == 0) atomicAdd(P.stats + 27 + k, s);
     }
     // load balance: the slowest wave bounds the launch
     w_empty = w_empty ? w_empty : ~0ull;

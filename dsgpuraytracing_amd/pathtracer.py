@@ -121,6 +121,7 @@ class Device:
         out = {k: getattr(s, k) for k, _ in native.pt_stats._fields_}
         out["section_clocks"] = list(s.section_clocks)
         out["wave_span"] = list(s.wave_span)
+        out["lane_iters"] = list(s.lane_iters)
         return out
 
     def launch_times(self, n: int = 256):

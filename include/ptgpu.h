@@ -189,6 +189,9 @@ typedef struct pt_stats {
                               first wave end, last wave end, first and last time a wave found
                               the work queue empty (launch ramp, queue drain and tail) */
   int32_t group_spp;       /* samples per work slot (pixel, sample group) of the last launch */
+  int64_t lane_iters[4];   /* traversal lane-iterations (64 per wave iteration) spent at the other
+                              step kind, finished and waiting for the shading round, retired
+                              (queue drained), stepping a leaf; node steps = node_visits */
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */
