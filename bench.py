@@ -146,9 +146,14 @@ def main():
     import torch.distributed as dist
 
     from dsgpuraytracing_amd.dist import TileExchange, init_from_env, shard_tiles
+    # PT_DIST_BACKEND=gloo + PT_BENCH_DEVICE=0: rehearsal of the N-rank flow
+    # with every rank on one GPU (the exchange then stages through host memory)
+    backend = os.environ.get("PT_DIST_BACKEND", "nccl")
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("PT_BENCH_DEVICE") is not None:
+        local = int(os.environ["PT_BENCH_DEVICE"])
     torch.cuda.set_device(local)
-    rank, world, local = init_from_env("nccl")
+    rank, world, _ = init_from_env(backend)
 
     from dsgpuraytracing_amd import scenes
     from dsgpuraytracing_amd.pathtracer import Device, Scene, tile_fifo
@@ -215,7 +220,7 @@ def main():
     kernel_ms, resolve_ms = dev.launch_times(args.steps)
     s = dev.stats()
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

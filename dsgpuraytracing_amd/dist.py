@@ -103,9 +103,17 @@ class TileExchange:
 
     def gather(self):
         """Every rank's packed tiles into `recv[rank]` on `dst` (one collective)."""
+        import torch
         import torch.distributed as dist
 
-        if self.world > 1:
+        if self.world > 1 and self.packed.is_cuda and dist.get_backend(self.group) == "gloo":
+            # gloo gathers host tensors only (tests / one-GPU rehearsals)
+            src = self.packed.cpu()
+            gl = [torch.empty_like(src) for _ in range(self.world)] if self.rank == self.dst else None
+            dist.gather(src, gather_list=gl, dst=self.dst, group=self.group)
+            if self.rank == self.dst:
+                self.recv.copy_(torch.stack(gl))
+        elif self.world > 1:
             gl = list(self.recv.unbind(0)) if self.rank == self.dst else None
             dist.gather(self.packed, gather_list=gl, dst=self.dst, group=self.group)
         else:
