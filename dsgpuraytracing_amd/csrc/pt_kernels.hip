@@ -282,35 +282,11 @@ __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb) {
   ra = tr;
 }
 
-template <bool STATS, bool FENCE = (PT_LOAD_FENCE & 1) != 0>
-__device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, const Stack& stk, Trav& tr,
-                                          Counters& ct) {
-  const float kRobust = PT_ROBUST;
-  const DNode* nd = nodes + tr.node;
-  float4 lx = nd->lox, hx = nd->hix, ly = nd->loy, hy = nd->hiy, lz = nd->loz, hz = nd->hiz;
-  int4 rf = nd->ref;
-  if (FENCE) {  // all seven loads issued before the first wait (see leaf_step)
-    PT_FENCE4(hz);
-    PT_FENCE4(rf);
-  }
-  if (STATS) ct.nodes++;
-  const float3 o = tr.o, inv = tr.inv;
-  const float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+// Second half of a node step: entry distances d (kMiss = not entered) and
+// references rf of the four children -> continue with the nearest, push the
+// other hits farthest first.
+__device__ __forceinline__ bool node_order(const Stack& stk, Trav& tr, const float* d, const int4 rf) {
   const float kMiss = 3.0e38f;
-  float d[4];
-  // (v_pk_fma_f32 over the SoA child pairs measured -2%: the broadcast
-  // operand pairs cost registers and moves)
-  const float* LX = &lx.x; const float* HX = &hx.x; const float* LY = &ly.x;
-  const float* HY = &hy.x; const float* LZ = &lz.x; const float* HZ = &hz.x;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    float ax = fmaf(LX[k], inv.x, -oi.x), bx = fmaf(HX[k], inv.x, -oi.x);
-    float ay = fmaf(LY[k], inv.y, -oi.y), by = fmaf(HY[k], inv.y, -oi.y);
-    float az = fmaf(LZ[k], inv.z, -oi.z), bz = fmaf(HZ[k], inv.z, -oi.z);
-    float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
-    float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tr.tmax)) * kRobust;
-    d[k] = tn <= tf ? tn : kMiss;
-  }
   int r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
   float d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3];
   // near-first order: 5-exchange sorting network on the entry distances
@@ -339,6 +315,75 @@ __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, const
   tr.sp = sp;
   tr.node = r0;
   return false;
+}
+
+#ifndef PT_OCTANT
+#define PT_OCTANT 1
+#endif
+
+template <bool STATS, bool FENCE = (PT_LOAD_FENCE & 1) != 0, bool OCT = PT_OCTANT != 0>
+__device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, const Stack& stk, Trav& tr,
+                                          Counters& ct) {
+  const float kRobust = PT_ROBUST;
+  const float3 o = tr.o, inv = tr.inv;
+  const float kMiss = 3.0e38f;
+  float d[4];
+  if constexpr (OCT) {
+  // Near/far planes chosen by the ray's direction signs through the load
+  // addresses: for inv.x >= 0 the near x plane is lo (offset 0), else hi
+  // (offset 16).  The slab test then needs no per-child min/max pairs:
+  // tn = max(near planes, 0), tf = min(far planes, tmax).
+  {
+    const char* nb = (const char*)nodes;
+    const uint32_t base = (uint32_t)tr.node << 7;
+    const uint32_t sx = (__float_as_uint(inv.x) >> 27) & 16u, sy = (__float_as_uint(inv.y) >> 27) & 16u,
+                   sz = (__float_as_uint(inv.z) >> 27) & 16u;
+    float4 nx = *(const float4*)(nb + (base + sx)), fx = *(const float4*)(nb + (base + (sx ^ 16u)));
+    float4 ny = *(const float4*)(nb + (base + 32u + sy)), fy = *(const float4*)(nb + (base + 32u + (sy ^ 16u)));
+    float4 nz = *(const float4*)(nb + (base + 64u + sz)), fz = *(const float4*)(nb + (base + 64u + (sz ^ 16u)));
+    int4 rf = *(const int4*)(nb + (base + 96u));
+    if (FENCE) {
+      PT_FENCE4(fz);
+      PT_FENCE4(rf);
+    }
+    if (STATS) ct.nodes++;
+    const float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+    const float* NX = &nx.x; const float* FX = &fx.x; const float* NY = &ny.x;
+    const float* FY = &fy.x; const float* NZ = &nz.x; const float* FZ = &fz.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float tn = fmaxf(fmaxf(fmaf(NX[k], inv.x, -oi.x), fmaf(NY[k], inv.y, -oi.y)),
+                             fmaxf(fmaf(NZ[k], inv.z, -oi.z), 0.0f));
+      const float tf = fminf(fminf(fmaf(FX[k], inv.x, -oi.x), fmaf(FY[k], inv.y, -oi.y)),
+                             fminf(fmaf(FZ[k], inv.z, -oi.z), tr.tmax)) * kRobust;
+      d[k] = tn <= tf ? tn : kMiss;
+    }
+    return node_order(stk, tr, d, rf);
+  }
+  }
+  const DNode* nd = nodes + tr.node;
+  float4 lx = nd->lox, hx = nd->hix, ly = nd->loy, hy = nd->hiy, lz = nd->loz, hz = nd->hiz;
+  int4 rf = nd->ref;
+  if (FENCE) {  // all seven loads issued before the first wait (see leaf_step)
+    PT_FENCE4(hz);
+    PT_FENCE4(rf);
+  }
+  if (STATS) ct.nodes++;
+  const float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+  // (v_pk_fma_f32 over the SoA child pairs measured -2%: the broadcast
+  // operand pairs cost registers and moves)
+  const float* LX = &lx.x; const float* HX = &hx.x; const float* LY = &ly.x;
+  const float* HY = &hy.x; const float* LZ = &lz.x; const float* HZ = &hz.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float ax = fmaf(LX[k], inv.x, -oi.x), bx = fmaf(HX[k], inv.x, -oi.x);
+    float ay = fmaf(LY[k], inv.y, -oi.y), by = fmaf(HY[k], inv.y, -oi.y);
+    float az = fmaf(LZ[k], inv.z, -oi.z), bz = fmaf(HZ[k], inv.z, -oi.z);
+    float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
+    float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tr.tmax)) * kRobust;
+    d[k] = tn <= tf ? tn : kMiss;
+  }
+  return node_order(stk, tr, d, rf);
 }
 
 // Binary node step over the reference topology (reference-count launch).
@@ -1074,8 +1119,9 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       } else {
         if (trav && !at_leaf) {
           if constexpr (BIN) done = node_step2<STATS>(P.nodes2, stk, tr, ct);
-          // (the ENV build spills registers with the node fence: without)
-          else done = node_step<STATS, (PT_LOAD_FENCE & 1) != 0 && !ENV>(P.nodes, stk, tr, ct);
+          // (the ENV build spills registers with the node fence or the
+          // octant loads: without)
+          else done = node_step<STATS, (PT_LOAD_FENCE & 1) != 0 && !ENV, PT_OCTANT != 0 && !ENV>(P.nodes, stk, tr, ct);
         }
       }
       if (done) mode = M_SHADE;
