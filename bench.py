@@ -10,12 +10,17 @@ Mrays/s = W*H*spp*frames / seconds / 1e6 (primary path samples, the unit of the
 reference's "Primary (M ray/s)" column); scene load / BVH build / upload are
 outside the timed region, as in the reference's timers.
 
-N > 1 (one process per GPU, torchrun): ranks render interleaved 32x32 tiles
-(tile_id mod N) into packed tile buffers (PT_FLAG_PACKED) that one RCCL gather
-over xGMI brings to rank 0, which scatters them into the frame (the image is
-bit-identical to the 1-GPU image).  The frame is fixed and split across the
-GPUs, so "scaling" is "strong"; value = all pixels*spp of the frame / max-rank
-time.  The gather and the scatter are inside the timed region.
+N > 1 (one process per GPU, torchrun), default --scaling weak: the path
+partitions into independent (pixel, sample) units, and every GPU renders one
+64-spp pass of the whole C3 frame with its own sample range (rank r: sample
+indices 64r .. 64r+63, pt_params.sample_base), i.e. exactly the 1-GPU
+workload; one RCCL sum-reduce over xGMI assembles the 64N-spp image on rank 0
+(the framebuffer exchange of SURVEY.md §8(e)).  value = N * W*H*64 / max-rank
+time, "scaling": "weak".  --scaling strong splits ONE 64-spp frame instead:
+ranks render interleaved 32x32 tiles into packed tile buffers
+(PT_FLAG_PACKED) that one RCCL gather brings to rank 0 (bit-identical to the
+1-GPU image); value = W*H*64 / max-rank time.  The exchange is inside the
+timed region in both modes.
 """
 from __future__ import annotations
 
@@ -137,6 +142,9 @@ def main():
     ap.add_argument("--emulate-shard", type=int, default=0,
                     help="diagnostic: render only one rank's share of an N-GPU split on this one GPU")
     ap.add_argument("--emulate-rank", type=int, default=0, help="the rank --emulate-shard renders")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N > 1: weak = one 64-spp pass of the whole frame per GPU (sample split); "
+                         "strong = one frame's tiles split across the GPUs")
     args = ap.parse_args()
     global W, H, SPP
     wl = WORKLOADS[args.workload]
@@ -153,6 +161,11 @@ def main():
     if os.environ.get("PT_BENCH_DEVICE") is not None:
         local = int(os.environ["PT_BENCH_DEVICE"])
     torch.cuda.set_device(local)
+    # A dedicated current stream: renders are queued on it (pt_render_tiles_device
+    # would put a NULL stream on the context's own non-blocking stream), so torch
+    # ops and the RCCL collectives, which follow the current stream, see the
+    # finished frame.
+    torch.cuda.set_stream(torch.cuda.Stream(device=local))
     rank, world, _ = init_from_env(backend)
 
     from dsgpuraytracing_amd import scenes
@@ -177,24 +190,40 @@ def main():
     dev.upload_scene(scene, gpu_bvh=args.lbvh)
     t_up = time.perf_counter() - t_up
     dev.set_camera(scene.camera)
-    dev.set_params(W, H, SPP, DEPTH, NSL, SEED)
+    weak = world > 1 and args.scaling == "weak"
+    # weak: this rank's pass covers sample indices SPP*rank .. SPP*rank+SPP-1
+    dev.set_params(W, H, SPP, DEPTH, NSL, SEED, sample_base=SPP * rank if weak else 0)
     t_load = time.perf_counter() - t_load
 
     tiles = tile_fifo(W, H)
     frame = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{local}")
     stream = torch.cuda.current_stream().cuda_stream
 
-    mine_arr = np.asarray(shard_tiles(tiles, rank, world), dtype=np.int32).reshape(-1, 4)
+    # strong: this rank's share of the tiles; weak (and one GPU): every tile
+    mine_arr = np.asarray(tiles if weak else shard_tiles(tiles, rank, world), dtype=np.int32).reshape(-1, 4)
     if args.emulate_shard > 1:
         mine_arr = np.asarray(shard_tiles(tiles, args.emulate_rank, args.emulate_shard),
                               dtype=np.int32).reshape(-1, 4)
-    ex = TileExchange(tiles, W, H, rank, world, frame.device) if world > 1 else None
+    ex = TileExchange(tiles, W, H, rank, world, frame.device) if world > 1 and not weak else None
     if ex is not None:
         mine_arr = np.asarray(ex.mine, dtype=np.int32).reshape(-1, 4)
 
+    def reduce_passes():  # weak: sum the N passes onto rank 0, mean over 64N samples
+        if backend == "gloo":  # host staging (one-GPU rehearsals)
+            h = frame.cpu()
+            dist.reduce(h, dst=0)
+            if rank == 0:
+                frame.copy_(h)
+        else:
+            dist.reduce(frame, dst=0)
+        if rank == 0:
+            frame.mul_(1.0 / world)
+
     def step(stats=False):
-        if ex is None:  # one GPU: the whole tile FIFO straight into the frame
+        if ex is None:  # the whole tile FIFO straight into the frame (one GPU, or this rank's pass)
             dev.render_tiles_device(mine_arr, frame.data_ptr(), stream, stats=stats)
+            if weak:
+                reduce_passes()
         else:  # this rank's tiles into its packed buffer, then one gather onto rank 0
             dev.render_tiles_device(mine_arr, ex.packed.data_ptr(), stream, stats=stats, packed=True)
             ex.exchange(frame)
@@ -234,7 +263,7 @@ def main():
         host_ms = (time.perf_counter() - t0h) / 2 * 1e3
     if rank == 0:
         frames = args.steps
-        value = W * H * SPP * frames / elapsed / 1e6
+        value = W * H * SPP * frames * (world if weak else 1) / elapsed / 1e6
         if args.emulate_shard > 1:
             value = float(np.sum(mine_arr[:, 2] * mine_arr[:, 3])) * SPP * frames / elapsed / 1e6
         bytes_launch = algorithmic_bytes(st_counts)
@@ -251,7 +280,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / frames * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "fp32",
             "data": {"c5": "synthetic: deterministic CBbunny_sub2 glass/mirror proxy for the missing CBlucy.dae + "
@@ -261,7 +290,8 @@ def main():
                            "synthetic: deterministic CBbunny_sub1 proxy for the missing CBdragon.dae (SURVEY §8(d))"),
             "config": {"workload": wl["desc"] + ", default camera",
                        "width": W, "height": H, "spp": SPP, "max_ray_depth": DEPTH, "ns_area_light": NSL,
-                       "parallelism": f"tiles{world}" if world > 1 else "single",
+                       "spp_total": SPP * world if weak else SPP,
+                       "parallelism": (f"samples{world}" if weak else f"tiles{world}") if world > 1 else "single",
                        "render_time_s": round(elapsed / frames, 4), "scene_load_s": round(t_load, 3),
                        "bvh": "gpu-lbvh" if args.lbvh else "reference-sah (host)",
                        "upload_s": round(t_up, 4),

@@ -751,6 +751,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.max_depth = c->params.max_depth;
   P.ns_area = c->params.ns_area_light;
   P.seed = c->params.seed;
+  P.sample_base = c->params.sample_base;
   P.n_lights = c->n_lights;
   P.n_bsdfs = c->n_bsdfs;
   P.n_tiles = (int)tl.size();

@@ -103,6 +103,7 @@ struct KParams {
   int W, H, spp, max_depth, ns_area;
   float inv_w, inv_h;  // 1/W, 1/H
   uint32_t seed;
+  uint32_t sample_base;  // first sample index of the pass (RNG keys)
   int n_lights;
   int n_bsdfs;
   int n_tiles;     // 32x32 (or smaller) tiles: 1024 pixels each

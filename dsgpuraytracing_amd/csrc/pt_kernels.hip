@@ -1042,7 +1042,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       // ---- camera rays: Camera::generate_ray (camera.cpp:113-129) at the
       // jittered pixel position of raytrace_pixel (pathtracer.cpp:571-575)
       while (mode == M_CAMERA) {
-        rbase = ptrng::stream_base(P.seed, (uint32_t)pix, (uint32_t)sample);
+        rbase = ptrng::stream_base(P.seed, (uint32_t)pix, (uint32_t)sample + P.sample_base);
         rdim = 0;
         const int py = pix / P.W, px = pix - py * P.W;
         float ry = ptrng::draw(rbase, rdim++);  // UniformGridSampler2D draws y first

@@ -75,7 +75,9 @@ class TileExchange:
     mine[i]); `exchange(frame)` gathers every rank's packed tiles onto `dst`
     and writes them into `frame` ((H, W, 3) float32 on `dst`'s device).  The
     index maps are built once: a frame's tile deal does not change between
-    steps."""
+    steps.  The render must be queued on torch's current stream (a non-zero
+    torch.cuda.Stream, see bench.py): the collective is ordered after the
+    current stream's work, not after the pt_ctx's own stream."""
 
     def __init__(self, tiles: Sequence[Tile], width: int, height: int, rank: int, world: int, device,
                  dst: int = 0, group=None, deal: str = "diag"):

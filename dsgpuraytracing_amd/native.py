@@ -73,7 +73,7 @@ class pt_scene(ctypes.Structure):
 
 class pt_params(ctypes.Structure):
     _fields_ = [("width", c_int32), ("height", c_int32), ("spp", c_int32), ("max_depth", c_int32),
-                ("ns_area_light", c_int32), ("seed", c_uint32)]
+                ("ns_area_light", c_int32), ("seed", c_uint32), ("sample_base", c_uint32)]
 
 
 class pt_tile(ctypes.Structure):

@@ -73,9 +73,10 @@ class Device:
     def set_camera(self, cam: native.pt_camera):
         check(self._lib.pt_set_camera(self.handle, ctypes.byref(cam)))
 
-    def set_params(self, width, height, spp, max_depth, ns_area_light, seed):
+    def set_params(self, width, height, spp, max_depth, ns_area_light, seed, sample_base=0):
+        """sample_base: first sample index of this pass (pt_params.sample_base)."""
         p = native.pt_params(width=width, height=height, spp=spp, max_depth=max_depth,
-                             ns_area_light=ns_area_light, seed=seed & 0xFFFFFFFF)
+                             ns_area_light=ns_area_light, seed=seed & 0xFFFFFFFF, sample_base=sample_base)
         check(self._lib.pt_set_params(self.handle, ctypes.byref(p)))
 
     @staticmethod

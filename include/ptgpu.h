@@ -149,6 +149,9 @@ typedef struct pt_params {
   int32_t max_depth;     /* max_ray_depth */
   int32_t ns_area_light; /* ns_area_light */
   uint32_t seed;         /* counter-RNG key: (seed, pixel, sample) */
+  uint32_t sample_base;  /* first sample index of this pass: samples sample_base .. sample_base+spp-1
+                            are rendered and averaged (0 = the reference's single pass; progressive
+                            passes / the multi-GPU sample split use disjoint ranges) */
 } pt_params;
 
 typedef struct pt_tile {

@@ -56,5 +56,5 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(native.pt_light) == 4 + 12 + 4 * 24 + 4 + 4  # trailing padding to 8
     assert ctypes.sizeof(native.pt_camera) == 15 * 8
     assert ctypes.sizeof(native.pt_bvh_node) == 6 * 8 + 4 * 8
-    assert ctypes.sizeof(native.pt_params) == 24
+    assert ctypes.sizeof(native.pt_params) == 28  # + sample_base
     assert ctypes.sizeof(native.pt_tile) == 16
