@@ -12,6 +12,10 @@
 //   * srand + start_raytracing + wait for DONE        (src/main.cpp:75,170-181)
 // Modes:
 //   render : writes the HDR sampleBuffer (float32 W*H*3, y=0 bottom) to a PTDUMP
+//   tiles  : times PathTracer::raytrace_tile (pathtracer.cpp:585-611) on every
+//            --tile-stride-th 32x32 tile of the FIFO from --tile-begin, on this
+//            one thread (the -t 1 worker's work, glibc rand() as shipped) — the
+//            CPU baseline of bench.py on a bounded sample of a frame
 //   dump   : writes the flattened scene the GPU seam would receive (PTDUMP)
 //   rays   : answers BVHAccel::intersect nearest/any-hit queries (KATs)
 //   rng    : prints the first rand() draws and the sampler draw order
@@ -58,6 +62,7 @@ struct Opts {
   string scene, mode = "render", out, cam, rays_in, envmap, in;
   int half = 0;
   size_t w = 64, h = 64, spp = 1, depth = 4, lights = 1, threads = 1;
+  size_t tile_begin = 0, tile_stride = 1;
   unsigned seed = 1;
 };
 
@@ -429,6 +434,8 @@ int main(int argc, char** argv) {
     else if (a == "--envmap") o.envmap = nxt();
     else if (a == "--in") o.in = nxt();
     else if (a == "--half") o.half = std::stoi(nxt());
+    else if (a == "--tile-begin") o.tile_begin = std::stoul(nxt());
+    else if (a == "--tile-stride") o.tile_stride = std::max<size_t>(1, std::stoul(nxt()));
     else o.scene = a;
   }
   if (o.mode == "rng") {
@@ -462,6 +469,29 @@ int main(int argc, char** argv) {
   }
   if (o.mode == "rays") {
     answer_rays(o, *pt);
+    return 0;
+  }
+  if (o.mode == "tiles") {
+    // the per-frame state start_raytracing sets up (pathtracer.cpp:192-207),
+    // without its worker threads
+    pt->continueRaytracing = true;
+    pt->sampleBuffer.clear();
+    pt->frameBuffer.clear();
+    pt->num_tiles_w = pt->sampleBuffer.w / 32 + 1;
+    pt->num_tiles_h = pt->sampleBuffer.h / 32 + 1;
+    pt->tile_samples.assign(pt->num_tiles_w * pt->num_tiles_h, 0);
+    const size_t ntx = (o.w + 31) / 32, nt = ntx * ((o.h + 31) / 32);
+    size_t px = 0, n = 0;
+    std::srand(o.seed);
+    auto t0 = std::chrono::steady_clock::now();
+    for (size_t i = o.tile_begin; i < nt; i += o.tile_stride) {
+      const size_t tx = (i % ntx) * 32, ty = (i / ntx) * 32;
+      pt->raytrace_tile((int)tx, (int)ty, 32, 32);
+      px += (std::min(o.w, tx + 32) - tx) * (std::min(o.h, ty + 32) - ty);
+      ++n;
+    }
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("{\"render_s\": %.6f, \"pixels\": %zu, \"tiles\": %zu, \"spp\": %zu}\n", secs, px, n, o.spp);
     return 0;
   }
   // render (main.cpp:170-181 with srand moved next to the render)
