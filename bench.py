@@ -3,24 +3,26 @@
 
 Metric (BASELINE.json): "Mrays/sec + wall-clock render time, CBdragon 1024x1024
 @ 64 spp".  A "step" is one full-frame render (every 32x32 tile of the
-reference's FIFO) of the C3 workload: 1024x1024, 64 spp, max_ray_depth 4,
-ns_area_light 1 (readme.txt:1 settings) on the CBdragon proxy CBbunny_sub1
-(114,316 triangles; CBdragon.dae is absent).
-Mrays/s = W*H*spp*frames / seconds / 1e6 (primary path samples, the unit of the
-reference's "Primary (M ray/s)" column); scene load / BVH build / upload are
-outside the timed region, as in the reference's timers.
+reference's FIFO) of a BASELINE config with max_ray_depth 4, ns_area_light 1
+(readme.txt:1 settings).  Mrays/s = W*H*spp*frames / seconds / 1e6 (primary
+path samples, the unit of the reference's "Primary (M ray/s)" column); scene
+load / BVH build / upload are outside the timed region, as in the reference's
+timers.  Samples whose camera ray provably misses the scene box (screen
+footprint cull, exact) count as rendered, as in the reference's own unit; the
+line also reports ray casts/s and a framed variant in which every pixel sees
+the scene.
 
-N > 1 (one process per GPU, torchrun), default --scaling weak: the path
-partitions into independent (pixel, sample) units, and every GPU renders one
-64-spp pass of the whole C3 frame with its own sample range (rank r: sample
-indices 64r .. 64r+63, pt_params.sample_base), i.e. exactly the 1-GPU
-workload; one RCCL sum-reduce over xGMI assembles the 64N-spp image on rank 0
-(the framebuffer exchange of SURVEY.md §8(e)).  value = N * W*H*64 / max-rank
-time, "scaling": "weak".  --scaling strong splits ONE 64-spp frame instead:
-ranks render interleaved 32x32 tiles into packed tile buffers
-(PT_FLAG_PACKED) that one RCCL gather brings to rank 0 (bit-identical to the
-1-GPU image); value = W*H*64 / max-rank time.  The exchange is inside the
-timed region in both modes.
+  * N = 1 (default): C3 = CBdragon proxy CBbunny_sub1 (114,316 triangles;
+    CBdragon.dae is absent), 1024x1024, 64 spp.
+  * N > 1 (torchrun, one process per GPU), default: BASELINE C4 = the same
+    scene at 1920x1080, 256 spp, ONE frame's 32x32 tiles dealt diagonally
+    over the GPUs, each rank rendering its tiles into a packed buffer, then
+    ONE RCCL gather of the packed tiles onto rank 0 (SURVEY.md §8(e));
+    value = W*H*256 / max-rank time ("scaling": "strong"), the image is
+    bit-identical to the 1-GPU image.  --scaling weak (opt-in) renders one
+    64-spp pass of the whole frame per GPU over disjoint sample ranges plus
+    one RCCL sum-reduce.
+The exchange is inside the timed region.
 """
 from __future__ import annotations
 
@@ -35,64 +37,130 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
-# BASELINE.json configs; C3 is the headline (default).
+# BASELINE.json configs; C3 is the headline (N = 1 default),
+# C4 the multi-GPU default.  c3f: C3 with a camera framing the box interior.
 WORKLOADS = {
     "c1": dict(scene="c1", w=256, h=256, spp=1, desc="C1 CBspheres_lambertian 256x256 1spp -m 4 -l 1"),
     "c2": dict(scene="c1", w=512, h=512, spp=16, desc="C2 CBspheres_lambertian 512x512 16spp -m 4 -l 1"),
     "c3": dict(scene="sub1", w=1024, h=1024, spp=64,
-               desc="C3 CBbunny_sub1 (114,316 tris; CBdragon proxy) 1024x1024 64spp -m 4 -l 1"),
+               desc="C3 CBbunny_sub1 (114,316 tris; CBdragon proxy) 1024x1024 64spp -m 4 -l 1, default camera"),
+    "c3f": dict(scene="sub1", w=1024, h=1024, spp=64, cam="cam_bunny_framed.info",
+                desc="C3 CBbunny_sub1 1024x1024 64spp -m 4 -l 1, camera framing the box interior "
+                     "(assets/cam_bunny_framed.info: no pixel misses the scene)"),
     "c4": dict(scene="sub1", w=1920, h=1080, spp=256,
-               desc="C4 CBbunny_sub1 (CBdragon proxy) 1920x1080 256spp -m 4 -l 1, tiles over N GPUs"),
+               desc="C4 CBbunny_sub1 (CBdragon proxy) 1920x1080 256spp -m 4 -l 1, default camera, tiles over N GPUs"),
     "c5": dict(scene="c5", w=1920, h=1080, spp=512,
                desc="C5 CBbunny_sub2_c5 (457,228 tris, glass bunny + mirror sphere; CBlucy proxy) + synthetic "
                     "512x256 environment light, 1920x1080 512spp -m 4 -l 1, tiles over N GPUs"),
 }
+HEADLINE_METRIC = "Mrays/sec + wall-clock render time, CBdragon 1024x1024 @ 64 spp"
 W, H, SPP, DEPTH, NSL, SEED = 1024, 1024, 64, 4, 1, 1
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec; L2 34.5 TB/s aggregate (8 XCDs);
+# VALU: each SIMD issues one wave64 VALU instruction per 2 cycles -> 2 per CU
+# per cycle, 256 CUs at 2.4 GHz.
+HBM_PEAK_GBS = 8000.0
+L2_PEAK_GBS = 34500.0
+VALU_PEAK_GINST = 256 * 2 * 2.4
+L2_LINE = 128
+
+
+def workload_scene(wl):
+    from dsgpuraytracing_amd import scenes
+    if wl["scene"] == "sub1":
+        dae, envmap = scenes.proxy_path(1), None
+    elif wl["scene"] == "c5":
+        dae, envmap = scenes.c5_path(2), scenes.c5_envmap_path()
+    else:
+        dae, envmap = scenes.C1_DAE, None
+    cam = os.path.join(ROOT, "assets", wl["cam"]) if wl.get("cam") else None
+    return dae, envmap, cam
 
 
 def algorithmic_bytes(st: dict) -> float:
     """SURVEY.md §8(d) reference-layout cost model: 64 B per BVH node visit,
     48 B per triangle test, 16 B per sphere test, 4 B per leaf primitive index,
-    36 B per hit (vertex normals), 12 B per pixel written."""
+    36 B per hit (vertex normals), 12 B per pixel written.  The counts are
+    those of the reference's binary BVH (PT_FLAG_REF_COUNTS launch).  The scene
+    is L2 / Infinity-Cache resident, so these bytes are CACHE-SERVED: they are
+    priced against the L2 roof, never against HBM."""
     prim = st["tri_tests"] + st["sphere_tests"]
     return (64.0 * st["node_visits"] + 48.0 * st["tri_tests"] + 16.0 * st["sphere_tests"] + 4.0 * prim
             + 36.0 * st["ext_hits"] + 12.0 * st["pixels"])
 
 
-def measured_traffic(workload: str):
-    """HBM bytes per launch of the render kernel on this workload, from the
-    rocprofv3 PMC passes committed under profiles/ (tools/profile_summary.py:
-    FETCH_SIZE doubled per the gfx950 correction of MI355X_MICROARCH.md §HBM,
-    + WRITE_SIZE; KB -> bytes).  None when no summary for this workload is
-    committed."""
-    p = os.path.join(ROOT, "profiles", "latest_traffic.json")
-    try:
-        with open(p) as f:
-            d = json.load(f)
-        return d.get("hbm_bytes_per_launch") if d.get("workload") == workload else None
-    except (OSError, ValueError):
-        return None
+def profile_summary(workload: str):
+    """PMC summary of the render kernel on this workload (tools/profile_summary.py
+    -> profiles/<round>/<workload>_summary.json; the newest round wins)."""
+    pdir = os.path.join(ROOT, "profiles")
+    rounds = sorted((d for d in os.listdir(pdir) if d.startswith("r") and d[1:].isdigit()),
+                    key=lambda d: int(d[1:]), reverse=True) if os.path.isdir(pdir) else []
+    for r in rounds:
+        p = os.path.join(pdir, r, f"{workload}_summary.json")
+        if os.path.exists(p):
+            with open(p) as f:
+                d = json.load(f)
+            d["source"] = os.path.relpath(p, ROOT)
+            return d
+    return None
 
 
-def measured_pmc(workload: str):
-    """Issue/latency view of the render kernel from the committed PMC summary
-    (informational: the kernel is latency- and issue-bound, not HBM-bound)."""
-    try:
-        with open(os.path.join(ROOT, "profiles", "latest_traffic.json")) as f:
-            src = json.load(f)["source"]
-        with open(os.path.join(ROOT, src)) as f:
-            d = json.load(f)
-        if d.get("workload") != workload:
-            return None
-        keys = ("avg_ms", "hbm_gbs", "l2_hit_rate", "valu_issue_util", "sq_wait_any_frac", "sq_wait_inst_any_frac",
-                "sq_active_inst_any_frac")
-        return {k: (round(d[k], 4) if isinstance(d.get(k), float) else d.get(k)) for k in keys} | {"source": src}
-    except (OSError, ValueError, KeyError):
-        return None
+def roofline(workload: str, kernel_ms: float, alg_bytes: float) -> dict:
+    """Roofline of the dominant kernel (render_kernel).  Per-launch counts come
+    from the committed PMC summary of the same workload (they are a property
+    of the workload, not of the clock); rates divide them by the kernel time
+    measured live in this run (HIP events on the launch stream).  Views:
+      hbm   -- (2 x FETCH_SIZE + WRITE_SIZE) bytes (gfx950 correction,
+               MI355X_MICROARCH.md §HBM) vs 8 TB/s;
+      l2    -- (TCC_HIT + TCC_MISS) requests x 128 B vs 34.5 TB/s (an upper
+               bound of the bytes the L2 served);
+      valu  -- SQ_INSTS_VALU wave-instructions vs 2 per CU per cycle;
+      algorithmic -- the §8(d) cost-model bytes, cache-served, vs the L2 roof.
+    `bound` names the measured view with the highest fraction; the kernel is
+    latency-bound below all of them (SQ_WAIT_ANY, see pmc)."""
+    t = kernel_ms * 1e-3
+    pm = profile_summary(workload)
+    views = {"algorithmic_cache_served": {
+        "bytes_per_launch": alg_bytes, "achieved": round(alg_bytes / t / 1e9, 1), "peak": L2_PEAK_GBS,
+        "unit": "GB/s", "frac": round(alg_bytes / t / 1e9 / L2_PEAK_GBS, 4)}}
+    hbm_bytes = None
+    if pm:
+        if "hbm_bytes_per_launch" in pm:
+            hbm_bytes = pm["hbm_bytes_per_launch"]
+            a = hbm_bytes / t / 1e9
+            views["hbm"] = {"bytes_per_launch": hbm_bytes, "achieved": round(a, 1), "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": round(a / HBM_PEAK_GBS, 4)}
+        tcc = pm.get("tcc", {})
+        if "TCC_HIT_sum" in tcc and "TCC_MISS_sum" in tcc:
+            b = (tcc["TCC_HIT_sum"] + tcc["TCC_MISS_sum"]) * L2_LINE
+            a = b / t / 1e9
+            views["l2"] = {"bytes_per_launch": b, "achieved": round(a, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(a / L2_PEAK_GBS, 4), "hit_rate": round(pm.get("l2_hit_rate", 0.0), 4)}
+        sq = pm.get("sq", {})
+        if "SQ_INSTS_VALU" in sq:
+            a = sq["SQ_INSTS_VALU"] / t / 1e9
+            views["valu"] = {"insts_per_launch": sq["SQ_INSTS_VALU"], "achieved": round(a, 1),
+                             "peak": VALU_PEAK_GINST, "unit": "G wave-instructions/s",
+                             "frac": round(a / VALU_PEAK_GINST, 4)}
+    measured = [k for k in ("hbm", "l2", "valu") if k in views]
+    bound = max(measured, key=lambda k: views[k]["frac"]) if measured else "algorithmic_cache_served"
+    v = views[bound]
+    out = {"bound": bound, "achieved": v["achieved"], "peak": v["peak"], "unit": v["unit"], "frac": v["frac"],
+           "traffic": hbm_bytes, "kernel_ms": round(kernel_ms, 4), "views": views}
+    if pm:
+        out["pmc"] = {k: (round(pm[k], 4) if isinstance(pm.get(k), float) else pm.get(k))
+                      for k in ("avg_ms", "sq_wait_any_frac", "sq_wait_inst_any_frac", "sq_active_inst_any_frac",
+                                "valu_issue_util", "l2_hit_rate", "source")}
+    return out
 
 
 REF_DRIVER = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+
+
+def _coprime(k, ntx):
+    import math
+    while k > 1 and math.gcd(k, ntx) != 1:  # strides sharing a factor with the row length sample columns
+        k += 1
+    return k
 
 
 def cpu_baseline_reference(dae: str, envmap, budget_s: float = 15.0) -> dict:
@@ -104,16 +172,10 @@ def cpu_baseline_reference(dae: str, envmap, budget_s: float = 15.0) -> dict:
     lock makes it anti-scale with threads), k sized from a calibration run so
     the sample takes about budget_s.  Scene load and BVH build are excluded,
     as in the reference's own timer."""
-    import math
     import subprocess
 
     ntx = (W + 31) // 32
     ntiles = ntx * ((H + 31) // 32)
-
-    def coprime(k):  # strides sharing a factor with the row length sample columns, not the frame
-        while k > 1 and math.gcd(k, ntx) != 1:
-            k += 1
-        return k
 
     def run(begin, stride):
         cmd = [REF_DRIVER, dae, "--mode", "tiles", "-w", str(W), "-h", str(H), "-s", str(SPP), "-m", str(DEPTH),
@@ -123,10 +185,10 @@ def cpu_baseline_reference(dae: str, envmap, budget_s: float = 15.0) -> dict:
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True, timeout=600, check=True)
         return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
 
-    cal = coprime(max(1, ntiles // 12))
+    cal = _coprime(max(1, ntiles // 12), ntx)
     c = run(cal // 2, cal)
     per_tile = max(c["render_s"], 1e-4) / max(1, c["tiles"])
-    step = coprime(max(1, int(round(ntiles * per_tile / budget_s))))
+    step = _coprime(max(1, int(round(ntiles * per_tile / budget_s))), ntx)
     m = run(step // 2, step)
     return {"value": m["pixels"] * SPP / m["render_s"] / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "reference",
             "sample": f"every {step}th 32x32 tile of the {W}x{H} frame ({m['pixels']} px, uniform) at {SPP} spp, "
@@ -135,42 +197,51 @@ def cpu_baseline_reference(dae: str, envmap, budget_s: float = 15.0) -> dict:
                       f"{m['render_s']:.1f} s of rendering"}
 
 
-def cpu_baseline(scene_dump: str, budget_s: float = 12.0) -> dict:
-    """Reference CPU algorithm (oracle/restate.cpp, bit-identical to the
-    reference binary at -t 1: glibc rand, one thread) timed on this host on a
-    bounded, UNIFORM sample of the same workload: every k-th tile of the 32x32
-    tile FIFO at the full spp, k sized from a 16-tile calibration so the sample
-    takes about budget_s (scene load excluded)."""
+def _tiles_px(begin, stride):
+    ntx = (W + 31) // 32
+    ntiles = ntx * ((H + 31) // 32)
+    px = 0
+    for ti in range(begin, ntiles, stride):
+        tx, ty = (ti % ntx) * 32, (ti // ntx) * 32
+        px += (min(W, tx + 32) - tx) * (min(H, ty + 32) - ty)
+    return px
+
+
+def cpu_baseline_port(scene_dump: str, budget_s: float = 12.0, rng_mode: int = 0, threads: int = 1) -> dict:
+    """The reference CPU algorithm as restated in oracle/restate.cpp, timed on
+    this host on a bounded, UNIFORM sample of the same workload: every k-th
+    tile of the 32x32 tile FIFO at the full spp, k sized from a calibration
+    run so the sample takes about budget_s (scene load excluded).
+      rng_mode 0, 1 thread: glibc rand(), bit-identical to the reference at -t 1;
+      rng_mode 1, T threads: the counter RNG (no shared rand() lock), the
+        "fair" CPU baseline of BASELINE.md §3 -- the same algorithm scaled
+        over the host cores the GPU job owns."""
     from tests.oracle_helpers import Restatement
     rs = Restatement()
     ntx = (W + 31) // 32
     ntiles = ntx * ((H + 31) // 32)
-
-    def tiles_px(begin, stride):
-        px = 0
-        for ti in range(begin, ntiles, stride):
-            tx, ty = (ti % ntx) * 32, (ti // ntx) * 32
-            px += (min(W, tx + 32) - tx) * (min(H, ty + 32) - ty)
-        return px
-
-    import math
-
-    def coprime(k):  # strides sharing a factor with the row length sample columns, not the frame
-        while k > 1 and math.gcd(k, ntx) != 1:
-            k += 1
-        return k
-
-    cal = coprime(max(1, ntiles // 16))
-    _, _, t_cal = rs.render_strided(scene_dump, W, H, SPP, DEPTH, NSL, SEED, rng_mode=0, tile_begin=cal // 2,
-                                    tile_stride=cal)
+    cal = _coprime(max(1, ntiles // 16), ntx)
+    _, _, t_cal = rs.render_strided(scene_dump, W, H, SPP, DEPTH, NSL, SEED, rng_mode=rng_mode, threads=threads,
+                                    tile_begin=cal // 2, tile_stride=cal)
     per_tile = max(t_cal, 1e-4) / len(range(cal // 2, ntiles, cal))
-    step = coprime(max(1, int(round(ntiles * per_tile / budget_s))))
-    _, _, secs = rs.render_strided(scene_dump, W, H, SPP, DEPTH, NSL, SEED, rng_mode=0, tile_begin=step // 2,
-                                   tile_stride=step)
-    px = tiles_px(step // 2, step)
-    return {"value": px * SPP / secs / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
+    step = _coprime(max(1, int(round(ntiles * per_tile / budget_s))), ntx)
+    _, _, secs = rs.render_strided(scene_dump, W, H, SPP, DEPTH, NSL, SEED, rng_mode=rng_mode, threads=threads,
+                                   tile_begin=step // 2, tile_stride=step)
+    px = _tiles_px(step // 2, step)
+    rng = "glibc-rand mode (== reference -t 1)" if rng_mode == 0 else "counter-RNG mode"
+    return {"value": px * SPP / secs / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"every {step}th 32x32 tile of the {W}x{H} frame ({px} px, uniform) at {SPP} spp, -m {DEPTH} "
-                      f"-l {NSL}, oracle/restate.cpp glibc-rand mode (== reference -t 1), {secs:.1f} s of rendering"}
+                      f"-l {NSL}, oracle/restate.cpp {rng}, {threads} thread(s), {secs:.1f} s of rendering"}
+
+
+def host_threads() -> int:
+    """Host threads this job may use: the affinity set, capped at 16 (the GPU
+    box's CPU share per GPU; os.cpu_count() there shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
 
 
 def main():
@@ -180,18 +251,18 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scene-dump", default=None, help="PTDUMP scene instead of the native .dae loader")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-extras", action="store_true",
+                    help="N = 1: skip the framed-C3 and single-GPU C4 companion measurements")
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                    help="default: c3 on one GPU, c4 (the BASELINE multi-GPU config) on N > 1")
     ap.add_argument("--lbvh", action="store_true", help="build the BVH on the GPU (pt_upload_scene_lbvh)")
     ap.add_argument("--emulate-shard", type=int, default=0,
                     help="diagnostic: render only one rank's share of an N-GPU split on this one GPU")
     ap.add_argument("--emulate-rank", type=int, default=0, help="the rank --emulate-shard renders")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="N > 1: weak = one 64-spp pass of the whole frame per GPU (sample split); "
-                         "strong = one frame's tiles split across the GPUs")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="N > 1: strong = one frame's tiles split across the GPUs + one RCCL gather (default); "
+                         "weak = one pass of the whole frame per GPU over disjoint sample ranges + one RCCL reduce")
     args = ap.parse_args()
-    global W, H, SPP
-    wl = WORKLOADS[args.workload]
-    W, H, SPP = wl["w"], wl["h"], wl["spp"]
 
     import torch
     import torch.distributed as dist
@@ -211,22 +282,21 @@ def main():
     torch.cuda.set_stream(torch.cuda.Stream(device=local))
     rank, world, _ = init_from_env(backend)
 
-    from dsgpuraytracing_amd import scenes
+    global W, H, SPP
+    workload = args.workload or ("c3" if world == 1 else "c4")
+    wl = WORKLOADS[workload]
+    W, H, SPP = wl["w"], wl["h"], wl["spp"]
+
     from dsgpuraytracing_amd.pathtracer import Device, Scene, tile_fifo
 
     t_load = time.perf_counter()
-    dae, envmap = None, None
+    dae, envmap, cam = None, None, None
     if args.scene_dump:
         scene = Scene.from_dump(args.scene_dump)
         dump_path = args.scene_dump
     else:
-        if wl["scene"] == "sub1":
-            dae = scenes.proxy_path(1)
-        elif wl["scene"] == "c5":
-            dae, envmap = scenes.c5_path(2), scenes.c5_envmap_path()
-        else:
-            dae = scenes.C1_DAE
-        scene = Scene.from_dae(dae, W, H, envmap=envmap)
+        dae, envmap, cam = workload_scene(wl)
+        scene = Scene.from_dae(dae, W, H, cam_info=cam, envmap=envmap)
         dump_path = None
     dev = Device(local)
     t_up = time.perf_counter()
@@ -245,13 +315,13 @@ def main():
     # strong: this rank's share of the tiles; weak (and one GPU): every tile
     mine_arr = np.asarray(tiles if weak else shard_tiles(tiles, rank, world), dtype=np.int32).reshape(-1, 4)
     if args.emulate_shard > 1:
-        mine_arr = np.asarray(shard_tiles(tiles, args.emulate_rank, args.emulate_shard),
+        mine_arr = np.asarray(shard_tiles(tiles, args.emulate_rank, args.emulate_shard, "diag"),
                               dtype=np.int32).reshape(-1, 4)
     ex = TileExchange(tiles, W, H, rank, world, frame.device) if world > 1 and not weak else None
     if ex is not None:
         mine_arr = np.asarray(ex.mine, dtype=np.int32).reshape(-1, 4)
 
-    def reduce_passes():  # weak: sum the N passes onto rank 0, mean over 64N samples
+    def reduce_passes():  # weak: sum the N passes onto rank 0, mean over SPP*N samples
         if backend == "gloo":  # host staging (one-GPU rehearsals)
             h = frame.cpu()
             dist.reduce(h, dst=0)
@@ -262,14 +332,28 @@ def main():
         if rank == 0:
             frame.mul_(1.0 / world)
 
-    def step(stats=False):
+    xev = []  # (start, end) events around each timed step's exchange
+
+    def step(stats=False, timed=False):
         if ex is None:  # the whole tile FIFO straight into the frame (one GPU, or this rank's pass)
             dev.render_tiles_device(mine_arr, frame.data_ptr(), stream, stats=stats)
             if weak:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
                 reduce_passes()
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                if timed:
+                    xev.append((e0, e1))
         else:  # this rank's tiles into its packed buffer, then one gather onto rank 0
             dev.render_tiles_device(mine_arr, ex.packed.data_ptr(), stream, stats=stats, packed=True)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
             ex.exchange(frame)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            if timed:
+                xev.append((e0, e1))
         return dev.stats() if stats else None
 
     # counters for the roofline's algorithmic bytes: the reference's binary BVH
@@ -283,18 +367,25 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):  # asynchronous: nothing waits on the GPU inside a step
-        step()
+        step(timed=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     # HIP events recorded around every launch on its stream (the timed ones)
     kernel_ms, resolve_ms = dev.launch_times(args.steps)
-    s = dev.stats()
+    xchg_ms = float(np.mean([a.elapsed_time(b) for a, b in xev])) if xev else 0.0
+    per_rank = None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        mine = torch.tensor([float(np.mean(kernel_ms)), float(np.mean(resolve_ms)), xchg_ms,
+                             float(np.sum(mine_arr[:, 2] * mine_arr[:, 3]))], dtype=torch.float64,
+                            device="cpu" if backend == "gloo" else f"cuda:{local}")
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [[round(float(v), 4) for v in r.cpu().tolist()] for r in allr]
 
     host_ms = None
     if world == 1:  # the drop-in pt_render_tiles path: output copied to a host buffer (PCIe-inclusive)
@@ -309,13 +400,11 @@ def main():
         value = W * H * SPP * frames * (world if weak else 1) / elapsed / 1e6
         if args.emulate_shard > 1:
             value = float(np.sum(mine_arr[:, 2] * mine_arr[:, 3])) * SPP * frames / elapsed / 1e6
-        bytes_launch = algorithmic_bytes(st_counts)
         avg_ms = float(np.mean(kernel_ms))
-        achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
         img = frame.float().cpu().numpy()
+        scaling = ("weak" if weak else "strong") if world > 1 else "weak"
         out = {
-            "metric": "Mrays/sec + wall-clock render time, CBdragon 1024x1024 @ 64 spp"
-                      if args.workload == "c3" else f"Mrays/sec + wall-clock render time, {wl['desc']}",
+            "metric": HEADLINE_METRIC if workload == "c3" else f"Mrays/sec + wall-clock render time, {wl['desc']}",
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -323,15 +412,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / frames * 1e3, 3),
             "higher_is_better": True,
-            "scaling": args.scaling,
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "fp32",
             "data": {"c5": "synthetic: deterministic CBbunny_sub2 glass/mirror proxy for the missing CBlucy.dae + "
                            "seeded 512x256 environment map (SURVEY §8(d))",
                      "c1": "CBspheres_lambertian.dae from the reference", "c2": "CBspheres_lambertian.dae from the reference"
-                     }.get(args.workload,
+                     }.get(workload,
                            "synthetic: deterministic CBbunny_sub1 proxy for the missing CBdragon.dae (SURVEY §8(d))"),
-            "config": {"workload": wl["desc"] + ", default camera",
+            "config": {"workload": wl["desc"],
                        "width": W, "height": H, "spp": SPP, "max_ray_depth": DEPTH, "ns_area_light": NSL,
                        "spp_total": SPP * world if weak else SPP,
                        "parallelism": (f"samples{world}" if weak else f"tiles{world}") if world > 1 else "single",
@@ -339,12 +428,8 @@ def main():
                        "bvh": "gpu-lbvh" if args.lbvh else "reference-sah (host)",
                        "upload_s": round(t_up, 4),
                        "host_output_ms_per_frame": None if host_ms is None else round(host_ms, 3)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": measured_traffic(args.workload),
-                         "kernel": "render_kernel<false>", "kernel_ms": round(avg_ms, 3),
-                         "resolve_ms": round(float(np.mean(resolve_ms)), 4),
-                         "algorithmic_bytes_per_launch": bytes_launch,
-                         "pmc": measured_pmc(args.workload)},
+            "roofline": roofline(workload, avg_ms, algorithmic_bytes(st_counts)),
+            "resolve_ms": round(float(np.mean(resolve_ms)), 4),
             "counters": {k: st_counts[k] for k in ("camera_rays", "bounce_rays", "shadow_rays", "node_visits",
                                                    "tri_tests", "sphere_tests", "ext_hits", "culled_samples")},
             "launch_counters": {k: st_perf[k] for k in ("node_visits", "tri_tests", "sphere_tests", "wave_trav_steps",
@@ -352,29 +437,84 @@ def main():
                                                         "hitshade_clocks", "trav_clocks", "max_wave_clocks",
                                                         "wave_wall_sum", "wave_wall_max", "section_clocks", "wave_span",
                                                         "lane_iters")},
-            "launch": {"grid_blocks": s["grid_blocks"], "block": 64, "blocks_per_cu_query": s["blocks_per_cu"],
-                       "bvh_nodes": s["bvh_nodes"], "bvh_stack": s["bvh_stack"]},
+            "launch": {"grid_blocks": s_get(dev, "grid_blocks"), "block": 64,
+                       "blocks_per_cu_query": s_get(dev, "blocks_per_cu"),
+                       "bvh_nodes": s_get(dev, "bvh_nodes"), "bvh_stack": s_get(dev, "bvh_stack"),
+                       "group_spp": s_get(dev, "group_spp")},
             "image_mean": float(img.mean()),
         }
         rays = st_counts["camera_rays"] + st_counts["bounce_rays"] + st_counts["shadow_rays"]
-        if world == 1:
-            out["ray_casts_per_s_M"] = round(rays * frames / elapsed / 1e6, 1)
+        out["ray_casts_per_s_M"] = round(rays * frames * (world if weak else 1) / elapsed / 1e6, 1)
+        if per_rank is not None:
+            out["per_rank"] = {"fields": ["kernel_ms", "resolve_ms", "exchange_ms", "pixels"], "ranks": per_rank}
+        elif xev:
+            out["exchange_ms"] = round(xchg_ms, 4)
+        if world == 1 and not args.no_extras and workload == "c3" and not args.scene_dump:
+            out["companions"] = companions(dev, local, stream, max(2, min(args.steps, 5)))
         if world == 1 and not args.no_cpu_baseline:
             try:
                 dp = dump_path
                 if dp is None:
                     from dsgpuraytracing_amd import scene_loader
-                    dp = os.path.join(ROOT, "_scenes", f"bench_{args.workload}.ptd")
-                    scene_loader.dump_dae(dae, W, H, dp, envmap=envmap)
-                if dae is not None and os.access(REF_DRIVER, os.X_OK):
+                    os.makedirs(os.path.join(ROOT, "_scenes"), exist_ok=True)
+                    dp = os.path.join(ROOT, "_scenes", f"bench_{workload}.ptd")
+                    scene_loader.dump_dae(dae, W, H, dp, cam_info=cam, envmap=envmap)
+                if dae is not None and os.access(REF_DRIVER, os.X_OK) and cam is None:
                     out["cpu_baseline"] = cpu_baseline_reference(dae, envmap)
                 else:  # the bit-identical restatement when the reference build is absent
-                    out["cpu_baseline"] = cpu_baseline(dp)
+                    out["cpu_baseline"] = cpu_baseline_port(dp)
+                out["cpu_baseline_fair"] = cpu_baseline_port(dp, budget_s=10.0, rng_mode=1, threads=host_threads())
             except Exception as e:  # reported, never silently replaced
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def s_get(dev, key):
+    return dev.stats().get(key)
+
+
+def companions(dev0, local, stream, frames):
+    """One-GPU companion numbers printed beside the C3 headline (not `value`):
+      * c3_framed: C3 through a camera that frames the box interior, so every
+        sample is traced (the headline's default camera leaves ~75% of the
+        frame outside the scene's footprint);
+      * c4_single_gpu: BASELINE C4 on this one GPU, the 1-GPU point of the
+        multi-GPU (C4, strong) scaling curve."""
+    import torch
+
+    from dsgpuraytracing_amd.pathtracer import Device, Scene, tile_fifo
+    res = {}
+    for name in ("c3f", "c4"):
+        wl = WORKLOADS[name]
+        dae, envmap, cam = workload_scene(wl)
+        sc = Scene.from_dae(dae, wl["w"], wl["h"], cam_info=cam, envmap=envmap)
+        dev = Device(local)
+        dev.upload_scene(sc)
+        dev.set_camera(sc.camera)
+        dev.set_params(wl["w"], wl["h"], wl["spp"], DEPTH, NSL, SEED)
+        tl = np.asarray(tile_fifo(wl["w"], wl["h"]), np.int32)
+        fr = torch.zeros((wl["h"], wl["w"], 3), dtype=torch.float32, device=f"cuda:{local}")
+        dev.render_tiles_device(tl, fr.data_ptr(), stream)
+        dev.render_tiles_device(tl, fr.data_ptr(), stream, stats=True)
+        st = dev.stats()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            dev.render_tiles_device(tl, fr.data_ptr(), stream)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        k, _ = dev.launch_times(frames)
+        rays = st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]
+        res["c3_framed" if name == "c3f" else "c4_single_gpu"] = {
+            "workload": wl["desc"], "value": round(wl["w"] * wl["h"] * wl["spp"] * frames / el / 1e6, 1),
+            "unit": "Mrays/s", "ms_per_step": round(el / frames * 1e3, 3), "kernel_ms": round(float(np.mean(k)), 3),
+            "frames": frames, "culled_samples": st["culled_samples"],
+            "ray_casts_per_s_M": round(rays * frames / el / 1e6, 1)}
+        dev.close()
+        del fr
+    return res
 
 
 if __name__ == "__main__":

@@ -13,6 +13,15 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
+_LAST = ("test_gpu_fullsize.py",)
+
+
+def pytest_collection_modifyitems(config, items):
+    """Cheap GPU parity cases first, full-size BASELINE configs last, so a
+    `-x` run reports the small HIP-vs-oracle cases before the long ones."""
+    items.sort(key=lambda it: os.path.basename(str(it.fspath)) in _LAST)
+
+
 @pytest.fixture(scope="session")
 def restate():
     from tests import oracle_helpers

@@ -1,11 +1,25 @@
-"""Parity at BASELINE.json's full sizes (SURVEY.md §8(d) C3 and C5).
+"""Parity at BASELINE.json's full sizes (SURVEY.md §8(d) C1-C5).
 
-The GPU renders the whole frame at the benchmark configuration; the oracle
-restatement (counter RNG, the same draws in the same order) renders a spread
-of sampled 32x32 tiles of it, which must match near-exactly, and the
-size-independent properties of the full frame are checked: finite and
-non-negative radiance, determinism, and that a tile split (the multi-GPU
-strong split) reassembles the frame bit for bit.
+C1 (256x256, 1 spp) and C2 (512x512, 16 spp) are cheap for the oracle, so the
+whole HIP frame is compared with the whole restatement frame (counter RNG, the
+same draws in the same order).  For C3 (1024x1024, 64 spp), C4 (1920x1080,
+256 spp) and C5 (1920x1080, 512 spp) the GPU renders the whole frame and the
+restatement renders a spread of sampled 32x32 tiles of it, which must match
+near-exactly; the size-independent properties of the whole frame are checked
+as well: finite and non-negative radiance, determinism, and that a tile split
+(the multi-GPU strong split) reassembles the frame bit for bit.
+
+The sampled tiles are chosen FROM THE ORACLE, never by hand: a 1-spp
+restatement render of the whole frame (C3: 0.15 s, C5: 1 s on 8 threads) gives
+every tile's coverage, the candidates are the full 32x32 tiles in which every
+pixel saw radiance, and k of them are taken at evenly spaced ranks.  The
+precondition (every chosen reference tile is lit) is asserted before the GPU
+render.
+
+Tolerance (SURVEY.md §8(c) criterion 2), for every config: >= 99.5% of
+pixels within 1e-3 relative and the (sampled-tile) image mean within 0.1%.
+Measured on the box: C1 100%, C2 99.995%, C3 99.988%,
+C4 99.935%, C5 99.902% of pixels; mean differences 2e-6 .. 1.3e-5.
 """
 import os
 
@@ -13,17 +27,32 @@ import numpy as np
 import pytest
 
 from dsgpuraytracing_amd import scene_loader, scenes
+from dsgpuraytracing_amd.dist import shard_tiles
 from dsgpuraytracing_amd.pathtracer import Device, Scene, tile_fifo
 
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
+WORKLOADS = {
+    # name: (dae, envmap, W, H, spp)
+    "c1": (scenes.C1_DAE, None, 256, 256, 1),
+    "c2": (scenes.C1_DAE, None, 512, 512, 16),
+    "c3": ("proxy1", None, 1024, 1024, 64),
+    "c4": ("proxy1", None, 1920, 1080, 256),
+    "c5": ("c5", "c5env", 1920, 1080, 512),
+}
+
 
 def _workload(name):
-    if name == "c3":
-        return scenes.proxy_path(1), None, 1024, 1024, 64
-    return scenes.c5_path(2), scenes.c5_envmap_path(), 1920, 1080, 512
+    dae, env, w, h, spp = WORKLOADS[name]
+    if dae == "proxy1":
+        dae = scenes.proxy_path(1)
+    elif dae == "c5":
+        dae = scenes.c5_path(2)
+    if env == "c5env":
+        env = scenes.c5_envmap_path()
+    return dae, env, w, h, spp
 
 
 def _device(dae, envmap, w, h, spp, seed=1):
@@ -35,36 +64,75 @@ def _device(dae, envmap, w, h, spp, seed=1):
     return dev
 
 
-def _tile_index(tx, ty, w):
-    return ty * ((w + 31) // 32) + tx
+def near_exact(a, b):
+    diff = np.abs(a - b).max(axis=-1)
+    scale = np.maximum(1.0, np.abs(b).max(axis=-1))
+    return float((diff <= 1e-3 * scale).mean())
 
 
-@pytest.mark.parametrize("name,tiles,min_close", [
-    # tile (column, row) pairs spread over the scene footprint (bunny, walls, floor, light)
-    ("c3", [(15, 8), (16, 14), (12, 20), (18, 24), (14, 11), (17, 17)], 0.99),
-    ("c5", [(29, 12), (31, 17), (27, 22), (33, 8)], 0.95),
-])
-def test_fullsize_sampled_tiles_match_oracle(tmp_path, restate, name, tiles, min_close):
+def lit_tiles(restate, dump, w, h, k, seed=1):
+    """k full 32x32 tiles, every pixel of which receives radiance in a 1-spp
+    restatement render, at evenly spaced ranks of the tile FIFO order."""
+    one, _ = restate.render(dump, w, h, 1, 4, 1, seed, rng_mode=1, threads=8)
+    cand = []
+    for x, y, _, _ in tile_fifo(w, h):
+        if x + 32 <= w and y + 32 <= h and (one[y:y + 32, x:x + 32].max(axis=2) > 0).all():
+            cand.append((x, y))
+    assert len(cand) >= k, f"only {len(cand)} fully lit tiles"
+    pick = np.linspace(0, len(cand) - 1, k).round().astype(int)
+    return [cand[i] for i in pick]
+
+
+@pytest.mark.parametrize("name", ["c1", "c2"])
+def test_fullframe_near_exact_vs_oracle(tmp_path, restate, name):
     dae, envmap, w, h, spp = _workload(name)
+    dump = str(tmp_path / f"{name}.ptd")
+    scene_loader.dump_dae(dae, w, h, dump, envmap=envmap)
+    ref, _ = restate.render(dump, w, h, spp, 4, 1, 1, rng_mode=1, threads=8)
+    assert ref.mean() > 0
     dev = _device(dae, envmap, w, h, spp)
     img = np.zeros((h, w, 3), np.float32)
     dev.render_tiles(tile_fifo(w, h), img)
     assert np.isfinite(img).all() and (img >= 0).all()
+    close = near_exact(img, ref)
+    rel_mean = abs(img.mean() - ref.mean()) / ref.mean()
+    print(f"{name}: {close * 100:.3f}% pixels within 1e-3, image-mean rel diff {rel_mean:.2e}")
+    assert close >= 0.995, close
+    assert rel_mean <= 1e-3, rel_mean
+
+
+# (name, tiles sampled, per-pixel near-exact fraction: SURVEY's 99.5% throughout)
+@pytest.mark.parametrize("name,k,min_close", [
+    ("c3", 8, 0.995),
+    ("c4", 6, 0.995),
+    ("c5", 4, 0.995),
+])
+def test_fullsize_sampled_tiles_match_oracle(tmp_path, restate, name, k, min_close):
+    dae, envmap, w, h, spp = _workload(name)
     dump = str(tmp_path / f"{name}.ptd")
     scene_loader.dump_dae(dae, w, h, dump, envmap=envmap)
-    closes, gm, rm = [], [], []
-    for tx, ty in tiles:
-        k = _tile_index(tx, ty, w)
-        ref, _ = restate.render(dump, w, h, spp, 4, 1, 1, rng_mode=1, threads=8, tile_begin=k, tile_end=k + 1)
-        sl = (slice(ty * 32, ty * 32 + 32), slice(tx * 32, tx * 32 + 32))
-        a, b = img[sl], ref[sl]
-        assert b.mean() > 0  # the tile sees the lit scene
-        closes.append((np.abs(a - b).max(axis=2) <= 1e-3 * np.maximum(1.0, np.abs(b).max(axis=2))).mean())
-        gm.append(a.mean())
-        rm.append(b.mean())
-    close = float(np.mean(closes))
-    assert close >= min_close, (closes, gm, rm)
-    assert abs(np.mean(gm) - np.mean(rm)) <= 0.01 * np.mean(rm)
+    tiles = lit_tiles(restate, dump, w, h, k)
+    tw = (w + 31) // 32
+    refs = []
+    for x, y in tiles:   # the oracle first: its precondition is checked before the GPU runs
+        t = (y // 32) * tw + x // 32
+        ref, _ = restate.render(dump, w, h, spp, 4, 1, 1, rng_mode=1, threads=8, tile_begin=t, tile_end=t + 1)
+        b = ref[y:y + 32, x:x + 32]
+        assert b.mean() > 0, (x, y)
+        refs.append(b)
+    dev = _device(dae, envmap, w, h, spp)
+    img = np.zeros((h, w, 3), np.float32)
+    dev.render_tiles(tile_fifo(w, h), img)
+    assert np.isfinite(img).all() and (img >= 0).all()
+    got = np.stack([img[y:y + 32, x:x + 32] for x, y in tiles])
+    ref = np.stack(refs)
+    closes = [near_exact(a, b) for a, b in zip(got, ref)]
+    close = near_exact(got, ref)
+    rel_mean = abs(got.mean() - ref.mean()) / ref.mean()
+    print(f"{name}: tiles {tiles}\n  per-tile {np.round(closes, 4).tolist()}\n"
+          f"  {close * 100:.3f}% pixels within 1e-3, sampled-tile mean rel diff {rel_mean:.2e}")
+    assert close >= min_close, closes
+    assert rel_mean <= 1e-3, rel_mean
 
 
 def test_c3_fullsize_deterministic_and_split():
@@ -75,10 +143,26 @@ def test_c3_fullsize_deterministic_and_split():
     again = np.zeros_like(full)
     dev.render_tiles(tile_fifo(w, h), again)
     assert np.array_equal(full, again)
-    from dsgpuraytracing_amd.dist import shard_tiles
     parts = np.zeros_like(full)
     for r in range(3):  # the strong multi-GPU split, one share at a time
         p = np.zeros_like(full)
         dev.render_tiles(shard_tiles(tile_fifo(w, h), r, 3, "diag"), p)
         parts += p
     assert np.array_equal(parts, full)
+
+
+def test_c4_fullsize_eight_way_split_bit_identical():
+    """BASELINE C4's multi-GPU split: the 8 diagonal tile shards, rendered one
+    share at a time, reassemble the 1-GPU frame bit for bit."""
+    dae, envmap, w, h, _ = _workload("c4")
+    spp = 16   # the split property does not depend on spp; 16 keeps the test short
+    dev = _device(dae, envmap, w, h, spp, seed=4)
+    full = np.zeros((h, w, 3), np.float32)
+    dev.render_tiles(tile_fifo(w, h), full)
+    parts = np.zeros_like(full)
+    for r in range(8):
+        p = np.zeros_like(full)
+        dev.render_tiles(shard_tiles(tile_fifo(w, h), r, 8, "diag"), p)
+        parts += p
+    assert np.array_equal(parts, full)
+    assert full.mean() > 0

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 WL=$1; R=$2; shift 2
 for r in $(seq 1 "$R"); do
   for v in "$@"; do
-    out=$(PT_LIB="$v" timeout -k 10 120 python bench.py --workload "$WL" --no-cpu-baseline --steps 10 --warmup 2 2>/dev/null) || { echo "FAILED $v"; exit 3; }
+    out=$(PT_LIB="$v" timeout -k 10 120 python bench.py --workload "$WL" --no-cpu-baseline --no-extras --steps 10 --warmup 2 2>/dev/null) || { echo "FAILED $v"; exit 3; }
     echo "$v $(echo "$out" | python -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d["value"], d["roofline"]["kernel_ms"])')"
   done
 done

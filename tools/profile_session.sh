@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 WL=${1:-c3}
 STEPS=${2:-5}
-B="python3 bench.py --workload $WL --steps $STEPS --warmup 2 --no-cpu-baseline"
+B="python3 bench.py --workload $WL --steps $STEPS --warmup 2 --no-cpu-baseline --no-extras"
 P="rocprofv3 --output-format csv"
 rm -rf gpurun_out/prof
 exec tools/gpu_session.sh \

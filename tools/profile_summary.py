@@ -6,8 +6,8 @@ Reads the passes written by tools/profile_session.sh under gpurun_out/prof/:
   write/  --pmc WRITE_SIZE            (KB)
   sq/     --pmc SQ_*                  (quad-cycle units for *_CYCLES / WAIT / ACTIVE)
   tcc/    --pmc TCC_HIT_sum TCC_MISS_sum
-and writes <out>/<workload>_kernel_stats.csv, <out>/<workload>_summary.json and
-profiles/latest_traffic.json (read by bench.py for roofline.traffic).
+and writes <out>/<workload>_kernel_stats.csv and <out>/<workload>_summary.json
+(bench.py's roofline reads the newest round's summary of its workload).
 Usage: python tools/profile_summary.py <workload> <out_dir> [prof_dir]
 """
 import collections
@@ -84,10 +84,6 @@ def main():
             s["l2_hit_rate"] = tcc["TCC_HIT_sum"] / (tcc["TCC_HIT_sum"] + tcc["TCC_MISS_sum"])
     with open(os.path.join(out, f"{workload}_summary.json"), "w") as f:
         json.dump(s, f, indent=1)
-    if "hbm_bytes_per_launch" in s:
-        with open("profiles/latest_traffic.json", "w") as f:
-            json.dump({"workload": workload, "kernel": KERNEL, "hbm_bytes_per_launch": s["hbm_bytes_per_launch"],
-                       "avg_ms": s["avg_ms"], "source": os.path.join(out, f"{workload}_summary.json")}, f, indent=1)
     print(json.dumps(s, indent=1))
 
 
