@@ -185,18 +185,14 @@ def tile_fifo(w: int, h: int, tile: int = TILE) -> List[Tuple[int, int, int, int
 
 def to_color(hdr: np.ndarray) -> np.ndarray:
     """HDRImageBuffer::toColor (image.h:174-189) + Color -> RGBA8
-    (ImageBuffer::update_pixel, image.h:49-58): c = (s*sqrt(2))^(1/2.2),
-    clamped to [0,1], times 255, truncated."""
-    gamma = np.float32(2.2)
-    one_over_gamma = np.float32(1.0) / gamma
-    exposure = np.float32(np.sqrt(np.float32(2.0)))
-    with np.errstate(invalid="ignore"):
-        c = np.power(hdr.astype(np.float32) * exposure, one_over_gamma)
-    c = np.nan_to_num(c, nan=0.0)
-    c = np.clip(c, 0.0, 1.0)
-    rgb = (c * 255).astype(np.uint8)
-    a = np.full(hdr.shape[:2] + (1,), 255, np.uint8)
-    return np.concatenate([rgb, a], axis=2)
+    (ImageBuffer::update_pixel, image.h:49-58) of a whole (H, W, 3) float32
+    buffer, through libptgpu.so's pt_to_color (the reference's powf
+    arithmetic, bit-exact: tests/test_output.py).  Returns (H, W, 4) uint8."""
+    hdr = np.ascontiguousarray(hdr, dtype=np.float32)
+    h, w = hdr.shape[:2]
+    frame = np.zeros((h, w), np.uint32)
+    native.check(native.lib().pt_to_color(hdr.ctypes.data, w, h, 0, 0, w, h, frame.ctypes.data))
+    return frame.view(np.uint8).reshape(h, w, 4)
 
 
 class PathTracer:

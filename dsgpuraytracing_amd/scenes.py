@@ -210,6 +210,29 @@ def c5_path(levels: int = 2, cache_dir: Optional[str] = None) -> str:
     return dst
 
 
+_REFRACTION_BSDF = """<refraction>
+            <transmittance>1 1 1</transmittance>
+            <roughness>0</roughness>
+            <ior>1.45</ior>
+          </refraction>"""
+
+
+def refraction_variant(dst: str) -> str:
+    """CBspheres.dae with its glass sphere's material rewritten as a
+    <refraction> material (RefractionBSDF, collada.cpp:893-901, bsdf.cpp:
+    90-111; no reference asset uses it): transmittance 1 1 1, roughness 0,
+    ior 1.45 -- the glass element's own values.  Everything else is the file
+    as shipped."""
+    txt = open(os.path.join(ASSETS, "CBspheres.dae")).read()
+    g0 = txt.index("<glass>")
+    g1 = txt.index("</glass>", g0) + len("</glass>")
+    txt = txt[:g0] + _REFRACTION_BSDF + txt[g1:]
+    if not os.path.exists(dst) or open(dst).read() != txt:
+        with open(dst, "w") as f:
+            f.write(txt)
+    return dst
+
+
 def c5_envmap_path(cache_dir: Optional[str] = None) -> str:
     """The C5 environment map: synthetic_envmap(512, 256, seed=7) as a ZIP OpenEXR."""
     from . import image_io

@@ -250,6 +250,15 @@ int pt_get_launch_times(pt_ctx* ctx, float* kernel_ms, float* resolve_ms, int32_
 int pt_get_wave_trace(pt_ctx* ctx, int64_t* out, int64_t cap, int64_t* n_waves);
 const char* pt_last_error(void);
 
+/* Output row, host side (no device needed):
+ * HDRImageBuffer::toColor(target, x0, y0, x1, y1) (src/image.h:174-189) of the
+ * HDR buffer `hdr` (width*height*3 float, the sampleBuffer layout) into the
+ * RGBA8 `frame` (width*height uint32, ImageBuffer::data: r | g<<8 | b<<16 |
+ * a<<24, image.h:49-58), with the reference's float arithmetic (powf; NaN ->
+ * 255).  Pixels outside [x0,x1) x [y0,y1) are left untouched. */
+int pt_to_color(const float* hdr, int32_t width, int32_t height, int32_t x0, int32_t y0, int32_t x1, int32_t y1,
+                uint32_t* frame);
+
 #ifdef __cplusplus
 }
 #endif

@@ -21,6 +21,9 @@
 //   rng    : prints the first rand() draws and the sampler draw order
 //   exr    : decodes --envmap with the reference's tinyexr + load_exr (main.cpp:30-67)
 //            and writes the HDRImageBuffer (float32 w*h*3) to a PTDUMP
+//   tocolor: HDRImageBuffer::toColor (image.h:174-189) of the PTDUMP "hdr" of --in
+//            into the RGBA8 frameBuffer, plus the vertically flipped copy
+//            PathTracer::save_image hands lodepng (pathtracer.cpp:649-674)
 //   exrw   : writes the PTDUMP "rgb" (w, h) of --in as a ZIP OpenEXR with the
 //            reference's tinyexr (SaveMultiChannelEXRToFile), channels B,G,R,
 //            pixel type --half 0/1 (fixtures for the native EXR loader)
@@ -151,6 +154,29 @@ static HDRImageBuffer* load_exr(const char* file_path) {
   return envmap;
 }
 
+// tocolor: --in PTDUMP {hdr f4 (h*w*3, row 0 = y 0), shape i8 (h, w, 3)} ->
+// --out {frame u4 (h*w, ImageBuffer::data), png_rows u4 (save_image's rows)}
+static int tocolor_mode(const Opts& o) {
+  std::vector<ptdump::Record> R;
+  if (!ptdump::read_all(o.in.c_str(), R)) die("cannot read --in");
+  vector<float> hdr;
+  vector<int64_t> shape;
+  if (!ptdump::get(R, "hdr", hdr) || !ptdump::get(R, "shape", shape) || shape.size() != 3) die("bad --in");
+  const size_t h = (size_t)shape[0], w = (size_t)shape[1];
+  HDRImageBuffer sb;
+  sb.resize(w, h);
+  for (size_t i = 0; i < w * h; ++i) sb.data[i] = Spectrum(hdr[3 * i], hdr[3 * i + 1], hdr[3 * i + 2]);
+  ImageBuffer fb;
+  fb.resize(w, h);
+  sb.toColor(fb, 0, 0, w, h);
+  vector<uint32_t> rows(w * h);  // save_image (pathtracer.cpp:662-667)
+  for (size_t i = 0; i < h; ++i) std::memcpy(&rows[i * w], &fb.data[(h - i - 1) * w], 4 * w);
+  ptdump::Writer wr(o.out.c_str());
+  wr.raw("frame", "u4", fb.data.data(), (int64_t)(w * h), 4);
+  wr.raw("png_rows", "u4", rows.data(), (int64_t)(w * h), 4);
+  return 0;
+}
+
 static int exr_modes(const Opts& o) {
   if (o.mode == "exr") {
     HDRImageBuffer* m = load_exr(o.envmap.c_str());
@@ -219,6 +245,41 @@ static void load_camera_file(const string& fn, Camera& cam) {
               &cam.c2w(2, 2));
   std::fclose(f);
   if (n != 19) die("bad camera file");
+}
+
+// main.cpp + Application::load + set_up_pathtracer: the PathTracer every mode uses.
+static PathTracer* setup_pathtracer(const Opts& o) {
+  Camera* camera = new Camera();
+  DynamicScene::Scene* dscene = nullptr;
+  build_scene(o, *camera, dscene);
+  g_envmap = o.envmap.empty() ? nullptr : load_exr(o.envmap.c_str());
+  PathTracer* pt = new PathTracer(o.spp, o.depth, o.lights, 1, 1, 1, o.threads, g_envmap);
+  pt->useCPU = true;
+  // set_up_pathtracer (application.cpp:624-633)
+  pt->set_camera(camera);
+  pt->set_scene(dscene->get_static_scene());
+  pt->set_frame_size(o.w, o.h);
+  if (!o.cam.empty()) load_camera_file(o.cam, *camera);
+  return pt;
+}
+
+// The same set-up for the INTEGRATION.md adapter link test (tests/adapter/,
+// built with -DREF_DRIVER_NO_MAIN): the PathTracer the reference's GPU seam
+// would be handed, and the -e environment map (or nullptr).
+PathTracer* ref_setup_pathtracer(const char* scene, size_t w, size_t h, size_t spp, size_t depth, size_t lights,
+                                 const char* cam, const char* envmap, HDRImageBuffer** env_out) {
+  Opts o;
+  o.scene = scene;
+  o.w = w;
+  o.h = h;
+  o.spp = spp;
+  o.depth = depth;
+  o.lights = lights;
+  if (cam) o.cam = cam;
+  if (envmap) o.envmap = envmap;
+  PathTracer* pt = setup_pathtracer(o);
+  if (env_out) *env_out = g_envmap;
+  return pt;
 }
 
 static void dump_scene(const Opts& o, PathTracer& pt) {
@@ -415,6 +476,7 @@ static void answer_rays(const Opts& o, PathTracer& pt) {
   w.i4("any", any);
 }
 
+#ifndef REF_DRIVER_NO_MAIN
 int main(int argc, char** argv) {
   Opts o;
   for (int i = 1; i < argc; ++i) {
@@ -449,19 +511,10 @@ int main(int argc, char** argv) {
     return 0;
   }
   if (o.mode == "exr" || o.mode == "exrw") return exr_modes(o);
+  if (o.mode == "tocolor") return tocolor_mode(o);
   if (o.scene.empty()) die("no scene");
 
-  Camera camera;
-  DynamicScene::Scene* dscene = nullptr;
-  build_scene(o, camera, dscene);
-  g_envmap = o.envmap.empty() ? nullptr : load_exr(o.envmap.c_str());
-  PathTracer* pt = new PathTracer(o.spp, o.depth, o.lights, 1, 1, 1, o.threads, g_envmap);
-  pt->useCPU = true;
-  // set_up_pathtracer (application.cpp:624-633)
-  pt->set_camera(&camera);
-  pt->set_scene(dscene->get_static_scene());
-  pt->set_frame_size(o.w, o.h);
-  if (!o.cam.empty()) load_camera_file(o.cam, camera);
+  PathTracer* pt = setup_pathtracer(o);
 
   if (o.mode == "dump") {
     dump_scene(o, *pt);
@@ -523,3 +576,4 @@ int main(int argc, char** argv) {
   }
   return 0;
 }
+#endif  // REF_DRIVER_NO_MAIN

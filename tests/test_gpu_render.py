@@ -43,6 +43,8 @@ def near_exact_report(a, b):
     ("c1_default_128x128", 128, 128, 16, 4, 1, 3),
     ("CBspheres_64x64", 64, 64, 4, 4, 1, 3),                         # mirror + glass spheres
     ("CBspheres_128x128", 128, 128, 16, 4, 1, 5),
+    ("CBspheres_refraction_64x64", 64, 64, 4, 4, 1, 3),              # RefractionBSDF (bsdf.cpp:90-111)
+    ("CBspheres_refraction_128x128", 128, 128, 16, 4, 1, 5),
     ("CBspheres_lambertian_pointlight_64x64", 64, 64, 4, 4, 1, 3),   # delta lights: EPS_N offset
     ("CBspheres_lambertian_dirlight_64x64", 64, 64, 4, 4, 1, 3),
     ("CBspheres_lambertian_ambientlight_64x64", 64, 64, 4, 4, 2, 3), # hemisphere light, 2 samples
@@ -86,6 +88,20 @@ def test_hip_mirror_glass_statistical_vs_reference_golden():
     r1 = ptdump.read(golden("CBspheres_128x128_s64_m4_l1_seed1.hdr.ptd"))["hdr"].reshape(128, 128, 3)
     r2 = ptdump.read(golden("CBspheres_128x128_s64_m4_l1_seed2.hdr.ptd"))["hdr"].reshape(128, 128, 3)
     g, _ = gpu_render("CBspheres_128x128", 128, 128, 64, 4, 1, seed=999)
+    floor = np.linalg.norm(r1 - r2, axis=2).mean()
+    dist = np.linalg.norm(g - r1, axis=2).mean()
+    sigma = (r1 - r2).mean(axis=2).std() / np.sqrt(128 * 128)
+    bias = abs(g.mean() - r1.mean())
+    print(f"L2 {dist:.5f} vs floor {floor:.5f}; bias {bias:.2e} vs 3 sigma {3*sigma:.2e}")
+    assert dist <= 1.10 * floor
+    assert bias <= 3 * sigma
+
+
+def test_hip_refraction_statistical_vs_reference_golden():
+    """RefractionBSDF sphere (CBspheres_refraction.dae) at 128x128 @ 64 spp vs the reference binary."""
+    r1 = ptdump.read(golden("CBspheres_refraction_128x128_s64_m4_l1_seed1.hdr.ptd"))["hdr"].reshape(128, 128, 3)
+    r2 = ptdump.read(golden("CBspheres_refraction_128x128_s64_m4_l1_seed2.hdr.ptd"))["hdr"].reshape(128, 128, 3)
+    g, _ = gpu_render("CBspheres_refraction_128x128", 128, 128, 64, 4, 1, seed=4242)
     floor = np.linalg.norm(r1 - r2, axis=2).mean()
     dist = np.linalg.norm(g - r1, axis=2).mean()
     sigma = (r1 - r2).mean(axis=2).std() / np.sqrt(128 * 128)

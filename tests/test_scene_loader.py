@@ -29,7 +29,7 @@ def test_c1_scene_bit_identical_to_reference(fixture, w, h, cam):
 
 
 @pytest.mark.parametrize("name", ["CBspheres", "CBspheres_lambertian_pointlight", "CBspheres_lambertian_dirlight",
-                                  "CBspheres_lambertian_ambientlight"])
+                                  "CBspheres_lambertian_ambientlight", "CBspheres_refraction"])
 def test_bsdf_and_light_variants_bit_identical(name):
     got = scene_loader.load_dae(os.path.join(ROOT, "assets", name + ".dae"), 64, 64)
     ref = ptdump.read(golden(f"{name}_64x64.scene.ptd"))
