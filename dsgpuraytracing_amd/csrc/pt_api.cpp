@@ -22,15 +22,6 @@
 #include "pt_error.h"
 
 namespace {
-thread_local std::string g_err;
-}  // namespace
-
-int pt_fail(int code, const std::string& msg) {
-  g_err = msg;
-  return code;
-}
-
-namespace {
 
 int fail(int code, const std::string& msg) { return pt_fail(code, msg); }
 
@@ -185,7 +176,6 @@ struct pt_ctx {
 
 extern "C" {
 
-const char* pt_last_error(void) { return g_err.c_str(); }
 
 int pt_create(int device, pt_ctx** out) {
   if (!out) return fail(PT_E_INVALID, "pt_create: out is NULL");

@@ -1273,7 +1273,17 @@ int load_impl(const char* path, int W, int H, const char* cam_info, pt_host_scen
       for (int j = 0; j < 3; ++j) camera.c2w[j][i] = m[3 * i + j];
   }
 
-  // BVH (pathtracer.cpp:242 -> bvh.cpp:181-202)
+  // BVH (pathtracer.cpp:242 -> bvh.cpp:181-202).  A non-finite coordinate
+  // (a corrupted or hostile file: "nan", "1e999") would turn the bucket index
+  // of bvh.cpp:47 into an out-of-range integer conversion; the reference reads
+  // out of bounds there, this pipeline refuses the scene.
+  if (prims.empty()) return pt_fail(PT_E_IO, "pt_host_scene_load: the scene has no primitives");
+  for (const Prim& p : prims) {
+    const BBox b = p.bbox();
+    for (int k = 0; k < 3; ++k)
+      if (!std::isfinite(b.min[k]) || !std::isfinite(b.max[k]))
+        return pt_fail(PT_E_IO, "pt_host_scene_load: non-finite primitive coordinate");
+  }
   BvhBuilder bb(prims);
   bb.run();
 
