@@ -22,7 +22,11 @@ the scene.
     bit-identical to the 1-GPU image.  --scaling weak (opt-in) renders one
     64-spp pass of the whole frame per GPU over disjoint sample ranges plus
     one RCCL sum-reduce.
-The exchange is inside the timed region.
+The exchange is inside the timed region.  Device renders are queued back to
+back and consecutive frames overlap on the GPU (pt_api.cpp's two-slot render
+pipeline: the next frame's waves fill the CUs the previous frame's drain
+leaves idle); config.single_frame_ms is the wall-clock time of one frame
+rendered alone, synchronised on both sides.
 """
 from __future__ import annotations
 
@@ -104,7 +108,7 @@ def profile_summary(workload: str):
     return None
 
 
-def roofline(workload: str, kernel_ms: float, alg_bytes: float) -> dict:
+def roofline(workload: str, kernel_ms: float, alg_bytes: float, frame_ms: float = 0.0) -> dict:
     """Roofline of the dominant kernel (render_kernel).  Per-launch counts come
     from the committed PMC summary of the same workload (they are a property
     of the workload, not of the clock); rates divide them by the kernel time
@@ -116,7 +120,10 @@ def roofline(workload: str, kernel_ms: float, alg_bytes: float) -> dict:
       valu  -- SQ_INSTS_VALU wave-instructions vs 2 per CU per cycle;
       algorithmic -- the §8(d) cost-model bytes, cache-served, vs the L2 roof.
     `bound` names the measured view with the highest fraction; the kernel is
-    latency-bound below all of them (SQ_WAIT_ANY, see pmc)."""
+    latency-bound below all of them (SQ_WAIT_ANY, see pmc).  Consecutive
+    renders overlap (the render pipeline of pt_api.cpp), so a launch lasts
+    longer than the frame interval: each view also gives frac_per_frame, the
+    same counts over the measured ms_per_step."""
     t = kernel_ms * 1e-3
     pm = profile_summary(workload)
     views = {"algorithmic_cache_served": {
@@ -141,6 +148,9 @@ def roofline(workload: str, kernel_ms: float, alg_bytes: float) -> dict:
             views["valu"] = {"insts_per_launch": sq["SQ_INSTS_VALU"], "achieved": round(a, 1),
                              "peak": VALU_PEAK_GINST, "unit": "G wave-instructions/s",
                              "frac": round(a / VALU_PEAK_GINST, 4)}
+    if frame_ms > 0:
+        for v in views.values():
+            v["frac_per_frame"] = round(v["frac"] * kernel_ms / frame_ms, 4)
     measured = [k for k in ("hbm", "l2", "valu") if k in views]
     bound = max(measured, key=lambda k: views[k]["frac"]) if measured else "algorithmic_cache_served"
     v = views[bound]
@@ -256,6 +266,7 @@ def main():
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
                     help="default: c3 on one GPU, c4 (the BASELINE multi-GPU config) on N > 1")
     ap.add_argument("--lbvh", action="store_true", help="build the BVH on the GPU (pt_upload_scene_lbvh)")
+    ap.add_argument("--spp", type=int, default=0, help="diagnostic: override the workload's spp (not a BASELINE config)")
     ap.add_argument("--emulate-shard", type=int, default=0,
                     help="diagnostic: render only one rank's share of an N-GPU split on this one GPU")
     ap.add_argument("--emulate-rank", type=int, default=0, help="the rank --emulate-shard renders")
@@ -285,7 +296,7 @@ def main():
     global W, H, SPP
     workload = args.workload or ("c3" if world == 1 else "c4")
     wl = WORKLOADS[workload]
-    W, H, SPP = wl["w"], wl["h"], wl["spp"]
+    W, H, SPP = wl["w"], wl["h"], args.spp or wl["spp"]
 
     from dsgpuraytracing_amd.pathtracer import Device, Scene, tile_fifo
 
@@ -388,7 +399,19 @@ def main():
         per_rank = [[round(float(v), 4) for v in r.cpu().tolist()] for r in allr]
 
     host_ms = None
-    if world == 1:  # the drop-in pt_render_tiles path: output copied to a host buffer (PCIe-inclusive)
+    single_ms = None
+    if world == 1:
+        # one frame alone, synchronised on both sides (no overlap with a
+        # neighbouring frame): the wall-clock render time of ONE frame
+        lat = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0s = time.perf_counter()
+            step()
+            torch.cuda.synchronize()
+            lat.append(time.perf_counter() - t0s)
+        single_ms = float(np.median(lat)) * 1e3
+        # the drop-in pt_render_tiles path: output copied to a host buffer (PCIe-inclusive)
         host = np.zeros((H, W, 3), np.float32)
         dev.render_tiles(mine_arr, host)
         t0h = time.perf_counter()
@@ -425,10 +448,11 @@ def main():
                        "spp_total": SPP * world if weak else SPP,
                        "parallelism": (f"samples{world}" if weak else f"tiles{world}") if world > 1 else "single",
                        "render_time_s": round(elapsed / frames, 4), "scene_load_s": round(t_load, 3),
+                       "single_frame_ms": None if single_ms is None else round(single_ms, 3),
                        "bvh": "gpu-lbvh" if args.lbvh else "reference-sah (host)",
                        "upload_s": round(t_up, 4),
                        "host_output_ms_per_frame": None if host_ms is None else round(host_ms, 3)},
-            "roofline": roofline(workload, avg_ms, algorithmic_bytes(st_counts)),
+            "roofline": roofline(workload, avg_ms, algorithmic_bytes(st_counts), elapsed / frames * 1e3),
             "resolve_ms": round(float(np.mean(resolve_ms)), 4),
             "counters": {k: st_counts[k] for k in ("camera_rays", "bounce_rays", "shadow_rays", "node_visits",
                                                    "tri_tests", "sphere_tests", "ext_hits", "culled_samples")},

@@ -37,7 +37,10 @@ struct DevBuf {
   size_t n = 0;
   hipError_t reserve(size_t count) {
     if (count <= n && p) return hipSuccess;
-    if (p) (void)hipFree(p);
+    if (p) {  // renders in flight on other streams may still read the old array
+      (void)hipDeviceSynchronize();
+      (void)hipFree(p);
+    }
     p = nullptr;
     n = 0;
     hipError_t e = hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T));
@@ -148,15 +151,27 @@ struct pt_ctx {
   DevBuf<float> norms;
   DevBuf<DBsdf> bsdfs;
   DevBuf<DLight> lights;
-  DevBuf<int4> tiles;
-  std::vector<int4> tiles_host;  // what `tiles` holds
-  DevBuf<int4> blocks;           // footprint-clipped 8x8 pixel blocks of the tiles
-  std::vector<int4> blocks_host;
+  // Render pipeline: launches alternate between kSlots slots, each with its
+  // own render stream and per-launch device state (tile and block lists,
+  // work-queue heads, sample-group sums, stack spill area).  A render waits
+  // only until the resolve of the previous launch of ITS slot has consumed
+  // the slot's group sums (ev_free), so consecutive device renders overlap:
+  // the next frame's waves fill the CUs the previous frame's drain leaves
+  // idle.  Each resolve runs on the caller's stream after its own render, so
+  // the caller's stream order is kept for everything it can observe.
+  static constexpr int kSlots = 2;
+  hipStream_t rstream[kSlots] = {};
+  hipEvent_t ev_free[kSlots] = {};
+  DevBuf<int4> tiles[kSlots];
+  std::vector<int4> tiles_host[kSlots];  // what `tiles` holds
+  DevBuf<int4> blocks[kSlots];           // footprint-clipped 8x8 pixel blocks of the tiles
+  std::vector<int4> blocks_host[kSlots];
+  DevBuf<float> partial[kSlots];   // per-slot sample-group sums
+  DevBuf<int> spill[kSlots];       // traversal stack entries beyond PT_STACK
+  DevBuf<uint32_t> counter[kSlots];
   int64_t culled_px = 0;         // pixels of the last launch outside the footprint
   DevBuf<float> frame;  // device framebuffer for host-output renders
-  DevBuf<float> partial;  // per-slot sample-group sums
-  DevBuf<int> spill;      // traversal stack entries beyond PT_STACK
-  DevBuf<uint32_t> counter;
+  DevBuf<int> q_spill;  // ray-query stack spill
   DevBuf<unsigned long long> stats;
   DevBuf<float> q_f;    // ray-query scratch
   DevBuf<int32_t> q_i;
@@ -187,9 +202,14 @@ int pt_create(int device, pt_ctx** out) {
   pt_ctx* c = new pt_ctx();
   c->device = device;
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  for (int k = 0; k < pt_ctx::kSlots; ++k) {
+    HIPCHK(hipStreamCreateWithFlags(&c->rstream[k], hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
+    HIPCHK(hipEventRecord(c->ev_free[k], c->stream));
+    HIPCHK(c->counter[k].reserve(PT_QUEUE_WORDS));  // work-queue heads, one 128-B line each
+  }
   for (auto& tri : c->ev)
     for (auto& e : tri) HIPCHK(hipEventCreate(&e));
-  HIPCHK(c->counter.reserve(PT_QUEUE_WORDS));  // work-queue heads, one 128-B line each
   HIPCHK(c->stats.reserve(PT_STATS_SLOTS));
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, device));
@@ -210,6 +230,7 @@ int pt_create(int device, pt_ctx** out) {
 int pt_destroy(pt_ctx* c) {
   if (!c) return PT_OK;
   (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();  // no render of this context may still be running
   c->nodes.release();
   c->nodes2.release();
   c->prim_map.release();
@@ -223,11 +244,17 @@ int pt_destroy(pt_ctx* c) {
   c->norms.release();
   c->bsdfs.release();
   c->lights.release();
-  c->tiles.release();
-  c->blocks.release();
-  c->spill.release();
+  for (int k = 0; k < pt_ctx::kSlots; ++k) {
+    c->tiles[k].release();
+    c->blocks[k].release();
+    c->spill[k].release();
+    c->partial[k].release();
+    c->counter[k].release();
+    if (c->ev_free[k]) (void)hipEventDestroy(c->ev_free[k]);
+    if (c->rstream[k]) (void)hipStreamDestroy(c->rstream[k]);
+  }
+  c->q_spill.release();
   c->frame.release();
-  c->counter.release();
   c->stats.release();
   c->q_f.release();
   c->q_i.release();
@@ -417,6 +444,42 @@ static int build_host_bvh(const pt_scene* s, std::vector<DNode>& dn, std::vector
         if (ch[k].ref >= 0) st.push_back({ch[k].ref, me, k, below});
     }
   }
+  // Breadth-first order (PT_BVH_ORDER=bfs; the default when the kernel
+  // stages a treelet): the top levels become the first nodes, which the
+  // render kernel copies into LDS (PT_TREELET).  Parents still precede their
+  // children, so every reference stays forward.
+  {
+    const char* ord = std::getenv("PT_BVH_ORDER");
+    const bool bfs = ord ? std::strcmp(ord, "bfs") == 0 : PT_TREELET > 0;
+    if (bfs && dn.size() > 1) {
+      std::vector<int> order, newid(dn.size(), -1);
+      order.reserve(dn.size());
+      order.push_back(0);
+      for (size_t q = 0; q < order.size(); ++q) {
+        const DNode& d = dn[(size_t)order[q]];
+        for (int k = 0; k < 4; ++k) {
+          const int r = (&d.ref.x)[k];
+          if (!std::isinf((&d.lox.x)[k]) && r > 0 && r < (int)dn.size() && newid[(size_t)r] < 0) {
+            newid[(size_t)r] = -2;  // queued
+            order.push_back(r);
+          }
+        }
+      }
+      if (order.size() == dn.size()) {
+        for (size_t q = 0; q < order.size(); ++q) newid[(size_t)order[q]] = (int)q;
+        std::vector<DNode> bn(dn.size());
+        for (size_t q = 0; q < order.size(); ++q) {
+          DNode d = dn[(size_t)order[q]];
+          for (int k = 0; k < 4; ++k) {
+            int& r = (&d.ref.x)[k];
+            if (!std::isinf((&d.lox.x)[k]) && r >= 0) r = newid[(size_t)r];
+          }
+          bn[q] = d;
+        }
+        dn.swap(bn);
+      }
+    }
+  }
   // Traversal termination rests on this: node references only point forward
   // (pre-order), so a ray can never re-enter a node it has left.
   for (size_t i = 0; i < dn.size(); ++i)
@@ -495,6 +558,7 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
   if (s->n_lights < 0 || (s->n_lights > 0 && !s->lights)) return fail(PT_E_INVALID, "pt_upload_scene: bad lights");
   if (s->n_prims > (int64_t)0x3fffffff) return fail(PT_E_INVALID, "pt_upload_scene: too many primitives");
   HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipDeviceSynchronize());  // renders in flight read the scene being replaced
 
   // ---- primitives (already in BVH order)
   std::vector<DPrim> prims((size_t)s->n_prims);
@@ -704,24 +768,32 @@ static void screen_footprint(const pt_ctx* c, KParams& P) {
   P.cull_y1 = (int)std::min((double)P.H, std::floor(y1) + 1);
 }
 
+// One render: the render kernel on the slot's render stream, then the resolve
+// on the caller's stream `s` (see pt_ctx: the render pipeline).
 static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStream_t s, uint32_t flags) {
   const bool stats = (flags & (PT_FLAG_STATS | PT_FLAG_REF_COUNTS)) != 0;
   std::memset(&c->last, 0, sizeof(c->last));
   c->times_pending = false;
   if (tl.empty()) return PT_OK;
+  // PT_PIPELINE=0: every render on the caller's stream, one slot (A/B)
+  static const bool pipeline = !std::getenv("PT_PIPELINE") || std::atoi(std::getenv("PT_PIPELINE")) != 0;
+  const int slot = pipeline ? (int)(c->n_launches % pt_ctx::kSlots) : 0;
+  hipStream_t rs = pipeline ? c->rstream[slot] : s;
+  // the slot's device state is free once the previous resolve that read it ran
+  HIPCHK(hipStreamWaitEvent(rs, c->ev_free[slot], 0));
   // the tile list rarely changes between frames: upload it only when it does
-  if (tl.size() != c->tiles_host.size() ||
-      std::memcmp(tl.data(), c->tiles_host.data(), tl.size() * sizeof(int4)) != 0) {
-    c->tiles_host.clear();
-    HIPCHK(c->tiles.reserve(tl.size()));
-    HIPCHK(hipMemcpyAsync(c->tiles.p, tl.data(), tl.size() * sizeof(int4), hipMemcpyHostToDevice, s));
-    c->tiles_host = tl;
+  std::vector<int4>& th = c->tiles_host[slot];
+  if (tl.size() != th.size() || std::memcmp(tl.data(), th.data(), tl.size() * sizeof(int4)) != 0) {
+    th = tl;
+    HIPCHK(c->tiles[slot].reserve(tl.size()));
+    HIPCHK(hipMemcpyAsync(c->tiles[slot].p, th.data(), th.size() * sizeof(int4), hipMemcpyHostToDevice, rs));
   }
-  HIPCHK(hipMemsetAsync(c->counter.p, 0, PT_QUEUE_WORDS * sizeof(uint32_t), s));
+  HIPCHK(hipMemsetAsync(c->counter[slot].p, 0, PT_QUEUE_WORDS * sizeof(uint32_t), rs));
   if (stats) {
     unsigned long long init[PT_STATS_SLOTS] = {0};
     init[21] = init[23] = init[25] = ~0ull;  // atomicMin slots
-    HIPCHK(hipMemcpyAsync(c->stats.p, init, sizeof(init), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->stats.p, init, sizeof(init), hipMemcpyHostToDevice, rs));
+    HIPCHK(hipStreamSynchronize(rs));  // `init` is a stack array
   }
   KParams P;
   std::memset(&P, 0, sizeof(P));
@@ -746,6 +818,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.n_bsdfs = c->n_bsdfs;
   P.n_tiles = (int)tl.size();
   P.nodes = c->nodes.p;
+  P.n_treelet = (int)std::min<size_t>(c->n_nodes4, (size_t)PT_TREELET);
   P.nodes2 = c->nodes2.p;
   P.prims = c->prims.p;
   P.norms = c->norms.p;
@@ -759,10 +832,10 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.env_pdf = c->env_pdf.p;
   P.env_gtheta = c->env_gtheta.p;
   P.env_gphi = c->env_gphi.p;
-  P.tiles = c->tiles.p;
+  P.tiles = c->tiles[slot].p;
   P.out = out_dev;
   P.packed = (flags & PT_FLAG_PACKED) ? 1 : 0;
-  P.work_counter = c->counter.p;
+  P.work_counter = c->counter[slot].p;
   P.stats = c->stats.p;
   P.dbg_pix = -1;
   for (int k = 0; k < 3; ++k) {
@@ -803,15 +876,14 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
       }
   }
   c->culled_px = px_all - px_in;
-  if (bl.size() != c->blocks_host.size() ||
-      std::memcmp(bl.data(), c->blocks_host.data(), bl.size() * sizeof(int4)) != 0) {
-    c->blocks_host.clear();
-    HIPCHK(c->blocks.reserve(bl.size()));
-    if (!bl.empty())
-      HIPCHK(hipMemcpyAsync(c->blocks.p, bl.data(), bl.size() * sizeof(int4), hipMemcpyHostToDevice, s));
-    c->blocks_host = bl;
+  std::vector<int4>& bh = c->blocks_host[slot];
+  if (bl.size() != bh.size() || std::memcmp(bl.data(), bh.data(), bl.size() * sizeof(int4)) != 0) {
+    bh = bl;
+    HIPCHK(c->blocks[slot].reserve(bl.size()));
+    if (!bh.empty())
+      HIPCHK(hipMemcpyAsync(c->blocks[slot].p, bh.data(), bh.size() * sizeof(int4), hipMemcpyHostToDevice, rs));
   }
-  P.blocks = c->blocks.p;
+  P.blocks = c->blocks[slot].p;
   P.n_blocks = (int)bl.size();
   // Work slots are (pixel, group of group_spp samples): small enough that
   // the dynamic queue balances the waves (a whole pixel per slot left the
@@ -849,15 +921,16 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
   if (slots + want * PT_CHUNK_MAX >= (int64_t)UINT32_MAX || npx * P.n_groups >= (int64_t)UINT32_MAX)
     return fail(PT_E_INVALID, "frame too large for one launch");
-  HIPCHK(c->partial.reserve((size_t)(npx * P.n_groups) * 3));
-  P.partial = c->partial.p;
+  HIPCHK(c->partial[slot].reserve((size_t)(npx * P.n_groups) * 3));
+  P.partial = c->partial[slot].p;
   int64_t max_grid = std::max<int64_t>(1, (slots + PT_BLOCK - 1) / PT_BLOCK);
   int grid = (int)std::min<int64_t>(want, max_grid);
   if (stats && (size_t)grid * PT_WAVE_TRACE + PT_STATS_SLOTS > c->stats.n) grid = (int)((c->stats.n - PT_STATS_SLOTS) / PT_WAVE_TRACE);
+  grid = std::max(PT_WG_WAVES, grid - grid % PT_WG_WAVES);  // whole workgroups of PT_WG_WAVES waves
   P.stack_spill = nullptr;
   if (c->bvh_stack > PT_STACK) {  // worst-case depth beyond the LDS stack
-    HIPCHK(c->spill.reserve((size_t)(c->bvh_stack - PT_STACK) * grid * PT_BLOCK));
-    P.stack_spill = c->spill.p;
+    HIPCHK(c->spill[slot].reserve((size_t)(c->bvh_stack - PT_STACK) * grid * PT_BLOCK));
+    P.stack_spill = c->spill[slot].p;
   }
   {
     hipEvent_t* tri = c->ev[c->n_launches % pt_ctx::kRing];
@@ -866,11 +939,13 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     c->ev2 = tri[2];
     ++c->n_launches;
   }
-  HIPCHK(hipEventRecord(c->ev0, s));
-  HIPCHK(ptk_launch_render(&P, grid, stats, (flags & PT_FLAG_REF_COUNTS) != 0, s));
-  HIPCHK(hipEventRecord(c->ev1, s));
+  HIPCHK(hipEventRecord(c->ev0, rs));
+  HIPCHK(ptk_launch_render(&P, grid, stats, (flags & PT_FLAG_REF_COUNTS) != 0, rs));
+  HIPCHK(hipEventRecord(c->ev1, rs));
+  if (rs != s) HIPCHK(hipStreamWaitEvent(s, c->ev1, 0));  // the resolve reads the finished group sums
   HIPCHK(ptk_launch_resolve(&P, s));
   HIPCHK(hipEventRecord(c->ev2, s));
+  HIPCHK(hipEventRecord(c->ev_free[slot], s));
   c->last.grid_blocks = grid;
   c->last.group_spp = P.group_spp;
   c->last.blocks_per_cu = stats ? c->bpc_stats : c->bpc_plain;
@@ -1028,8 +1103,8 @@ int pt_intersect(pt_ctx* c, int64_t n, const double* o, const double* d, const d
   int32_t* da = c->q_i.p + 2 * n;
   int* spill = nullptr;
   if (c->bvh_stack > PT_STACK) {
-    HIPCHK(c->spill.reserve((size_t)(c->bvh_stack - PT_STACK) * (size_t)((n + PT_BLOCK - 1) / PT_BLOCK * PT_BLOCK)));
-    spill = c->spill.p;
+    HIPCHK(c->q_spill.reserve((size_t)(c->bvh_stack - PT_STACK) * (size_t)((n + PT_BLOCK - 1) / PT_BLOCK * PT_BLOCK)));
+    spill = c->q_spill.p;
   }
   HIPCHK(ptk_launch_intersect(c->nodes.p, c->prims.p, c->q_f.p, c->q_f.p + 3 * n, c->q_f.p + 6 * n, n, dh, dt, dp, da,
                               spill, c->prim_map.p, c->stream));

@@ -7,6 +7,12 @@
 #ifndef PT_BLOCK
 #define PT_BLOCK 64  // one wave64 per workgroup: the persistent queue is per wave
 #endif
+#ifndef PT_WG_WAVES
+#define PT_WG_WAVES 1  // waves per render workgroup (> 1: the workgroup shares an LDS treelet)
+#endif
+#ifndef PT_TREELET
+#define PT_TREELET 0  // BVH4 nodes (the first ones, breadth-first: the top levels) staged in LDS
+#endif
 #ifndef PT_CHUNK
 #define PT_CHUNK 128  // smallest claim of work slots a wave takes from the queue per atomic
 #endif
@@ -130,6 +136,7 @@ struct KParams {
   int n_blocks;
   uint32_t* work_counter;
   unsigned long long* stats;  // counters (PT_FLAG_STATS / PT_FLAG_REF_COUNTS)
+  int n_treelet;               // BVH4 nodes [0, n_treelet) read from the workgroup's LDS copy
   int* stack_spill;           // traversal stack entries beyond PT_STACK (null if the BVH never needs them)
   int dbg_pix;                // diagnostic printf trace of one pixel (-1: off)
   int shade_batch;            // leave the traversal phase once this many lanes finished their ray

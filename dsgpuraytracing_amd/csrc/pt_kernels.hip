@@ -321,9 +321,22 @@ __device__ __forceinline__ bool node_order(const Stack& stk, Trav& tr, const flo
 #define PT_OCTANT 1
 #endif
 
-template <bool STATS, bool FENCE = (PT_LOAD_FENCE & 1) != 0, bool OCT = PT_OCTANT != 0>
+typedef __attribute__((address_space(3))) const char lds_cchar;
+typedef float pt_v4f __attribute__((ext_vector_type(4)));
+typedef int pt_v4i __attribute__((ext_vector_type(4)));
+// 16-B LDS loads (ds_read_b128) into HIP vector types
+__device__ __forceinline__ float4 lds_f4(lds_cchar* p) {
+  const pt_v4f v = *(__attribute__((address_space(3))) const pt_v4f*)p;
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ int4 lds_i4(lds_cchar* p) {
+  const pt_v4i v = *(__attribute__((address_space(3))) const pt_v4i*)p;
+  return make_int4(v.x, v.y, v.z, v.w);
+}
+
+template <bool STATS, bool FENCE = (PT_LOAD_FENCE & 1) != 0, bool OCT = PT_OCTANT != 0, bool TREE = false>
 __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, const Stack& stk, Trav& tr,
-                                          Counters& ct) {
+                                          Counters& ct, lds_cchar* tree = nullptr, int n_tree = 0) {
   const float kRobust = PT_ROBUST;
   const float3 o = tr.o, inv = tr.inv;
   const float kMiss = 3.0e38f;
@@ -338,13 +351,28 @@ __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, const
     const uint32_t base = (uint32_t)tr.node << 7;
     const uint32_t sx = (__float_as_uint(inv.x) >> 27) & 16u, sy = (__float_as_uint(inv.y) >> 27) & 16u,
                    sz = (__float_as_uint(inv.z) >> 27) & 16u;
-    float4 nx = *(const float4*)(nb + (base + sx)), fx = *(const float4*)(nb + (base + (sx ^ 16u)));
-    float4 ny = *(const float4*)(nb + (base + 32u + sy)), fy = *(const float4*)(nb + (base + 32u + (sy ^ 16u)));
-    float4 nz = *(const float4*)(nb + (base + 64u + sz)), fz = *(const float4*)(nb + (base + 64u + (sz ^ 16u)));
-    int4 rf = *(const int4*)(nb + (base + 96u));
-    if (FENCE) {
-      PT_FENCE4(fz);
-      PT_FENCE4(rf);
+    float4 nx, fx, ny, fy, nz, fz;
+    int4 rf;
+    if (TREE && tr.node < n_tree) {  // top levels: the workgroup's LDS copy (ds_read_b128)
+      nx = lds_f4(tree + (base + sx));
+      fx = lds_f4(tree + (base + (sx ^ 16u)));
+      ny = lds_f4(tree + (base + 32u + sy));
+      fy = lds_f4(tree + (base + 32u + (sy ^ 16u)));
+      nz = lds_f4(tree + (base + 64u + sz));
+      fz = lds_f4(tree + (base + 64u + (sz ^ 16u)));
+      rf = lds_i4(tree + (base + 96u));
+    } else {
+      nx = *(const float4*)(nb + (base + sx));
+      fx = *(const float4*)(nb + (base + (sx ^ 16u)));
+      ny = *(const float4*)(nb + (base + 32u + sy));
+      fy = *(const float4*)(nb + (base + 32u + (sy ^ 16u)));
+      nz = *(const float4*)(nb + (base + 64u + sz));
+      fz = *(const float4*)(nb + (base + 64u + (sz ^ 16u)));
+      rf = *(const int4*)(nb + (base + 96u));
+      if (FENCE) {
+        PT_FENCE4(fz);
+        PT_FENCE4(rf);
+      }
     }
     if (STATS) ct.nodes++;
     const float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
@@ -590,12 +618,24 @@ enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 // memory; the common build reads them from LDS through address-space-typed
 // pointers, never through FLAT accesses).
 template <bool STATS, bool DBG, bool BIN, bool ENV, bool GTAB>
-__global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel(KParams P) {
-  __shared__ int s_stack[PT_STACK * PT_BLOCK];
+__global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void render_kernel(KParams P) {
+  // one PT_STACK x 64 region of the LDS stack per wave (lane-contiguous rows)
+  __shared__ int s_stack[PT_WG_WAVES * PT_STACK * PT_BLOCK];
   const int lane = threadIdx.x & 63;
-  const uint32_t gid = blockIdx.x * PT_BLOCK + threadIdx.x;
-  const Stack stk{(lds_int*)(s_stack + threadIdx.x), P.stack_spill ? P.stack_spill + gid : nullptr,
-                  gridDim.x * PT_BLOCK};
+  const uint32_t wave_id = blockIdx.x * PT_WG_WAVES + (threadIdx.x >> 6);  // the persistent wave
+  const uint32_t n_waves = gridDim.x * PT_WG_WAVES;
+  const uint32_t gid = wave_id * PT_BLOCK + lane;
+  const Stack stk{(lds_int*)(s_stack + (threadIdx.x >> 6) * (PT_STACK * PT_BLOCK) + lane),
+                  P.stack_spill ? P.stack_spill + gid : nullptr, n_waves * PT_BLOCK};
+  // BVH4 treelet: the first n_treelet nodes (the top levels, breadth-first
+  // order) copied once per workgroup; node steps on them read LDS
+  __shared__ DNode s_tree[PT_TREELET > 0 ? PT_TREELET : 1];
+  if (PT_TREELET > 0) {
+    const int nt = min(P.n_treelet, PT_TREELET) * (int)(sizeof(DNode) / 16);
+    for (int k = threadIdx.x; k < nt; k += PT_BLOCK * PT_WG_WAVES)
+      ((float4*)s_tree)[k] = ((const float4*)P.nodes)[k];
+  }
+  const int n_tree = PT_TREELET > 0 ? min(P.n_treelet, PT_TREELET) : 0;
 
   // Material and light tables are read by every shading step: keep small
   // ones in LDS (the usual case); larger ones stay in global memory.
@@ -604,9 +644,9 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   typedef __attribute__((address_space(3))) const float lds_f;
   if (!GTAB) {
     const int nb = P.n_bsdfs * (int)(sizeof(DBsdf) / 4);
-    for (int k = lane; k < nb; k += PT_BLOCK) ((float*)s_bsdf)[k] = ((const float*)P.bsdfs)[k];
+    for (int k = threadIdx.x; k < nb; k += PT_BLOCK * PT_WG_WAVES) ((float*)s_bsdf)[k] = ((const float*)P.bsdfs)[k];
     const int nl = P.n_lights * (int)(sizeof(DLight) / 4);
-    for (int k = lane; k < nl; k += PT_BLOCK) ((float*)s_light)[k] = ((const float*)P.lights)[k];
+    for (int k = threadIdx.x; k < nl; k += PT_BLOCK * PT_WG_WAVES) ((float*)s_light)[k] = ((const float*)P.lights)[k];
   }
   // Table fields are read where they are used (address-space-typed ds_read
   // loads in the LDS build), never copied whole into registers: every value
@@ -997,7 +1037,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             nbase = total_slots;
           } else {
             const uint32_t left = total_slots - seen;
-            csize = min((uint32_t)PT_CHUNK_MAX, max((uint32_t)PT_CHUNK, left / (PT_CHUNK_DIV * gridDim.x))) & ~63u;
+            csize = min((uint32_t)PT_CHUNK_MAX, max((uint32_t)PT_CHUNK, left / (PT_CHUNK_DIV * n_waves))) & ~63u;
             if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
             nbase = __builtin_amdgcn_readfirstlane(__shfl(nbase, 0));  // wave-uniform: an SGPR
             seen = nbase + csize;
@@ -1121,7 +1161,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           if constexpr (BIN) done = node_step2<STATS>(P.nodes2, stk, tr, ct);
           // (the ENV build spills registers with the node fence or the
           // octant loads: without)
-          else done = node_step<STATS, (PT_LOAD_FENCE & 1) != 0 && !ENV, PT_OCTANT != 0 && !ENV>(P.nodes, stk, tr, ct);
+          else done = node_step<STATS, (PT_LOAD_FENCE & 1) != 0 && !ENV, PT_OCTANT != 0 && !ENV,
+                                (PT_TREELET > 0) && !ENV>(P.nodes, stk, tr, ct, (lds_cchar*)s_tree, n_tree);
         }
       }
       if (done) mode = M_SHADE;
@@ -1190,7 +1231,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       atomicMax(P.stats + 15, w);
       // per-wave trace (pt_get_wave_trace): start, first empty queue, end,
       // (XCC id << 32 | HW_ID), camera samples
-      unsigned long long* tw = P.stats + PT_STATS_SLOTS + PT_WAVE_TRACE * (size_t)blockIdx.x;
+      unsigned long long* tw = P.stats + PT_STATS_SLOTS + PT_WAVE_TRACE * (size_t)wave_id;
       tw[0] = w_start;
       tw[1] = w_empty;
       tw[2] = w_end;
@@ -1272,15 +1313,17 @@ __global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __rest
 
 // ------------------------------------------------------------------ launchers
 template <bool ENV, bool GTAB>
-static void launch_render(const KParams* P, int grid, bool stats, bool ref_counts, hipStream_t s) {
+static void launch_render(const KParams* P, int waves, bool stats, bool ref_counts, hipStream_t s) {
+  const int grid = (waves + PT_WG_WAVES - 1) / PT_WG_WAVES;  // workgroups of PT_WG_WAVES waves
+  const dim3 blk(PT_BLOCK * PT_WG_WAVES);
   if (ref_counts)
-    hipLaunchKernelGGL((ptk::render_kernel<true, false, true, ENV, GTAB>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+    hipLaunchKernelGGL((ptk::render_kernel<true, false, true, ENV, GTAB>), dim3(grid), blk, 0, s, *P);
   else if (P->dbg_pix >= 0)
-    hipLaunchKernelGGL((ptk::render_kernel<false, true, false, ENV, GTAB>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+    hipLaunchKernelGGL((ptk::render_kernel<false, true, false, ENV, GTAB>), dim3(grid), blk, 0, s, *P);
   else if (stats)
-    hipLaunchKernelGGL((ptk::render_kernel<true, false, false, ENV, GTAB>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+    hipLaunchKernelGGL((ptk::render_kernel<true, false, false, ENV, GTAB>), dim3(grid), blk, 0, s, *P);
   else
-    hipLaunchKernelGGL((ptk::render_kernel<false, false, false, ENV, GTAB>), dim3(grid), dim3(PT_BLOCK), 0, s, *P);
+    hipLaunchKernelGGL((ptk::render_kernel<false, false, false, ENV, GTAB>), dim3(grid), blk, 0, s, *P);
 }
 
 extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, bool ref_counts, hipStream_t s) {
@@ -1312,10 +1355,13 @@ extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prim
   return hipGetLastError();
 }
 
-extern "C" hipError_t ptk_render_occupancy(int* blocks_per_cu, bool stats) {
-  if (stats)
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ptk::render_kernel<true, false, false, false, false>,
-                                                        PT_BLOCK, 0);
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ptk::render_kernel<false, false, false, false, false>,
-                                                      PT_BLOCK, 0);
+// Resident render WAVES per CU (workgroups per CU x PT_WG_WAVES).
+extern "C" hipError_t ptk_render_occupancy(int* waves_per_cu, bool stats) {
+  int blocks = 0;
+  hipError_t e = stats ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                             &blocks, ptk::render_kernel<true, false, false, false, false>, PT_BLOCK * PT_WG_WAVES, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                             &blocks, ptk::render_kernel<false, false, false, false, false>, PT_BLOCK * PT_WG_WAVES, 0);
+  *waves_per_cu = blocks * PT_WG_WAVES;
+  return e;
 }
