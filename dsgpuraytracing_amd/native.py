@@ -124,6 +124,23 @@ _SIGS = {
 _lib = None
 
 
+def _init_torch_hip_first():
+    """PyTorch-ROCm wheels bundle their own HIP runtime beside the system one
+    this library links (/opt/rocm).  In one process the two coexist only if
+    torch's initialises first: after ours has opened the device, torch reports
+    "No HIP GPUs are available".  So when torch is already imported, its HIP
+    state is initialised before this library is loaded (a no-op without a GPU)."""
+    import sys
+    torch = sys.modules.get("torch")
+    if torch is None:
+        return
+    try:
+        if torch.cuda.device_count() > 0:
+            torch.cuda.init()
+    except Exception:  # no GPU / CPU-only torch: nothing to order
+        pass
+
+
 def lib():
     """Load libptgpu.so (once).  Raises NativeLibraryError if it is absent.
     PT_LIB=<path> loads another build of the same library instead (A/B
@@ -133,6 +150,7 @@ def lib():
         return _lib
     if os.environ.get("PT_LIB"):
         LIB_PATH = os.path.abspath(os.environ["PT_LIB"])
+    _init_torch_hip_first()
     if not os.path.exists(LIB_PATH):
         raise NativeLibraryError(
             f"{LIB_PATH} is missing: build it with `python -m dsgpuraytracing_amd.build` "

@@ -16,6 +16,16 @@ def pytest_configure(config):
 _LAST = ("test_gpu_fullsize.py",)
 
 
+def pytest_runtest_setup(item):
+    """GPU tests mix libptgpu.so (system HIP runtime) with torch (its own
+    bundled HIP runtime): torch's must initialise first (see
+    dsgpuraytracing_amd.native._init_torch_hip_first), whatever the test order."""
+    if item.get_closest_marker("gpu") is not None:
+        import torch
+        if torch.cuda.device_count() > 0:
+            torch.cuda.init()
+
+
 def pytest_collection_modifyitems(config, items):
     """Cheap GPU parity cases first, full-size BASELINE configs last, so a
     `-x` run reports the small HIP-vs-oracle cases before the long ones."""
