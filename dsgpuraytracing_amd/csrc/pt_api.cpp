@@ -166,7 +166,8 @@ struct pt_ctx {
   std::vector<int4> tiles_host[kSlots];  // what `tiles` holds
   DevBuf<int4> blocks[kSlots];           // footprint-clipped 8x8 pixel blocks of the tiles
   std::vector<int4> blocks_host[kSlots];
-  DevBuf<float> partial[kSlots];   // per-slot sample-group sums
+  DevBuf<float> partial[kSlots];   // per-slot sample-group sums (PT_PIXEL_ACC 0)
+  DevBuf<float> fb[kSlots];        // per-slot pixel means written by the render (PT_PIXEL_ACC 1)
   DevBuf<int> spill[kSlots];       // traversal stack entries beyond PT_STACK
   DevBuf<uint32_t> counter[kSlots];
   int64_t culled_px = 0;         // pixels of the last launch outside the footprint
@@ -249,6 +250,7 @@ int pt_destroy(pt_ctx* c) {
     c->blocks[k].release();
     c->spill[k].release();
     c->partial[k].release();
+    c->fb[k].release();
     c->counter[k].release();
     if (c->ev_free[k]) (void)hipEventDestroy(c->ev_free[k]);
     if (c->rstream[k]) (void)hipStreamDestroy(c->rstream[k]);
@@ -556,6 +558,7 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
     return fail(PT_E_INVALID, "pt_upload_scene: empty scene");
   if (s->n_bsdfs <= 0 || !s->bsdfs) return fail(PT_E_INVALID, "pt_upload_scene: no BSDFs");
   if (s->n_lights < 0 || (s->n_lights > 0 && !s->lights)) return fail(PT_E_INVALID, "pt_upload_scene: bad lights");
+  if (s->n_lights > 65535) return fail(PT_E_INVALID, "pt_upload_scene: more than 65535 lights");
   if (s->n_prims > (int64_t)0x3fffffff) return fail(PT_E_INVALID, "pt_upload_scene: too many primitives");
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipDeviceSynchronize());  // renders in flight read the scene being replaced
@@ -701,6 +704,8 @@ int pt_set_params(pt_ctx* c, const pt_params* p) {
   if (!c || !p) return fail(PT_E_INVALID, "pt_set_params: NULL argument");
   if (p->width <= 0 || p->height <= 0 || p->spp <= 0 || p->max_depth < 0 || p->ns_area_light <= 0)
     return fail(PT_E_INVALID, "pt_set_params: width/height/spp/ns_area_light must be positive, max_depth >= 0");
+  if (p->max_depth > 254 || p->ns_area_light > 255)  // packed in 8 bits each in the kernel's path state
+    return fail(PT_E_INVALID, "pt_set_params: max_depth must be <= 254 and ns_area_light <= 255");
   if ((int64_t)p->width * p->height > (int64_t)1 << 30) return fail(PT_E_INVALID, "pt_set_params: frame too large");
   c->params = *p;
   c->have_params = true;
@@ -908,9 +913,25 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     if (v > 0) P.group_spp = v;
   }
   P.group_spp = std::min(P.group_spp, P.spp);
+  const int64_t npx = (int64_t)P.W * P.H;
+#if PT_PIXEL_ACC
+  // On-chip pixel sums: a pixel is either one work slot (its lane renders
+  // every sample) or >= 16 slots (a wave's chunk then holds at most 8 pixels
+  // of its PT_RING-pixel accumulator ring).  The grouping no longer decides
+  // any pixel's value: the ring sums in exact fixed point.
+  P.n_groups = (P.spp + P.group_spp - 1) / P.group_spp;
+  if (P.n_groups > 1 && P.n_groups < 16) {
+    P.group_spp = P.spp;
+    P.n_groups = 1;
+  }
+  const int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
+  if (slots + want * std::max<int64_t>(PT_CHUNK_MAX, P.n_groups) >= (int64_t)UINT32_MAX)
+    return fail(PT_E_INVALID, "frame too large for one launch");
+  HIPCHK(c->fb[slot].reserve((size_t)npx * 3));
+  P.fb = c->fb[slot].p;
+#else
   // 32-bit slot and partial indices (the queue head may overshoot by one
   // chunk per wave); the per-pixel group sums stay within 4 GiB
-  const int64_t npx = (int64_t)P.W * P.H;
   for (;;) {
     P.n_groups = (P.spp + P.group_spp - 1) / P.group_spp;
     int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
@@ -923,6 +944,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     return fail(PT_E_INVALID, "frame too large for one launch");
   HIPCHK(c->partial[slot].reserve((size_t)(npx * P.n_groups) * 3));
   P.partial = c->partial[slot].p;
+#endif
   int64_t max_grid = std::max<int64_t>(1, (slots + PT_BLOCK - 1) / PT_BLOCK);
   int grid = (int)std::min<int64_t>(want, max_grid);
   if (stats && (size_t)grid * PT_WAVE_TRACE + PT_STATS_SLOTS > c->stats.n) grid = (int)((c->stats.n - PT_STATS_SLOTS) / PT_WAVE_TRACE);

@@ -13,6 +13,14 @@
 #ifndef PT_TREELET
 #define PT_TREELET 0  // BVH4 nodes (the first ones, breadth-first: the top levels) staged in LDS
 #endif
+#ifndef PT_PIXEL_ACC
+#define PT_PIXEL_ACC 0  // 1: pixel sums accumulated on chip (per-wave LDS ring, fixed point); 0: group sums in HBM
+#endif
+#ifndef PT_RING
+#define PT_RING 32  // pixels per wave's accumulator ring (power of two)
+#endif
+#define PT_RING_FREE 0xffffffffu
+static_assert((PT_RING & (PT_RING - 1)) == 0 && PT_RING >= 16 && PT_RING <= 64, "PT_RING: power of two in [16, 64]");
 #ifndef PT_CHUNK
 #define PT_CHUNK 128  // smallest claim of work slots a wave takes from the queue per atomic
 #endif
@@ -28,6 +36,7 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #endif
 #define PT_QUEUE_WORDS (32 * 8)  // queue heads 128 B apart (room for 8)
 static_assert(PT_XCD_QUEUES >= 1 && PT_XCD_QUEUES <= 8, "at most 8 queues");
+static_assert(!(PT_PIXEL_ACC && PT_XCD_QUEUES > 1), "the pixel ring needs the single work queue");
 #ifndef PT_GROUP_SPP
 #define PT_GROUP_SPP 2  // default samples per work slot
 #endif
@@ -82,6 +91,16 @@ struct alignas(16) DPrim {
   float4 v0, e1, e2;
 };
 
+// One pixel's accumulator in a wave's LDS ring (PT_PIXEL_ACC): the sums of
+// its samples in unsigned 32.32 fixed point (exact, so any order and any
+// grouping of the samples gives the same bits), the samples counted so far,
+// and whether the slot is taken.
+struct alignas(16) PxAcc {
+  unsigned long long s[3];
+  uint32_t count;
+  uint32_t owner;
+};
+
 struct alignas(16) DBsdf {
   int type;
   float a[3];  // albedo / reflectance
@@ -131,7 +150,8 @@ struct KParams {
   const int4* tiles;  // (x, y, w, h)
   float* out;         // W*H*3, or n_tiles*1024*3 when packed
   int packed;         // PT_FLAG_PACKED: tile i's pixel (x, y) -> out[3 * (i*1024 + (y-ty)*32 + (x-tx))]
-  float* partial;     // W*H*n_groups*3: each sample group's sum, resolved into `out` in group order
+  float* partial;     // PT_PIXEL_ACC 0: W*H*n_groups*3, each sample group's sum, resolved into `out` in group order
+  float* fb;          // PT_PIXEL_ACC 1: W*H*3, each traced pixel's mean, written by the lane completing it
   const int4* blocks;  // (x, y, w<=8, h<=8): footprint-clipped pixel blocks of the tiles
   int n_blocks;
   uint32_t* work_counter;

@@ -369,6 +369,12 @@ __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, const
       nz = *(const float4*)(nb + (base + 64u + sz));
       fz = *(const float4*)(nb + (base + 64u + (sz ^ 16u)));
       rf = *(const int4*)(nb + (base + 96u));
+#if PT_DIAG_EXTRA_LOAD
+      // diagnostic only: one more 16-B load per node step (the node's pad),
+      // to measure how the kernel's time responds to vector-memory traffic
+      int4 px = *(const int4*)(nb + (base + 112u));
+      asm volatile("" ::"v"(px.x), "v"(px.y), "v"(px.z), "v"(px.w));
+#endif
       if (FENCE) {
         PT_FENCE4(fz);
         PT_FENCE4(rf);
@@ -596,6 +602,20 @@ __device__ __forceinline__ void env_sample(const KParams& P, float r1, float r2,
   wi = f3(-st * sp, ct, st * cp);
 }
 
+// Unsigned 32.32 fixed point of a sample's radiance (PT_PIXEL_ACC): integer
+// sums are exact, so a pixel's value does not depend on the order or grouping
+// in which its samples are added.  Clamped to [0, 2^31) (NaN -> 0); the
+// fraction is truncated at 2^-32.
+__device__ __forceinline__ unsigned long long to_fixed32(float v) {
+  v = fminf(fmaxf(v, 0.0f), 2147483520.0f);
+  const uint32_t hi = (uint32_t)v;
+  const uint32_t lo = (uint32_t)((v - (float)hi) * 4294967296.0f);
+  return ((unsigned long long)hi << 32) | lo;
+}
+typedef __attribute__((address_space(3))) PxAcc lds_acc;
+typedef __attribute__((address_space(3))) unsigned long long lds_u64;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
 #ifndef PT_DRAIN_NO_ATOMIC
 #define PT_DRAIN_NO_ATOMIC 1
 #endif
@@ -661,6 +681,19 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
   };
 #define PT_BSDF3(i, field) f3(bsdf_f(i, offsetof(DBsdf, field) / 4), bsdf_f(i, offsetof(DBsdf, field) / 4 + 1), bsdf_f(i, offsetof(DBsdf, field) / 4 + 2))
 #define PT_LIGHT3(i, field) f3(light_f(i, offsetof(DLight, field) / 4), light_f(i, offsetof(DLight, field) / 4 + 1), light_f(i, offsetof(DLight, field) / 4 + 2))
+#if PT_PIXEL_ACC
+  // The wave's ring of pixel accumulators: a pixel's samples are summed on
+  // chip and the lane that completes the pixel writes its mean, so no
+  // per-group sums go through HBM.  A wave claims whole pixels (every group
+  // of a pixel is rendered by this wave) and only when the ring has room.
+  __shared__ PxAcc s_ring[PT_WG_WAVES * PT_RING];
+  lds_acc* const ring = (lds_acc*)(s_ring + (threadIdx.x >> 6) * PT_RING);
+  if (lane < PT_RING) {
+    ring[lane].s[0] = ring[lane].s[1] = ring[lane].s[2] = 0ull;
+    ring[lane].count = 0u;
+    ring[lane].owner = PT_RING_FREE;
+  }
+#endif
   __syncthreads();
 
   // ---- per-lane state
@@ -669,15 +702,21 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
   // the work slot (pixel, sample group) this lane renders: its pixel and
   // current sample; the group is sample / group_spp
   int pix = 0, sample = 0;
+#if PT_PIXEL_ACC
+  int rslot = 0;  // the pixel's accumulator in the wave's ring
+#endif
   uint32_t rbase = 0, rdim = 0;
   float3 acc = f3(0, 0, 0);  // the slot's radiance sum: each path contribution is added as it is found
   float3 T = f3(1, 1, 1);    // path throughput
-  int depth = 0;
+  // path depth (bits 0-7) and the NEE cursor: light sample (8-15), light
+  // index (16-31), packed in one register -- they persist across traversal,
+  // where every register counts (max_depth <= 254, ns_area_light <= 255,
+  // lights < 65536: pt_set_params / pt_upload_scene check)
+  uint32_t cur = 0;
   bool includeLe = true;
   // shading record of the current path vertex
   float3 hp = f3(0, 0, 0), ns = f3(0, 0, 1), ng = f3(0, 0, 1);
   int bsdf = 0;
-  int li = 0, ls = 0;         // NEE cursor: light index, light sample index
   float3 pend = f3(0, 0, 0);  // NEE contribution awaiting its shadow ray
   Trav tr;
   trav_init(tr, f3(0, 0, 0), f3(0, 0, 1), 0.0f, false);
@@ -691,6 +730,11 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
   uint32_t n_atomics = 0;              // work-queue atomics (lane 0)
   uint32_t chunk_next = 0, chunk_end = 0;  // the wave's private range of work slots
   uint32_t seen = 0;                       // queue head after this wave's last claim
+#if PT_PIXEL_ACC
+  // ring bookkeeping (wave-uniform): the ring position of the next claimed
+  // pixel, and of the current chunk's first pixel + that chunk's first slot
+  uint32_t px_seq = 0, cur_px = 0, cur_first = 0, old_px = 0, old_first = 0;
+#endif
 #if PT_XCD_QUEUES > 1
   // the wave's current queue (its XCD's first) and how many it found exhausted
   uint32_t qcur = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) % PT_XCD_QUEUES, qtried = 0;
@@ -718,10 +762,40 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
   }
 
   const uint32_t n_groups = (uint32_t)P.n_groups;
+#if PT_PIXEL_ACC
+  // A sample of this lane's pixel finished (`sample` already advanced).  The
+  // lane sums its group's samples in float (in sample order, as the group
+  // layout fixed per frame dictates); at the end of the group, one-group
+  // pixels (the lane rendered every sample) write the mean, otherwise the
+  // group sum goes into the ring in exact fixed point and the lane that
+  // brings the pixel's count of groups to n_groups writes its mean.
+  auto sample_done = [&]() {
+    if (sample < P.spp && sample % P.group_spp != 0) return;  // the group goes on
+    if (n_groups == 1u) {
+      store3(P.fb + 3 * (size_t)pix, acc * (float)(1.0 / (double)P.spp));
+      return;
+    }
+    __hip_atomic_fetch_add((lds_u64*)&ring[rslot].s[0], to_fixed32(acc.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add((lds_u64*)&ring[rslot].s[1], to_fixed32(acc.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add((lds_u64*)&ring[rslot].s[2], to_fixed32(acc.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t done = __hip_atomic_fetch_add((lds_u32*)&ring[rslot].count, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (done == n_groups - 1u) {  // the pixel's last group: every add above is in
+      const double k = 2.3283064365386963e-10 / (double)P.spp;  // 2^-32 / spp
+      store3(P.fb + 3 * (size_t)pix, f3((float)((double)ring[rslot].s[0] * k), (float)((double)ring[rslot].s[1] * k),
+                                        (float)((double)ring[rslot].s[2] * k)));
+      ring[rslot].s[0] = ring[rslot].s[1] = ring[rslot].s[2] = 0ull;
+      ring[rslot].count = 0u;
+      ring[rslot].owner = PT_RING_FREE;
+    }
+    acc = f3(0, 0, 0);
+  };
+#else
   // partial-sum slot of a finished group: (pixel, group of the last sample)
   auto slot_of = [&](int p, int s_next) -> size_t {
     return (size_t)p * n_groups + (uint32_t)((s_next - 1) / P.group_spp);
   };
+#endif
   const uint32_t total_slots = (uint32_t)P.n_blocks * 64u * n_groups;
   // first slot of queue part q (part PT_XCD_QUEUES ends at total_slots)
   auto q_start = [&](uint32_t q) -> uint32_t {
@@ -785,9 +859,8 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         if ((meta & 1) && dot(tr.d, ns) > 0.0f) ns = f3(0, 0, 0) - ns;
         ng = normalize(ng);
         if (includeLe) acc = acc + mul(T, PT_BSDF3(bsdf, e));
-        if (DBG && pix == P.dbg_pix) printf("  depth %d hit prim %d bsdf %d t=%.9g n=(%.6g %.6g %.6g) T=(%.5g)\n", depth, tr.prim, bsdf, tr.tmax, ns.x, ns.y, ns.z, T.x);
-        li = 0;
-        ls = 0;
+        if (DBG && pix == P.dbg_pix) printf("  depth %d hit prim %d bsdf %d t=%.9g n=(%.6g %.6g %.6g) T=(%.5g)\n", (int)(cur & 0xffu), tr.prim, bsdf, tr.tmax, ns.x, ns.y, ns.z, T.x);
+        cur &= 0xffu;  // NEE starts at light 0, sample 0
         stage = 0;
       }
       PT_STAMP(0);
@@ -796,6 +869,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         const Frame fr = make_frame(ns);
         bool emitted = false;
         // ---- next-event estimation over all lights (pathtracer.cpp:469-523)
+        int li = (int)(cur >> 16), ls = (int)((cur >> 8) & 0xffu);
         while (li < P.n_lights) {
           const int ltype = __float_as_int(light_f(li, 0));
           const bool delta = ltype == 0 || ltype == 2;
@@ -858,11 +932,12 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
           if (STATS) n_shadow++;
           break;
         }
+        cur = (cur & 0xffu) | ((uint32_t)ls << 8) | ((uint32_t)li << 16);
         PT_STAMP(1);
         if (emitted) {
           shadow = true;
           mode = M_TRAV;
-        } else if (depth >= P.max_depth) {
+        } else if ((int)(cur & 0xffu) >= P.max_depth) {
           finish = true;
         } else {
           // ---- indirect bounce (pathtracer.cpp:527-552)
@@ -929,7 +1004,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
             float3 v = normalize(fr.to_world(wi));
             trav_init(tr, offset_ray(hp, dot(v, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng), v, 3.0e38f, false);
             includeLe = btype == 1 || btype == 2 || btype == 3;
-            ++depth;
+            ++cur;  // depth + 1
             shadow = false;
             mode = M_TRAV;
             if (STATS) n_bounce++;
@@ -939,10 +1014,15 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
       PT_STAMP(2);
       if (finish) {
         ++sample;
+#if PT_PIXEL_ACC
+        sample_done();
+#endif
         if (sample < P.spp && sample % P.group_spp != 0) {
           mode = M_CAMERA;
         } else {
+#if !PT_PIXEL_ACC
           store3(P.partial + 3 * slot_of(pix, sample), acc);
+#endif
           PT_SLOT_DONE();
           mode = M_FETCH;
         }
@@ -961,6 +1041,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
     for (;;) {
       bool need = mode == M_FETCH;
       unsigned long long m = __ballot(need);
+      bool blocked = false;  // PT_PIXEL_ACC: the ring has no room for a new chunk's pixels
       if (m != 0ull) {
         // Lanes are served from the wave's private chunk of consecutive slots;
         // one atomic refills it.  Guided self-scheduling: a chunk is about
@@ -1027,6 +1108,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
           chunk_next += cnt;
         }
 #else
+        bool claimed = false;  // PT_PIXEL_ACC: this refill took a new chunk (the ring bookkeeping moved)
         if (cnt > avail) {
           if (PT_DRAIN_NO_ATOMIC && seen >= total_slots) {
             // This wave already saw the queue drained: every further claim
@@ -1038,16 +1120,53 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
           } else {
             const uint32_t left = total_slots - seen;
             csize = min((uint32_t)PT_CHUNK_MAX, max((uint32_t)PT_CHUNK, left / (PT_CHUNK_DIV * n_waves))) & ~63u;
-            if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
-            nbase = __builtin_amdgcn_readfirstlane(__shfl(nbase, 0));  // wave-uniform: an SGPR
-            seen = nbase + csize;
-            if (STATS) n_atomics += lane == 0;
+#if PT_PIXEL_ACC
+            uint32_t k_px = 0;  // pixels of the new chunk
+            if (n_groups > 1u) {
+              // whole pixels per chunk (every chunk starts on a pixel), and
+              // only when their ring slots are free
+              csize = (csize + n_groups - 1u) / n_groups * n_groups;
+              k_px = csize / n_groups;
+              const bool busy = lane < (int)k_px && ring[(px_seq + (uint32_t)lane) & (PT_RING - 1)].owner != PT_RING_FREE;
+              blocked = __ballot(busy) != 0ull;
+            }
+            if (!blocked) {
+#endif
+              if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
+              nbase = __builtin_amdgcn_readfirstlane(__shfl(nbase, 0));  // wave-uniform: an SGPR
+              seen = nbase + csize;
+              if (STATS) n_atomics += lane == 0;
+#if PT_PIXEL_ACC
+              if (n_groups > 1u) {
+                // take the ring slots of the chunk's (existing) pixels
+                if (lane < (int)k_px) {
+                  const uint32_t bq = nbase / n_groups + (uint32_t)lane;
+                  if (bq * n_groups < total_slots) {
+                    const int4 b = P.blocks[bq >> 6];
+                    if ((int)(bq & 7u) < b.z && (int)((bq >> 3) & 7u) < b.w)
+                      ring[(px_seq + (uint32_t)lane) & (PT_RING - 1)].owner = bq;
+                  }
+                }
+                old_px = cur_px;
+                old_first = cur_first;
+                cur_px = px_seq;
+                cur_first = nbase;
+                px_seq = __builtin_amdgcn_readfirstlane(px_seq + k_px);
+                claimed = true;
+              }
+            } else {
+              csize = 0;
+            }
+#endif
           }
         }
         if (need) {
           uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-          uint32_t slot = rank < avail ? chunk_next + rank : nbase + (rank - avail);
-          if (slot >= total_slots) {
+          const bool from_old = rank < avail;
+          uint32_t slot = from_old ? chunk_next + rank : nbase + (rank - avail);
+          if (!from_old && blocked) {
+            // no slot this round: the lane stays M_FETCH until the ring has room
+          } else if (slot >= total_slots) {
             mode = M_DONE;
             if (STATS && w_empty == 0ull) w_empty = wall_clock64();
           } else {
@@ -1064,15 +1183,24 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
               pix = b.x + qx + (b.y + qy) * P.W;
               sample = (int)g * P.group_spp;
               acc = f3(0, 0, 0);
+#if PT_PIXEL_ACC
+              // the ring slot of the slot's pixel: pixels of a chunk take
+              // consecutive ring positions from the chunk's first one
+              const bool in_cur = !from_old || !claimed;
+              const uint32_t base_px = in_cur ? cur_px : old_px, first = in_cur ? cur_first : old_first;
+              rslot = (int)((base_px + (slot - first) / n_groups) & (PT_RING - 1));
+#endif
               if (STATS) slot_t0 = wall_clock64();
               mode = M_CAMERA;
             }
           }
         }
-        if (cnt > avail) {  // wave-uniform
+        if (cnt > avail && !blocked) {  // wave-uniform
           chunk_next = nbase + (cnt - avail);
           chunk_end = nbase + csize;
           if (csize == 0) chunk_next = chunk_end = total_slots;  // drained: nothing left to hand out
+        } else if (cnt > avail) {  // blocked: the old chunk is used up, no new one yet
+          chunk_next = chunk_end;
         } else {
           chunk_next += cnt;
         }
@@ -1097,7 +1225,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         if (DBG && pix == P.dbg_pix) printf("pixel (%d,%d) sample %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g)\n", px, py, sample, tr.o.x, tr.o.y, tr.o.z, d.x, d.y, d.z);
         if (box_hit(tr, P.root_lo, P.root_hi)) {
           T = f3(1, 1, 1);
-          depth = 0;
+          cur = 0;  // depth 0
           includeLe = true;
           shadow = false;
           mode = M_TRAV;
@@ -1105,13 +1233,20 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         }
         // miss: the sample sees the environment (includeLe) or nothing
         if (ENV) acc = acc + env_dir(P, d);
-        if (++sample >= P.spp || sample % P.group_spp == 0) {
+        ++sample;
+#if PT_PIXEL_ACC
+        sample_done();
+#endif
+        if (sample >= P.spp || sample % P.group_spp == 0) {
+#if !PT_PIXEL_ACC
           store3(P.partial + 3 * slot_of(pix, sample), acc);
+#endif
           PT_SLOT_DONE();
           mode = M_FETCH;
         }
       }
-      if (__ballot(mode == M_FETCH) == 0ull) break;
+      // (blocked: let the wave's other paths progress; the claim is retried next round)
+      if (__ballot(mode == M_FETCH) == 0ull || blocked) break;
     }
     // ================= traversal phase =================
     // Step every in-flight ray one node at a time; leave as soon as `batch`
@@ -1249,12 +1384,16 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
 // Lanes that resolve one pixel: the pixel's groups are read as one coalesced
 // run (the per-pixel partials are n_groups * 12 B contiguous).
 __host__ __device__ __forceinline__ int resolve_team(int n_groups) {
+  if (PT_PIXEL_ACC) return 1;  // the render wrote each pixel's mean: a copy per lane
   int k = 1;
   while (k < n_groups && k < 64) k <<= 1;
   return k;
 }
 
-// Sums each pixel's sample groups in a fixed order (so the sum is a fixed
+// PT_PIXEL_ACC: copies each traced pixel's mean from the slot framebuffer the
+// render wrote (and 0 for pixels outside the footprint) to the caller's
+// output, frame or packed layout.  Otherwise:
+// sums each pixel's sample groups in a fixed order (so the sum is a fixed
 // function of the pixel, independent of scheduling and of the tile -> GPU
 // assignment) and writes the pixel's average, SampleBuffer-style
 // (pathtracer.cpp:577-581).  A team of k lanes (power of two) per pixel: lane
@@ -1271,14 +1410,18 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
   int2 xy = live ? tile_pixel(tile, tq & 1023u) : make_int2(-1, -1);
   float3 acc = f3(0, 0, 0);
   if (xy.x >= 0 && !culled(P, xy.x, xy.y)) {
+#if PT_PIXEL_ACC
+    acc = ld3(P.fb + 3 * ((size_t)xy.x + (size_t)xy.y * (size_t)P.W));
+#else
     const float* p = P.partial + 3 * ((size_t)xy.x + (size_t)xy.y * (size_t)P.W) * (size_t)P.n_groups;
     for (int g = j; g < P.n_groups; g += k) acc = acc + ld3(p + 3 * g);
+#endif
   }
   // team lanes are consecutive, aligned, and all reach the shuffles
   for (int off = 1; off < k; off <<= 1)
     acc = acc + f3(__shfl_xor(acc.x, off), __shfl_xor(acc.y, off), __shfl_xor(acc.z, off));
   if (xy.x < 0 || j != 0) return;
-  const float inv_spp = (float)(1.0 / (double)P.spp);
+  const float inv_spp = PT_PIXEL_ACC ? 1.0f : (float)(1.0 / (double)P.spp);
   const size_t o = P.packed ? (size_t)(tq & ~1023u) + (size_t)((xy.y - tile.y) * 32 + (xy.x - tile.x))
                             : (size_t)xy.x + (size_t)xy.y * (size_t)P.W;
   store3(P.out + 3 * o, acc * inv_spp);
