@@ -13,6 +13,12 @@
 #ifndef PT_TREELET
 #define PT_TREELET 0  // BVH4 nodes (the first ones, breadth-first: the top levels) staged in LDS
 #endif
+#ifndef PT_ROOT_LDS
+#define PT_ROOT_LDS 1  // fresh rays take their root step from an LDS copy of the root node (C3 +2%)
+#endif
+#ifndef PT_LEAF_MASK
+#define PT_LEAF_MASK 0  // 1: one-primitive leaf steps skip the second primitive's loads (measured -2%: the branch costs more)
+#endif
 #ifndef PT_PIXEL_ACC
 #define PT_PIXEL_ACC 0  // 1: pixel sums accumulated on chip (per-wave LDS ring, fixed point); 0: group sums in HBM
 #endif

@@ -471,7 +471,18 @@ __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const
   const bool two = n >= 2;
   const int pb = two ? pa + 1 : pa;
   float4 a0 = prims[pa].v0, a1 = prims[pa].e1, a2 = prims[pa].e2;
+#if PT_LEAF_MASK
+  // a one-primitive step issues no second triple of loads (vector-memory
+  // address cycles are counted per active lane)
+  float4 b0 = a0, b1 = a1, b2 = a2;
+  if (two) {
+    b0 = prims[pb].v0;
+    b1 = prims[pb].e1;
+    b2 = prims[pb].e2;
+  }
+#else
   float4 b0 = prims[pb].v0, b1 = prims[pb].e1, b2 = prims[pb].e2;
+#endif
   // One memory round trip per leaf step: without the fence the compiler sinks
   // the first primitive's e2 load into the triangle branch (a second
   // dependent L2 trip).  The fence makes the last-issued loads' values live
@@ -656,6 +667,12 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
       ((float4*)s_tree)[k] = ((const float4*)P.nodes)[k];
   }
   const int n_tree = PT_TREELET > 0 ? min(P.n_treelet, PT_TREELET) : 0;
+#if PT_ROOT_LDS
+  // The BVH4 root, which every ray visits first: one LDS copy per workgroup,
+  // so the root step of a fresh ray costs no vector-memory traffic (below).
+  __shared__ DNode s_root;
+  if (!BIN && threadIdx.x < (int)(sizeof(DNode) / 16)) ((float4*)&s_root)[threadIdx.x] = ((const float4*)P.nodes)[threadIdx.x];
+#endif
 
   // Material and light tables are read by every shading step: keep small
   // ones in LDS (the usual case); larger ones stay in global memory.
@@ -1253,6 +1270,18 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
     // lanes have finished their ray, so finished lanes are refilled together
     // (coherent shading) while the others keep their traversal state.
     if (__ballot(mode == M_TRAV) == 0ull) break;  // every lane is M_DONE
+#if PT_ROOT_LDS
+    // Fresh rays (node 0: references only point forward, so no ray returns
+    // to the root) take their root step here, all together, from the LDS
+    // copy: the wave's first traversal iteration no longer waits on a global
+    // load for them.
+    if constexpr (!BIN) {
+      if (mode == M_TRAV && tr.node == 0) {
+        if (node_step<STATS, false, PT_OCTANT != 0 && !ENV, true>(P.nodes, stk, tr, ct, (lds_cchar*)&s_root, 1))
+          mode = M_SHADE;
+      }
+    }
+#endif
     // Once the queue is drained, lanes retire (M_DONE): shade when 3/4 of the
     // lanes still working are ready, not when `batch` of 64 are, or the tail
     // would wait for the slowest ray of the wave at every bounce.
