@@ -28,6 +28,13 @@ C1_DAE = os.path.join(ASSETS, "CBspheres_lambertian.dae")
 BUNNY_DAE = os.path.join(ASSETS, "CBbunny.dae")
 
 
+def _tmp_name(dst: str) -> str:
+    """A temporary name private to this process: the ranks of a multi-GPU
+    run generate the same scene files concurrently, each writes its own copy
+    and os.replace()s it into place (same bytes, atomic)."""
+    return f"{dst}.{os.getpid()}.tmp"
+
+
 def _subdivide_once(pos_tokens, tris):
     """pos_tokens: list of 3-tuples of text tokens; tris: (n,3) int array."""
     pos = np.array([[np.float32(t) for t in p] for p in pos_tokens], dtype=np.float32)
@@ -86,7 +93,7 @@ def make_subdivided(src: str, dst: str, levels: int = 1, geometry_id: str = "Mes
     geo2 = re.sub(r"<polylist[^>]*>.*?</polylist>", lambda _: new_pl, geo2, count=1, flags=re.S)
     out = txt[:g0] + geo2 + txt[g1:]
     os.makedirs(os.path.dirname(os.path.abspath(dst)), exist_ok=True)
-    tmp = dst + ".tmp"
+    tmp = _tmp_name(dst)
     with open(tmp, "w") as f:
         f.write(out)
     os.replace(tmp, dst)
@@ -197,8 +204,10 @@ def make_c5(levels: int, dst: str) -> str:
     txt = txt[:lg] + _MIRROR_SPHERE_GEOM + "  " + txt[lg:]
     vs = txt.index("</visual_scene>")
     txt = txt[:vs] + _MIRROR_SPHERE_NODE + "    " + txt[vs:]
-    with open(dst, "w") as f:
+    tmp = _tmp_name(dst)
+    with open(tmp, "w") as f:
         f.write(txt)
+    os.replace(tmp, dst)
     return dst
 
 
@@ -228,8 +237,10 @@ def refraction_variant(dst: str) -> str:
     g1 = txt.index("</glass>", g0) + len("</glass>")
     txt = txt[:g0] + _REFRACTION_BSDF + txt[g1:]
     if not os.path.exists(dst) or open(dst).read() != txt:
-        with open(dst, "w") as f:
+        tmp = _tmp_name(dst)
+        with open(tmp, "w") as f:
             f.write(txt)
+        os.replace(tmp, dst)
     return dst
 
 
@@ -240,7 +251,9 @@ def c5_envmap_path(cache_dir: Optional[str] = None) -> str:
     dst = os.path.join(cache_dir, "c5_sky_512x256.exr")
     if not os.path.exists(dst) or os.path.getmtime(dst) < os.path.getmtime(__file__):
         os.makedirs(cache_dir, exist_ok=True)
-        image_io.write_exr(dst, synthetic_envmap(512, 256, seed=7), "zip")
+        tmp = _tmp_name(dst)
+        image_io.write_exr(tmp, synthetic_envmap(512, 256, seed=7), "zip")
+        os.replace(tmp, dst)
     return dst
 
 
