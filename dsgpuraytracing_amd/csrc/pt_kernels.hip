@@ -670,8 +670,25 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
 #if PT_ROOT_LDS
   // The BVH4 root, which every ray visits first: one LDS copy per workgroup,
   // so the root step of a fresh ray costs no vector-memory traffic (below).
-  __shared__ DNode s_root;
-  if (!BIN && threadIdx.x < (int)(sizeof(DNode) / 16)) ((float4*)&s_root)[threadIdx.x] = ((const float4*)P.nodes)[threadIdx.x];
+  // PT_ROOT_LDS >= 2: also the root's (up to four) internal children, slots 1-4
+  __shared__ DNode s_root[PT_ROOT_LDS >= 2 ? 5 : 1];
+  if (!BIN && threadIdx.x < (int)(sizeof(DNode) / 16)) ((float4*)s_root)[threadIdx.x] = ((const float4*)P.nodes)[threadIdx.x];
+#if PT_ROOT_LDS >= 2
+  int4 top_ref = make_int4(-1, -1, -1, -1);  // the root's children as LDS slots 1-4 (-1: leaf / empty)
+  if constexpr (!BIN) {
+    const int4 rr = P.nodes[0].ref;  // wave-uniform
+    const float4 lx = P.nodes[0].lox;
+    const int r[4] = {rr.x, rr.y, rr.z, rr.w};
+    const float l[4] = {lx.x, lx.y, lx.z, lx.w};
+    int t[4];
+    for (int k = 0; k < 4; ++k) {
+      t[k] = (r[k] > 0 && !__builtin_isinf(l[k])) ? r[k] : -1;
+      if (t[k] > 0 && threadIdx.x < (int)(sizeof(DNode) / 16))
+        ((float4*)(s_root + 1 + k))[threadIdx.x] = ((const float4*)(P.nodes + t[k]))[threadIdx.x];
+    }
+    top_ref = make_int4(t[0], t[1], t[2], t[3]);
+  }
+#endif
 #endif
 
   // Material and light tables are read by every shading step: keep small
@@ -1277,9 +1294,22 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
     // load for them.
     if constexpr (!BIN) {
       if (mode == M_TRAV && tr.node == 0) {
-        if (node_step<STATS, false, PT_OCTANT != 0 && !ENV, true>(P.nodes, stk, tr, ct, (lds_cchar*)&s_root, 1))
+        if (node_step<STATS, false, PT_OCTANT != 0 && !ENV, true>(P.nodes, stk, tr, ct, (lds_cchar*)s_root, 1))
           mode = M_SHADE;
       }
+#if PT_ROOT_LDS >= 2
+      // ...and every ray at one of the root's children (fresh rays after
+      // their root step, or one popped back to it) takes that step from LDS too
+      const int k1 = tr.node == top_ref.x ? 1 : tr.node == top_ref.y ? 2 : tr.node == top_ref.z ? 3
+                   : tr.node == top_ref.w ? 4 : 0;
+      if (mode == M_TRAV && tr.node > 0 && k1 > 0) {
+        const int nd = tr.node;
+        tr.node = 0;  // the LDS slot as node 0 of a one-node "tree" at s_root + k1
+        if (node_step<STATS, false, PT_OCTANT != 0 && !ENV, true>(P.nodes, stk, tr, ct, (lds_cchar*)(s_root + k1), 1))
+          mode = M_SHADE;
+        (void)nd;
+      }
+#endif
     }
 #endif
     // Once the queue is drained, lanes retire (M_DONE): shade when 3/4 of the
