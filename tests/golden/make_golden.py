@@ -16,11 +16,15 @@ available on the GPU box) and stores inputs + outputs as small PTDUMP files:
   <scene>env_<W>x<H>...        scenes / renders with the EnvironmentLight (-e)
   CBspheres_refraction_*       the glass sphere of CBspheres.dae as a <refraction>
                                material (RefractionBSDF, bsdf.cpp:90-111)
+  c3proxy_128x128_s64_* / c5proxy_128x128_s64_*
+                               reference renders of the BASELINE C3 / C5 proxy scenes
+                               (scenes.proxy_path(1); scenes.c5_path(2) + its env map)
+                               at 128x128, 64 spp, two seeds (statistical parity)
   tocolor_in.ptd / tocolor_ref.ptd
                                HDR edge cases -> HDRImageBuffer::toColor's RGBA8
                                frameBuffer and save_image's flipped rows
 
-Usage: python tests/golden/make_golden.py [--only env|refraction|tocolor]
+Usage: python tests/golden/make_golden.py [--only env|refraction|tocolor|baseline]
 (needs oracle/_ref/ref_driver)
 """
 from __future__ import annotations
@@ -142,6 +146,22 @@ def make_tocolor():
     run(["--mode", "tocolor", "--in", src, "--out", os.path.join(HERE, "tocolor_ref.ptd")])
 
 
+def make_baseline_scenes():
+    """The reference's own renders of the C3 and C5 proxies (default camera,
+    -m 4 -l 1) at 128x128, 64 spp, seeds 1 and 2."""
+    from dsgpuraytracing_amd import scenes
+    for name, dae, env in (("c3proxy", scenes.proxy_path(1), None),
+                           ("c5proxy", scenes.c5_path(2), scenes.c5_envmap_path())):
+        for seed in (1, 2):
+            out = os.path.join(HERE, f"{name}_128x128_s64_m4_l1_seed{seed}.hdr.ptd")
+            args = [dae, "-w", "128", "-h", "128", "-s", "64", "-m", "4", "-l", "1", "--seed", str(seed), "--out", out]
+            if env:
+                args += ["--envmap", env]
+            run(args)
+            d = ptdump.read(out)
+            ptdump.write(out, {"hdr": d["hdr"], "shape": d["shape"]})
+
+
 def main():
     if not os.path.exists(REF):
         sys.exit("oracle/_ref/ref_driver missing: run `make -C oracle/ref` in the build container")
@@ -150,11 +170,14 @@ def main():
         return make_refraction()
     if only == "tocolor":
         return make_tocolor()
+    if only == "baseline":
+        return make_baseline_scenes()
     make_env()
     if only:
         return
     make_refraction()
     make_tocolor()
+    make_baseline_scenes()
     for cam, w, h in SCENES:
         args = [C1, "-w", str(w), "-h", str(h), "--mode", "dump", "--out", os.path.join(HERE, scene_name(cam, w, h))]
         if CAMS[cam]:

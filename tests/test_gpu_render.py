@@ -111,6 +111,32 @@ def test_hip_refraction_statistical_vs_reference_golden():
     assert bias <= 3 * sigma
 
 
+@pytest.mark.parametrize("name", ["c3proxy", "c5proxy"])
+def test_hip_baseline_proxy_statistical_vs_reference_golden(name):
+    """The BASELINE C3 / C5 proxy scenes at 128x128 @ 64 spp vs the reference
+    binary's own renders (two seeds: the noise floor).  Same criterion as the
+    fixture scenes: mean per-pixel RGB-L2 <= 1.10 x the
+    reference's seed-to-seed distance, image-mean bias <= 3 sigma."""
+    from dsgpuraytracing_amd import scenes
+    dae, env = (scenes.proxy_path(1), None) if name == "c3proxy" else (scenes.c5_path(2), scenes.c5_envmap_path())
+    r1 = ptdump.read(golden(f"{name}_128x128_s64_m4_l1_seed1.hdr.ptd"))["hdr"].reshape(128, 128, 3)
+    r2 = ptdump.read(golden(f"{name}_128x128_s64_m4_l1_seed2.hdr.ptd"))["hdr"].reshape(128, 128, 3)
+    sc = Scene.from_dae(dae, 128, 128, envmap=env)
+    pt = PathTracer(ns_aa=64, max_ray_depth=4, ns_area_light=1, seed=4242)
+    pt.set_frame_size(128, 128)
+    pt.set_camera(sc.camera)
+    pt.set_scene(sc)
+    pt.start_raytracing()
+    g = pt.sampleBuffer.copy()
+    floor = np.linalg.norm(r1 - r2, axis=2).mean()
+    dist = np.linalg.norm(g - r1, axis=2).mean()
+    sigma = (r1 - r2).mean(axis=2).std() / np.sqrt(128 * 128)
+    bias = abs(g.mean() - r1.mean())
+    print(f"{name}: L2 {dist:.5f} vs floor {floor:.5f}; bias {bias:.2e} vs 3 sigma {3*sigma:.2e}")
+    assert dist <= 1.10 * floor
+    assert bias <= 3 * sigma
+
+
 @pytest.mark.parametrize("seed", [77])
 def test_hip_environment_light_statistical_vs_reference_golden(seed):
     """C1 + EnvironmentLight at 128x128 @ 64 spp vs the reference binary (-e)."""
@@ -316,6 +342,14 @@ def test_hip_error_paths():
     with pytest.raises(native.PtError) as e:
         dev.render_tiles([(0, 0, 8, 8)], out)
     assert e.value.code == native.PT_E_NOSCENE
+    # the kernel packs path depth and the light-sample cursor in 8 bits each
+    with pytest.raises(native.PtError) as e:
+        dev.set_params(8, 8, 1, 255, 1, 1)
+    assert e.value.code == native.PT_E_INVALID
+    with pytest.raises(native.PtError) as e:
+        dev.set_params(8, 8, 1, 4, 256, 1)
+    assert e.value.code == native.PT_E_INVALID
+    dev.set_params(8, 8, 1, 254, 255, 1)
 
 
 def test_hip_packed_tiles_match_frame():
