@@ -449,7 +449,7 @@ def main():
                        "parallelism": (f"samples{world}" if weak else f"tiles{world}") if world > 1 else "single",
                        "render_time_s": round(elapsed / frames, 4), "scene_load_s": round(t_load, 3),
                        "single_frame_ms": None if single_ms is None else round(single_ms, 3),
-                       "bvh": "gpu-lbvh" if args.lbvh else "reference-sah (host)",
+                       "bvh": "gpu-lbvh" if args.lbvh else ("reference-sah (host)" if os.environ.get("PT_BVH_BUILD") == "ref" else "own binned SAH, 128 bins, C_isect 1 (host)"),
                        "upload_s": round(t_up, 4),
                        "host_output_ms_per_frame": None if host_ms is None else round(host_ms, 3)},
             "roofline": roofline(workload, avg_ms, algorithmic_bytes(st_counts), elapsed / frames * 1e3),
@@ -460,7 +460,7 @@ def main():
                                                         "leaf_steps", "wave_rounds", "queue_atomics", "shade_clocks",
                                                         "hitshade_clocks", "trav_clocks", "max_wave_clocks",
                                                         "wave_wall_sum", "wave_wall_max", "section_clocks", "wave_span",
-                                                        "lane_iters")},
+                                                        "lane_iters", "uniform_node_steps")},
             "launch": {"grid_blocks": s_get(dev, "grid_blocks"), "block": 64,
                        "blocks_per_cu_query": s_get(dev, "blocks_per_cu"),
                        "bvh_nodes": s_get(dev, "bvh_nodes"), "bvh_stack": s_get(dev, "bvh_stack"),

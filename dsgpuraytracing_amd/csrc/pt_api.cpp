@@ -142,7 +142,11 @@ struct pt_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;  // the current launch's triple
   DevBuf<DNode> nodes;
   DevBuf<DNode2> nodes2;  // binary tree for PT_FLAG_REF_COUNTS
-  DevBuf<int> prim_map;   // GPU-built BVH: sorted primitive -> uploaded index (else empty)
+  DevBuf<int> prim_map;   // own BVH order (SAH or GPU-built) -> uploaded primitive index (else empty)
+  // primitives in the caller's (reference BVH) order, for the reference-count
+  // launch over nodes2 when the render tree is our own (else empty)
+  DevBuf<DPrim> prims_ref;
+  DevBuf<float> norms_ref;
   DevBuf<float4> env_tex;          // environment map RGB (w*h, .w unused)
   DevBuf<float> env_ptheta, env_pphi, env_pdf;  // EnvironmentLight tables
   DevBuf<int> env_gtheta, env_gphi;               // their guide tables
@@ -446,6 +450,29 @@ static int build_host_bvh(const pt_scene* s, std::vector<DNode>& dn, std::vector
         if (ch[k].ref >= 0) st.push_back({ch[k].ref, me, k, below});
     }
   }
+  if (std::getenv("PT_BVH_REPORT")) {
+    // expected steps per random ray (surface-area heuristic over the BVH4):
+    // node steps = sum of node areas / root area; leaf steps = sum over
+    // leaves of area * ceil(count / 2) / root area
+    auto a3 = [](float lx, float hx, float ly, float hy, float lz, float hz) {
+      const double dx = hx - lx, dy = hy - ly, dz = hz - lz;
+      return dx * dy + dy * dz + dz * dx;
+    };
+    double root = 0, nodes = 0, leaves = 0;
+    for (size_t i = 0; i < dn.size(); ++i) {
+      const DNode& d = dn[i];
+      for (int k = 0; k < 4; ++k) {
+        if (std::isinf((&d.lox.x)[k])) continue;
+        const double a = a3((&d.lox.x)[k], (&d.hix.x)[k], (&d.loy.x)[k], (&d.hiy.x)[k], (&d.loz.x)[k], (&d.hiz.x)[k]);
+        root += i == 0 ? a : 0.0;
+        const int r = (&d.ref.x)[k];
+        if (r >= 0) nodes += a;
+        else leaves += a * (double)((((~r) & 7) + 2) / 2);
+      }
+    }
+    std::fprintf(stderr, "[pt] BVH4: %zu nodes, stack %d, SAH node steps %.3f leaf steps %.3f (per root-box ray)\n",
+                 dn.size(), max_stack, (nodes + root) / root, leaves / root);
+  }
   // Breadth-first order (PT_BVH_ORDER=bfs; the default when the kernel
   // stages a treelet): the top levels become the first nodes, which the
   // render kernel copies into LDS (PT_TREELET).  Parents still precede their
@@ -506,6 +533,156 @@ static int build_host_bvh(const pt_scene* s, std::vector<DNode>& dn, std::vector
   return PT_OK;
 }
 
+// ---- Own binned-SAH binary tree over the scene's primitives (PT_BVH_BUILD=sah).
+// The traversal result is the nearest hit whatever the tree, so the tree is
+// free to follow this kernel's cost model instead of the reference's builder
+// (bvh.cpp:21-178: 32 buckets over the node box, always split down to <= 4).
+// Here: PT_SAH_BINS buckets over the CENTROID bounds, per-axis sweeps, and a
+// leaf wherever the SAH says a split no longer pays (C_trav = 1 per binary
+// node, C_isect = PT_SAH_CI per primitive), at most PT_SAH_LEAF primitives.
+// Output in the reference's pt_bvh_node format (pre-order, ranges over the
+// permuted primitive order `perm`: new index -> uploaded index), so the
+// BVH4 collapse below is shared with the reference-tree path.
+static void build_sah_tree(const pt_scene* s, std::vector<pt_bvh_node>& out, std::vector<int64_t>& perm) {
+  const int64_t n = s->n_prims;
+  const int bins = std::getenv("PT_SAH_BINS") ? std::max(2, std::atoi(std::getenv("PT_SAH_BINS"))) : 128;
+  const double ci = std::getenv("PT_SAH_CI") ? std::atof(std::getenv("PT_SAH_CI")) : 1.0;
+  const int64_t max_leaf = std::getenv("PT_SAH_LEAF") ? std::max(1, std::min(8, std::atoi(std::getenv("PT_SAH_LEAF")))) : 4;
+  std::vector<double> lo((size_t)n * 3), hi((size_t)n * 3), cen((size_t)n * 3);
+  for (int64_t i = 0; i < n; ++i) {
+    const double* g = s->prim_geom + 9 * i;
+    for (int k = 0; k < 3; ++k) {
+      double a, b;
+      if (s->prim_type[i] == PT_PRIM_TRIANGLE) {
+        a = std::min({g[k], g[3 + k], g[6 + k]});
+        b = std::max({g[k], g[3 + k], g[6 + k]});
+      } else {
+        a = g[k] - std::fabs(g[3]);
+        b = g[k] + std::fabs(g[3]);
+      }
+      lo[3 * i + k] = a;
+      hi[3 * i + k] = b;
+      cen[3 * i + k] = 0.5 * (a + b);
+    }
+  }
+  auto half_area = [](const double* a, const double* b) {
+    const double dx = b[0] - a[0], dy = b[1] - a[1], dz = b[2] - a[2];
+    return dx * dy + dy * dz + dz * dx;
+  };
+  perm.resize((size_t)n);
+  for (int64_t i = 0; i < n; ++i) perm[(size_t)i] = i;
+  out.clear();
+  struct Task { int64_t node, start, count; };
+  std::vector<Task> st;
+  auto make_node = [&](int64_t start, int64_t count) {
+    pt_bvh_node d{};
+    for (int k = 0; k < 3; ++k) {
+      d.bb_min[k] = INFINITY;
+      d.bb_max[k] = -INFINITY;
+    }
+    for (int64_t j = start; j < start + count; ++j) {
+      const int64_t p = perm[(size_t)j];
+      for (int k = 0; k < 3; ++k) {
+        d.bb_min[k] = std::min(d.bb_min[k], lo[3 * p + k]);
+        d.bb_max[k] = std::max(d.bb_max[k], hi[3 * p + k]);
+      }
+    }
+    d.start = start;
+    d.range = count;
+    d.left = d.right = -1;
+    out.push_back(d);
+    return (int64_t)out.size() - 1;
+  };
+  struct Bin { double lo[3], hi[3]; int64_t n; };
+  std::vector<Bin> bn((size_t)bins);
+  std::vector<double> rcost((size_t)bins);
+  st.push_back({make_node(0, n), 0, n});
+  while (!st.empty()) {
+    const Task t = st.back();
+    st.pop_back();
+    if (t.count <= 1) continue;
+    double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t j = t.start; j < t.start + t.count; ++j)
+      for (int k = 0; k < 3; ++k) {
+        clo[k] = std::min(clo[k], cen[3 * perm[(size_t)j] + k]);
+        chi[k] = std::max(chi[k], cen[3 * perm[(size_t)j] + k]);
+      }
+    const double area = half_area(out[(size_t)t.node].bb_min, out[(size_t)t.node].bb_max);
+    double best = INFINITY;
+    int best_axis = -1, best_split = 0;
+    for (int k = 0; k < 3; ++k) {
+      if (!(chi[k] > clo[k])) continue;
+      const double scale = bins / (chi[k] - clo[k]);
+      for (Bin& b : bn) {
+        b.n = 0;
+        for (int q = 0; q < 3; ++q) {
+          b.lo[q] = INFINITY;
+          b.hi[q] = -INFINITY;
+        }
+      }
+      for (int64_t j = t.start; j < t.start + t.count; ++j) {
+        const int64_t p = perm[(size_t)j];
+        const int b = std::min(bins - 1, (int)((cen[3 * p + k] - clo[k]) * scale));
+        Bin& B = bn[(size_t)b];
+        B.n++;
+        for (int q = 0; q < 3; ++q) {
+          B.lo[q] = std::min(B.lo[q], lo[3 * p + q]);
+          B.hi[q] = std::max(B.hi[q], hi[3 * p + q]);
+        }
+      }
+      // right sweep: cost of bins [b, bins)
+      double rl[3] = {INFINITY, INFINITY, INFINITY}, rh[3] = {-INFINITY, -INFINITY, -INFINITY};
+      int64_t rn = 0;
+      for (int b = bins - 1; b > 0; --b) {
+        const Bin& B = bn[(size_t)b];
+        rn += B.n;
+        for (int q = 0; q < 3; ++q) {
+          rl[q] = std::min(rl[q], B.lo[q]);
+          rh[q] = std::max(rh[q], B.hi[q]);
+        }
+        rcost[(size_t)b] = rn ? half_area(rl, rh) * (double)rn : 0.0;
+      }
+      double ll[3] = {INFINITY, INFINITY, INFINITY}, lh[3] = {-INFINITY, -INFINITY, -INFINITY};
+      int64_t ln = 0;
+      for (int b = 0; b < bins - 1; ++b) {  // split between bin b and b+1
+        const Bin& B = bn[(size_t)b];
+        ln += B.n;
+        for (int q = 0; q < 3; ++q) {
+          ll[q] = std::min(ll[q], B.lo[q]);
+          lh[q] = std::max(lh[q], B.hi[q]);
+        }
+        if (ln == 0 || ln == t.count) continue;
+        const double c = half_area(ll, lh) * (double)ln + rcost[(size_t)b + 1];
+        if (c < best) {
+          best = c;
+          best_axis = k;
+          best_split = b + 1;
+        }
+      }
+    }
+    const double split_cost = 1.0 + ci * best / std::max(area, 1e-300);
+    const double leaf_cost = ci * (double)t.count;
+    int64_t mid;
+    if (best_axis < 0) {  // coincident centroids
+      if (t.count <= max_leaf) continue;
+      mid = t.start + t.count / 2;
+    } else {
+      if (t.count <= max_leaf && leaf_cost <= split_cost) continue;
+      const double scale = bins / (chi[best_axis] - clo[best_axis]);
+      auto it = std::partition(perm.begin() + t.start, perm.begin() + t.start + t.count, [&](int64_t p) {
+        return std::min(bins - 1, (int)((cen[3 * p + best_axis] - clo[best_axis]) * scale)) < best_split;
+      });
+      mid = (int64_t)(it - perm.begin());
+    }
+    const int64_t l = make_node(t.start, mid - t.start);
+    const int64_t r = make_node(mid, t.start + t.count - mid);
+    out[(size_t)t.node].left = l;
+    out[(size_t)t.node].right = r;
+    st.push_back({r, mid, t.start + t.count - mid});
+    st.push_back({l, t.start, mid - t.start});
+  }
+}
+
 // GPU linear-BVH build over the primitives already in c->prims / c->norms
 // (CUDAPathTracer::buildBVH, cuda_src/setup.cu:478-686; kernels in lbvh.hip).
 static int build_gpu_bvh(pt_ctx* c, const pt_scene* s) {
@@ -563,9 +740,46 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipDeviceSynchronize());  // renders in flight read the scene being replaced
 
+  // Own SAH tree (PT_BVH_BUILD=sah): the primitives are permuted into its
+  // leaf order and uploaded that way; prim_map takes ray-query ids back.
+  std::vector<pt_bvh_node> sah_nodes;
+  std::vector<int64_t> perm;
+  std::vector<int32_t> ptype, pbsdf;
+  std::vector<double> pgeom, pnorm;
+  pt_scene ps;
+  const pt_scene* const s0 = s;  // the caller's scene (reference BVH order)
+  int rc0 = 0;
+  const char* bb = std::getenv("PT_BVH_BUILD");  // "ref": render over the reference's own tree
+  if (!gpu_bvh && !(bb && std::strcmp(bb, "ref") == 0)) {
+    build_sah_tree(s, sah_nodes, perm);
+    const size_t np = (size_t)s->n_prims;
+    ptype.resize(np);
+    pbsdf.resize(np);
+    pgeom.resize(np * 9);
+    pnorm.resize(np * 9);
+    for (size_t i = 0; i < np; ++i) {
+      const size_t p = (size_t)perm[i];
+      ptype[i] = s->prim_type[p];
+      pbsdf[i] = s->prim_bsdf[p];
+      std::memcpy(&pgeom[9 * i], s->prim_geom + 9 * p, 9 * sizeof(double));
+      std::memcpy(&pnorm[9 * i], s->prim_norm + 9 * p, 9 * sizeof(double));
+    }
+    ps = *s;
+    ps.prim_type = ptype.data();
+    ps.prim_bsdf = pbsdf.data();
+    ps.prim_geom = pgeom.data();
+    ps.prim_norm = pnorm.data();
+    ps.nodes = sah_nodes.data();
+    ps.n_nodes = (int64_t)sah_nodes.size();
+    s = &ps;
+  }
+
   // ---- primitives (already in BVH order)
-  std::vector<DPrim> prims((size_t)s->n_prims);
-  std::vector<float> norms((size_t)s->n_prims * 9);
+  std::vector<DPrim> prims, prims0;
+  std::vector<float> norms, norms0;
+  auto convert = [&](const pt_scene* s, std::vector<DPrim>& prims, std::vector<float>& norms) -> int {
+  prims.resize((size_t)s->n_prims);
+  norms.assign((size_t)s->n_prims * 9, 0.f);
   for (int64_t i = 0; i < s->n_prims; ++i) {
     const double* g = s->prim_geom + 9 * i;
     const double* n = s->prim_norm + 9 * i;
@@ -591,6 +805,10 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
       return fail(PT_E_INVALID, "pt_upload_scene: unknown primitive type");
     }
   }
+  return PT_OK;
+  };
+  if (int rc = convert(s, prims, norms)) return rc;
+  if (s != s0 && (rc0 = convert(s0, prims0, norms0))) return rc0;
 
   std::vector<DBsdf> bs((size_t)s->n_bsdfs);
   for (int i = 0; i < s->n_bsdfs; ++i) {
@@ -639,16 +857,36 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
   HIPCHK(hipMemcpy(c->prims.p, prims.data(), prims.size() * sizeof(DPrim), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(c->norms.p, norms.data(), norms.size() * sizeof(float), hipMemcpyHostToDevice));
   c->prim_map.release();
+  c->prims_ref.release();
+  c->norms_ref.release();
+  if (!prims0.empty()) {
+    HIPCHK(c->prims_ref.reserve(prims0.size()));
+    HIPCHK(c->norms_ref.reserve(norms0.size()));
+    HIPCHK(hipMemcpy(c->prims_ref.p, prims0.data(), prims0.size() * sizeof(DPrim), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->norms_ref.p, norms0.data(), norms0.size() * sizeof(float), hipMemcpyHostToDevice));
+  }
   if (!gpu_bvh) {
     std::vector<DNode> dn;
     std::vector<DNode2> d2;
     int max_stack = 0;
     int rc = build_host_bvh(s, dn, d2, max_stack);
     if (rc) return rc;
+    if (s != s0) {  // the reference-count launch walks the caller's (reference) tree
+      std::vector<DNode> dn0;
+      int ms0 = 0;
+      d2.clear();
+      if ((rc = build_host_bvh(s0, dn0, d2, ms0))) return rc;
+      max_stack = std::max(max_stack, ms0);
+    }
     HIPCHK(c->nodes2.reserve(d2.size()));
     HIPCHK(hipMemcpy(c->nodes2.p, d2.data(), d2.size() * sizeof(DNode2), hipMemcpyHostToDevice));
     HIPCHK(c->nodes.reserve(dn.size()));
     HIPCHK(hipMemcpy(c->nodes.p, dn.data(), dn.size() * sizeof(DNode), hipMemcpyHostToDevice));
+    if (!perm.empty()) {
+      std::vector<int> pm(perm.begin(), perm.end());
+      HIPCHK(c->prim_map.reserve(pm.size()));
+      HIPCHK(hipMemcpy(c->prim_map.p, pm.data(), pm.size() * sizeof(int), hipMemcpyHostToDevice));
+    }
     c->bvh_stack = max_stack;
     c->n_nodes4 = dn.size();
     const pt_bvh_node* N = s->nodes;
@@ -827,6 +1065,10 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.nodes2 = c->nodes2.p;
   P.prims = c->prims.p;
   P.norms = c->norms.p;
+  if ((flags & PT_FLAG_REF_COUNTS) && c->prims_ref.p) {  // nodes2 indexes the caller's order
+    P.prims = c->prims_ref.p;
+    P.norms = c->norms_ref.p;
+  }
   P.bsdfs = c->bsdfs.p;
   P.lights = c->lights.p;
   P.env_w = c->env_w;
@@ -1026,6 +1268,7 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags, bool sync) {
     c->last.hitshade_clocks = (int64_t)v[16];
     for (int k = 0; k < 4; ++k) c->last.section_clocks[k] = (int64_t)v[17 + k];
     for (int k = 0; k < 4; ++k) c->last.lane_iters[k] = (int64_t)v[27 + k];
+    c->last.uniform_node_steps = (int64_t)v[31];
     for (int k = 0; k < 3; ++k) c->last.wave_span[k] = (int64_t)(v[22 + k] - v[21]);
     for (int k = 0; k < 2; ++k) c->last.wave_span[3 + k] = v[25 + k] ? (int64_t)(v[25 + k] - v[21]) : -1;
     c->last.counters_valid = 1;

@@ -16,6 +16,12 @@
 #ifndef PT_ROOT_LDS
 #define PT_ROOT_LDS 1  // fresh rays take their root step from an LDS copy of the root node (C3 +2%)
 #endif
+#ifndef PT_EARLY_BOUNCE
+#define PT_EARLY_BOUNCE 0  // 1: the bounce is sampled with the last light sample and its ray starts where the shadow ray ends (C3 -9%: shading code growth, SGPR spills)
+#endif
+#ifndef PT_SCALAR_NODE
+#define PT_SCALAR_NODE 0  // 1: node steps whose lanes all stand at one node read it through the scalar cache (C3: 3% of node steps; measured -0.5%)
+#endif
 #ifndef PT_LEAF_MASK
 #define PT_LEAF_MASK 0  // 1: one-primitive leaf steps skip the second primitive's loads (measured -2%: the branch costs more)
 #endif

@@ -420,6 +420,46 @@ __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, const
   return node_order(stk, tr, d, rf);
 }
 
+// Node step of a wave whose node-stepping lanes all stand at the same node
+// `n` (wave-uniform, an SGPR): the node is read through the scalar cache
+// (constant address space: s_load, no vector-memory instruction, no texture
+// addresser cycles -- the path the per-lane node fetches saturate) and every
+// lane tests the four children against its own ray.  The direction signs may
+// differ per lane, so the slab test takes per-axis min/max here.
+typedef __attribute__((address_space(4))) const float4 cst_f4;
+typedef __attribute__((address_space(4))) const int4 cst_i4;
+template <bool STATS>
+__device__ __forceinline__ bool node_step_uniform(const DNode* __restrict__ nodes, int n, const Stack& stk, Trav& tr,
+                                                  Counters& ct) {
+  const float kRobust = PT_ROBUST;
+  const float kMiss = 3.0e38f;
+  // two s_load_dwordx16 (the 128-B node)
+  typedef float pt_v16f __attribute__((ext_vector_type(16)));
+  typedef __attribute__((address_space(4))) const pt_v16f cst_v16;
+  cst_v16* np = (cst_v16*)((const char*)nodes + ((size_t)(uint32_t)n << 7));
+  const pt_v16f A = np[0], B = np[1];
+  const float4 lx = make_float4(A[0], A[1], A[2], A[3]), hx = make_float4(A[4], A[5], A[6], A[7]);
+  const float4 ly = make_float4(A[8], A[9], A[10], A[11]), hy = make_float4(A[12], A[13], A[14], A[15]);
+  const float4 lz = make_float4(B[0], B[1], B[2], B[3]), hz = make_float4(B[4], B[5], B[6], B[7]);
+  const int4 rf = make_int4(__float_as_int(B[8]), __float_as_int(B[9]), __float_as_int(B[10]), __float_as_int(B[11]));
+  if (STATS) ct.nodes++;
+  const float3 o = tr.o, inv = tr.inv;
+  const float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+  const float* LX = &lx.x; const float* HX = &hx.x; const float* LY = &ly.x;
+  const float* HY = &hy.x; const float* LZ = &lz.x; const float* HZ = &hz.x;
+  float d[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float ax = fmaf(LX[k], inv.x, -oi.x), bx = fmaf(HX[k], inv.x, -oi.x);
+    float ay = fmaf(LY[k], inv.y, -oi.y), by = fmaf(HY[k], inv.y, -oi.y);
+    float az = fmaf(LZ[k], inv.z, -oi.z), bz = fmaf(HZ[k], inv.z, -oi.z);
+    float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
+    float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tr.tmax)) * kRobust;
+    d[k] = tn <= tf ? tn : kMiss;
+  }
+  return node_order(stk, tr, d, rf);
+}
+
 // Binary node step over the reference topology (reference-count launch).
 template <bool STATS>
 __device__ __forceinline__ bool node_step2(const DNode2* __restrict__ nodes, const Stack& stk, Trav& tr,
@@ -752,12 +792,17 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
   float3 hp = f3(0, 0, 0), ns = f3(0, 0, 1), ng = f3(0, 0, 1);
   int bsdf = 0;
   float3 pend = f3(0, 0, 0);  // NEE contribution awaiting its shadow ray
+  // PT_EARLY_BOUNCE: what follows the shadow ray in flight -- 0: the shading
+  // round (more light samples, then the bounce), 1: the bounce ray already
+  // sampled (origin in hp, direction in ns), 2: the end of the sample
+  int post = 0;
   Trav tr;
   trav_init(tr, f3(0, 0, 0), f3(0, 0, 1), 0.0f, false);
   Counters ct = {0, 0, 0};
   uint32_t n_cam = 0, n_bounce = 0, n_shadow = 0, n_hits = 0;
   uint32_t n_titer = 0, n_rounds = 0;  // wave-level traversal steps / shading rounds (lane 0)
   uint32_t n_leafit = 0;               // of the traversal steps: leaf steps
+  uint32_t n_uninode = 0;              // of the traversal steps: wave-uniform node steps (PT_SCALAR_NODE)
   // traversal lane-iterations: at the other step kind, finished and waiting
   // for the shading round, retired, stepping a leaf
   uint32_t l_other = 0, l_ready = 0, l_dead = 0, l_leaf = 0;
@@ -848,6 +893,16 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         if (!found) acc = acc + pend;  // unoccluded (the light sample was already counted)
         if (DBG && pix == P.dbg_pix) printf("    shadow %s (pend %.6g) prim %d t %.9g\n", found ? "occluded" : "clear", pend.x, tr.prim, tr.tmax);
         stage = 0;
+        if (PT_EARLY_BOUNCE && post == 1) {  // the bounce was sampled with the last light sample
+          trav_init(tr, hp, ns, 3.0e38f, false);
+          shadow = false;
+          mode = M_TRAV;
+          stage = 3;
+        } else if (PT_EARLY_BOUNCE && post == 2) {
+          finish = true;
+          stage = 2;
+        }
+        post = 0;
       } else if (!found) {
         // miss: the environment map if there is one and includeLe (pathtracer.cpp:411-427)
         if (ENV && includeLe) acc = acc + mul(T, env_dir(P, tr.d));
@@ -902,6 +957,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         const int btype = __float_as_int(bsdf_f(bsdf, 0));
         const Frame fr = make_frame(ns);
         bool emitted = false;
+        bool emit_last = false;  // the shadow ray emitted is the vertex's last light sample
         // ---- next-event estimation over all lights (pathtracer.cpp:469-523)
         int li = (int)(cur >> 16), ls = (int)((cur >> 8) & 0xffu);
         while (li < P.n_lights) {
@@ -951,6 +1007,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
           }
           const float scale = 1.0f / (float)nls;
           ++ls;
+          emit_last = ls >= nls && li + 1 >= P.n_lights;
           // f() is zero for every BSDF but Diffuse (bsdf.cpp:34-202): nothing to add.
           if (btype != 0 || !lit) continue;
           float cos_t = fmaxf(0.0f, fr.to_local(wi).z);
@@ -971,8 +1028,16 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         if (emitted) {
           shadow = true;
           mode = M_TRAV;
+        }
+        // Without PT_EARLY_BOUNCE the bounce waits for the shading round after
+        // the vertex's last shadow ray.  With it, the bounce is sampled now,
+        // together with the last light sample (the same draws in the same
+        // order: every light draw precedes it), and the lane starts the bounce
+        // ray right where its shadow ray ends, inside the traversal loop.
+        if (emitted && !(PT_EARLY_BOUNCE && emit_last)) {
         } else if ((int)(cur & 0xffu) >= P.max_depth) {
-          finish = true;
+          if (emitted) post = 2;
+          else finish = true;
         } else {
           // ---- indirect bounce (pathtracer.cpp:527-552)
           float3 wi;
@@ -1031,16 +1096,24 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
           float pterm = fmaxf(1.0f - illum(f), 0.0f);
           if (ptrng::draw(rbase, rdim++) < pterm) {
             if (DBG && pix == P.dbg_pix) printf("    RR terminate (p=%.4g)\n", pterm);
-            finish = true;
+            if (emitted) post = 2;
+            else finish = true;
           } else {
             if (DBG && pix == P.dbg_pix) printf("    bounce wi=(%.6g %.6g %.6g) pdf %.5g p %.4g dim %u\n", wi.x, wi.y, wi.z, pdf, pterm, rdim);
             T = mul(T, f * (fabsf(wi.z) * rcp(pdf * (1.0f - pterm))));
             float3 v = normalize(fr.to_world(wi));
-            trav_init(tr, offset_ray(hp, dot(v, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng), v, 3.0e38f, false);
+            const float3 bo = offset_ray(hp, dot(v, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng);
+            if (emitted) {  // after the shadow ray (tr holds it now)
+              hp = bo;
+              ns = v;
+              post = 1;
+            } else {
+              trav_init(tr, bo, v, 3.0e38f, false);
+              shadow = false;
+              mode = M_TRAV;
+            }
             includeLe = btype == 1 || btype == 2 || btype == 3;
             ++cur;  // depth + 1
-            shadow = false;
-            mode = M_TRAV;
             if (STATS) n_bounce++;
           }
         }
@@ -1143,6 +1216,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         }
 #else
         bool claimed = false;  // PT_PIXEL_ACC: this refill took a new chunk (the ring bookkeeping moved)
+        (void)claimed;
         if (cnt > avail) {
           if (PT_DRAIN_NO_ATOMIC && seen >= total_slots) {
             // This wave already saw the queue drained: every further claim
@@ -1352,14 +1426,39 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         if (STATS) n_leafit += lane == 0;
       } else {
         if (trav && !at_leaf) {
-          if constexpr (BIN) done = node_step2<STATS>(P.nodes2, stk, tr, ct);
-          // (the ENV build spills registers with the node fence or the
-          // octant loads: without)
-          else done = node_step<STATS, (PT_LOAD_FENCE & 1) != 0 && !ENV, PT_OCTANT != 0 && !ENV,
-                                (PT_TREELET > 0) && !ENV>(P.nodes, stk, tr, ct, (lds_cchar*)s_tree, n_tree);
+          if constexpr (BIN) {
+            done = node_step2<STATS>(P.nodes2, stk, tr, ct);
+          } else {
+#if PT_SCALAR_NODE
+            // every node-stepping lane at one node: fetch it through the
+            // scalar cache (coherent camera and shadow rays high in the tree)
+            const int n0 = __builtin_amdgcn_readfirstlane(tr.node);
+            if (__ballot(tr.node != n0) == 0ull) {
+              if (STATS) n_uninode += lane == __builtin_amdgcn_readfirstlane(lane);
+              done = node_step_uniform<STATS>(P.nodes, n0, stk, tr, ct);
+            } else
+#endif
+            // (the ENV build spills registers with the node fence or the
+            // octant loads: without)
+            done = node_step<STATS, (PT_LOAD_FENCE & 1) != 0 && !ENV, PT_OCTANT != 0 && !ENV,
+                             (PT_TREELET > 0) && !ENV>(P.nodes, stk, tr, ct, (lds_cchar*)s_tree, n_tree);
+          }
         }
       }
       if (done) mode = M_SHADE;
+#if PT_EARLY_BOUNCE
+      // a shadow ray ended whose bounce is already sampled: add the light
+      // sample and go on with the bounce ray, no shading round
+      if (__ballot(done && shadow && post == 1) != 0ull) {
+        if (done && shadow && post == 1) {
+          if (!tr.found) acc = acc + pend;
+          trav_init(tr, hp, ns, 3.0e38f, false);
+          shadow = false;
+          post = 0;
+          mode = M_TRAV;
+        }
+      }
+#endif
       if (STATS && done) {
         ray_steps_max = max(ray_steps_max, r_steps);
         ray_idle_max = max(ray_idle_max, r_idle);
@@ -1390,6 +1489,11 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
       unsigned long long s = li[k];
       for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
       if (lane == 0) atomicAdd(P.stats + 27 + k, s);
+    }
+    {
+      unsigned long long s = n_uninode;
+      for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
+      if (lane == 0) atomicAdd(P.stats + 31, s);
     }
     // load balance: the slowest wave bounds the launch
     w_empty = w_empty ? w_empty : ~0ull;

@@ -195,6 +195,8 @@ typedef struct pt_stats {
   int64_t lane_iters[4];   /* traversal lane-iterations (64 per wave iteration) spent at the other
                               step kind, finished and waiting for the shading round, retired
                               (queue drained), stepping a leaf; node steps = node_visits */
+  int64_t uniform_node_steps; /* of wave_trav_steps: node steps whose lanes all stood at one node
+                                 (read through the scalar cache, PT_SCALAR_NODE builds) */
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */

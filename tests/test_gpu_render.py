@@ -235,10 +235,12 @@ def _single_leaf_scene(name):
 
 
 @pytest.mark.parametrize("name", ["c1_default_64x64", "CBspheres_64x64"])
-def test_hip_oversize_leaf_split_matches_reference_bvh(name):
+def test_hip_oversize_leaf_split_matches_reference_bvh(monkeypatch, name):
     """Closest hits do not depend on the BVH: a scene whose reference BVH is a
-    single oversize leaf renders like the reference BVH."""
+    single oversize leaf renders like the reference BVH (rendering over the
+    caller's tree, PT_BVH_BUILD=ref, where the leaf split happens)."""
     from dsgpuraytracing_amd.pathtracer import Device
+    monkeypatch.setenv("PT_BVH_BUILD", "ref")
     rays = ptdump.read(golden("c1_rays.ptd"))
     res = []
     for sc in (Scene.from_dump(golden(f"{name}.scene.ptd")), _single_leaf_scene(name)):
@@ -291,8 +293,9 @@ def _deep_chain_scene(n=96):
     return d
 
 
-def test_hip_deep_bvh_stack_spill_vs_restatement(restate, tmp_path):
+def test_hip_deep_bvh_stack_spill_vs_restatement(monkeypatch, restate, tmp_path):
     from dsgpuraytracing_amd.pathtracer import Device
+    monkeypatch.setenv("PT_BVH_BUILD", "ref")  # traverse the chain itself (the SAH rebuild balances it)
     d = _deep_chain_scene()
     path = str(tmp_path / "deep.ptd")
     ptdump.write(path, d)
@@ -317,6 +320,53 @@ def test_hip_deep_bvh_stack_spill_vs_restatement(restate, tmp_path):
     assert np.array_equal(prim[both], rp[both])
     assert np.allclose(t[both], rt[both], rtol=1e-5)
     assert np.array_equal(anyh, ra)
+
+
+@pytest.mark.parametrize("name", ["c3proxy", "CBspheres_64x64", "c1env_64x64"])
+def test_own_sah_tree_matches_reference_tree(monkeypatch, name):
+    """The render tree is this library's own binned-SAH BVH by default
+    (pt_api.cpp build_sah_tree); the caller's (reference) tree only decides the
+    primitive order handed over.  Closest hits do not depend on the tree:
+    ray queries give the same hits / primitives / distances (ids mapped back
+    to the caller's order) and frames agree near-exactly with the frames
+    rendered over the reference tree (PT_BVH_BUILD=ref)."""
+    from dsgpuraytracing_amd.pathtracer import Device
+    from dsgpuraytracing_amd import scenes
+    if name == "c3proxy":
+        sc = Scene.from_dae(scenes.proxy_path(1), 96, 96)
+        w = h = 96
+        rng = np.random.default_rng(11)
+        m = 20000
+        o = np.tile(np.asarray(list(sc.camera.pos), np.float64), (m, 1)) + rng.normal(0, 0.05, (m, 3))
+        tgt = rng.uniform(-0.6, 0.6, (m, 3))
+        dr = tgt - o
+        dr /= np.linalg.norm(dr, axis=1, keepdims=True)
+        maxt = rng.uniform(0.5, 8.0, m)
+    else:
+        sc = Scene.from_dump(golden(f"{name}.scene.ptd"))
+        w = h = 64
+        rays = ptdump.read(golden("c1_rays.ptd"))
+        o, dr, maxt = rays["ray_o"], rays["ray_d"], rays["ray_maxt"]
+    res = []
+    for mode in ("ref", "sah"):
+        monkeypatch.setenv("PT_BVH_BUILD", mode)
+        dev = Device(0)
+        dev.upload_scene(sc)
+        res.append(dev.intersect(o, dr, maxt))
+        pt = PathTracer(ns_aa=8, max_ray_depth=4, ns_area_light=1, seed=4)
+        pt.set_frame_size(w, h)
+        pt.set_camera(sc.camera)
+        pt.set_scene(sc)
+        pt.start_raytracing()
+        res.append(pt.sampleBuffer.copy())
+    (h0, t0, p0, a0), img0, (h1, t1, p1, a1), img1 = res
+    assert h0.mean() > 0.2
+    assert (h0 == h1).mean() >= 0.999 and (a0 == a1).mean() >= 0.999
+    same = (h0 == 1) & (h1 == 1)
+    assert (p0[same] == p1[same]).mean() >= 0.999
+    assert np.allclose(t0[same], t1[same], rtol=1e-5, atol=1e-6)
+    frac, rel_mean = near_exact_report(img1, img0)
+    assert frac >= 0.995 and rel_mean <= 1e-3, (frac, rel_mean)
 
 
 def test_hip_stats_counters():
