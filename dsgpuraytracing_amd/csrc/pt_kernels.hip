@@ -320,6 +320,14 @@ __device__ __forceinline__ bool node_order(const Stack& stk, Trav& tr, const flo
 #ifndef PT_OCTANT
 #define PT_OCTANT 1
 #endif
+// the ENV (environment light) build: octant-selected node loads / node load
+// fence (round 1: they made it spill; on the round-2 code both together C5 +2.5%)
+#ifndef PT_ENV_OCT
+#define PT_ENV_OCT 1
+#endif
+#ifndef PT_ENV_FENCE
+#define PT_ENV_FENCE 1
+#endif
 
 typedef __attribute__((address_space(3))) const char lds_cchar;
 typedef float pt_v4f __attribute__((ext_vector_type(4)));
@@ -1368,7 +1376,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
     // load for them.
     if constexpr (!BIN) {
       if (mode == M_TRAV && tr.node == 0) {
-        if (node_step<STATS, false, PT_OCTANT != 0 && !ENV, true>(P.nodes, stk, tr, ct, (lds_cchar*)s_root, 1))
+        if (node_step<STATS, false, PT_OCTANT != 0 && (!ENV || PT_ENV_OCT), true>(P.nodes, stk, tr, ct, (lds_cchar*)s_root, 1))
           mode = M_SHADE;
       }
 #if PT_ROOT_LDS >= 2
@@ -1379,7 +1387,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
       if (mode == M_TRAV && tr.node > 0 && k1 > 0) {
         const int nd = tr.node;
         tr.node = 0;  // the LDS slot as node 0 of a one-node "tree" at s_root + k1
-        if (node_step<STATS, false, PT_OCTANT != 0 && !ENV, true>(P.nodes, stk, tr, ct, (lds_cchar*)(s_root + k1), 1))
+        if (node_step<STATS, false, PT_OCTANT != 0 && (!ENV || PT_ENV_OCT), true>(P.nodes, stk, tr, ct, (lds_cchar*)(s_root + k1), 1))
           mode = M_SHADE;
         (void)nd;
       }
@@ -1438,9 +1446,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
               done = node_step_uniform<STATS>(P.nodes, n0, stk, tr, ct);
             } else
 #endif
-            // (the ENV build spills registers with the node fence or the
-            // octant loads: without)
-            done = node_step<STATS, (PT_LOAD_FENCE & 1) != 0 && !ENV, PT_OCTANT != 0 && !ENV,
+            done = node_step<STATS, (PT_LOAD_FENCE & 1) != 0 && (!ENV || PT_ENV_FENCE), PT_OCTANT != 0 && (!ENV || PT_ENV_OCT),
                              (PT_TREELET > 0) && !ENV>(P.nodes, stk, tr, ct, (lds_cchar*)s_tree, n_tree);
           }
         }

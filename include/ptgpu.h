@@ -6,7 +6,14 @@
  *   pt_create / pt_destroy      CUDAPathTracer::CUDAPathTracer / ~CUDAPathTracer
  *                               (cuda_src/setup.h:90-148, setup.cu:92-115)
  *   pt_upload_scene             CUDAPathTracer::init -> loadPrimitives/loadLights/
- *                               loadBVH (setup.cu:181-201, 249-476, 689-774)
+ *                               loadBVH (setup.cu:181-201, 249-476, 689-774).  The
+ *                               render tree is the library's own binned-SAH BVH over
+ *                               the handed-over primitives (the nearest
+ *                               hit does not depend on the tree); scene.nodes (the
+ *                               reference's tree) is validated and kept for
+ *                               PT_FLAG_REF_COUNTS, and rendered over when the
+ *                               environment sets PT_BVH_BUILD=ref.  Primitive ids
+ *                               reported anywhere stay in the caller's order.
  *   pt_upload_scene_lbvh        the same with the BVH built on the GPU: the reference's
  *                               PARALLEL_BUILD_BVH path CUDAPathTracer::buildBVH
  *                               (setup.cu:188-189, 478-686; kernel.cu:358-493) —
