@@ -155,5 +155,9 @@ def init_from_env(backend: str):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend)
+        if backend == "nccl":  # RCCL: bind the group to this rank's GPU (eager communicator init)
+            import torch
+            dist.init_process_group(backend, device_id=torch.device("cuda", torch.cuda.current_device()))
+        else:
+            dist.init_process_group(backend)
     return rank, world, local
