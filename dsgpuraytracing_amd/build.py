@@ -58,11 +58,16 @@ def build(force: bool = False, verbose: bool = False) -> str:
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
                "-Wno-unused-function", f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}", "-c", src, "-o", obj]
         cmd[1:1] = os.environ.get("PT_HIPCC_FLAGS", "").split()  # experiments, e.g. -DPT_MIN_WAVES_PER_SIMD=5
-        if src.endswith("pt_kernels.hip"):
+        base = os.path.basename(src)
+        if base in ("pt_kernels.hip", "pt_kernels_env.hip"):
             # SLP-packed float3 math (v_pk_*_f32) needs operand shuffles that
             # cost more VALU slots and VGPRs than the pairing saves here
             # (render_kernel 103 -> 99 VGPRs; C3 +3.5%)
             cmd.insert(1, "-fno-slp-vectorize")
+        if base == "pt_kernels.hip":
+            # iterative-ILP machine scheduling: C3 +1.7%, framed C3 +1.8% (the
+            # ENV kernels, -2.9% with it, live in pt_kernels_env.hip without it)
+            cmd[1:1] = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
         if src.endswith(".cpp") and "pt_api" not in src:
             cmd.insert(1, "-xc++")  # host-only translation units
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
