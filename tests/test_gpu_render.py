@@ -369,6 +369,37 @@ def test_own_sah_tree_matches_reference_tree(monkeypatch, name):
     assert frac >= 0.995 and rel_mean <= 1e-3, (frac, rel_mean)
 
 
+def test_own_sah_tree_degenerate_centroids(monkeypatch):
+    """40 copies of one triangle (every centroid equal: no SAH split exists, the
+    builder halves the range down to <= 4-primitive leaves) under a one-leaf
+    reference tree: same hits and distances as rendering over the reference
+    tree (which primitive of the identical copies answers may differ)."""
+    from dsgpuraytracing_amd.pathtracer import Device
+    d = dict(ptdump.read(golden("c1_default_64x64.scene.ptd")))
+    tri = int(np.flatnonzero(d["prim_type"] == 1)[0])
+    k = 40
+    for key, width in (("prim_geom", 9), ("prim_norm", 9)):
+        a = d[key].reshape(-1, width)
+        d[key] = np.concatenate([a, np.repeat(a[tri:tri + 1], k, 0)]).reshape(-1)
+    for key in ("prim_type", "prim_bsdf", "prim_orig"):
+        if key in d:
+            d[key] = np.concatenate([d[key], np.repeat(d[key][tri:tri + 1], k)])
+    n = len(d["prim_type"])
+    d["node_bb"] = d["node_bb"].reshape(-1, 6)[:1].reshape(-1).copy()
+    d["node_info"] = np.array([0, n, -1, -1], dtype=d["node_info"].dtype)
+    sc = Scene(native.SceneArrays(d))
+    rays = ptdump.read(golden("c1_rays.ptd"))
+    res = []
+    for mode in ("ref", "sah"):
+        monkeypatch.setenv("PT_BVH_BUILD", mode)
+        dev = Device(0)
+        dev.upload_scene(sc)
+        res.append(dev.intersect(rays["ray_o"], rays["ray_d"], rays["ray_maxt"]))
+    (h0, t0, _, a0), (h1, t1, _, a1) = res
+    assert h0.mean() > 0.2 and np.array_equal(h0, h1) and np.array_equal(a0, a1)
+    assert np.allclose(t0[h0 == 1], t1[h1 == 1], rtol=1e-6, atol=1e-7)
+
+
 def test_own_sah_tree_independent_of_build_threads(monkeypatch):
     """The SAH tree's subtrees are built on a pool of host threads: the tree,
     hence the frame, is bit-identical for any thread count."""
