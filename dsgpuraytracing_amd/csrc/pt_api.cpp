@@ -1188,15 +1188,16 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     if (w > 0) want = (int64_t)w * c->n_cu;
   }
   P.group_spp = PT_GROUP_SPP;
-  // Small FRAMES get one-sample groups: at least ~16 work slots per lane keep
-  // the tail short.  The grouping decides the float summation order of a
+  // Smaller FRAMES get smaller groups (down to one sample): at least ~16 work
+  // slots per lane keep the tail short.  The grouping decides the float summation order of a
   // pixel, so it is a function of the frame (W, H, spp) and the device's
   // resident grid only -- never of the launch's tile set or of a stats build:
   // any split of a frame into tile launches (raytrace_tile calls, the
   // multi-GPU shards) sums every pixel in the same order as the whole frame.
   const int64_t frame_px = (int64_t)P.W * P.H;
   const int64_t want_plain = std::getenv("PT_WAVES_PER_CU") ? want : c->grid_plain;
-  if (frame_px * ((P.spp + P.group_spp - 1) / P.group_spp) < want_plain * PT_BLOCK * 16) P.group_spp = 1;
+  while (P.group_spp > 1 && frame_px * ((P.spp + P.group_spp - 1) / P.group_spp) < want_plain * PT_BLOCK * 16)
+    P.group_spp /= 2;
   if (const char* g = std::getenv("PT_SAMPLE_GROUP")) {  // tuning knob
     int v = std::atoi(g);
     if (v > 0) P.group_spp = v;

@@ -50,7 +50,7 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 static_assert(PT_XCD_QUEUES >= 1 && PT_XCD_QUEUES <= 8, "at most 8 queues");
 static_assert(!(PT_PIXEL_ACC && PT_XCD_QUEUES > 1), "the pixel ring needs the single work queue");
 #ifndef PT_GROUP_SPP
-#define PT_GROUP_SPP 2  // default samples per work slot
+#define PT_GROUP_SPP 4  // default samples per work slot (C3 +3.3% over 2; 8 or more: C3 -4%, C5 -10%)
 #endif
 #ifndef PT_SHADE_BATCH
 #define PT_SHADE_BATCH 48  // default: leave traversal when this many lanes finished their ray
