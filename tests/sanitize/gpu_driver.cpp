@@ -6,7 +6,7 @@
 // whole-frame, single-tile, ragged, packed and device renders -> ray queries
 // -> stats / launch times / wave trace; then malformed scenes, tiles and
 // arguments, each of which must be refused with a PT_E_* code.
-// usage: gpu_driver <scene.dae> <env.exr>
+// usage: gpu_driver <scene.dae> <env.exr> [large_scene.dae]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -116,6 +116,26 @@ int main(int argc, char** argv) {
   OK(pt_host_scene_view(hs, &s, &cam));
   OK(pt_upload_scene(c, &s));
   OK(pt_render_tiles(c, &whole, 1, out.data(), 0));
+  // a large mesh (optional third argument, e.g. the C3 proxy): the SAH render
+  // tree's threaded subtree build, the render over it, the reference-count
+  // launch over the caller-order copy, and both trees again
+  if (argc > 3) {
+    pt_host_scene* hb = nullptr;
+    OK(pt_host_scene_load(argv[3], W, H, nullptr, &hb));
+    pt_scene sb2;
+    pt_camera cb2;
+    OK(pt_host_scene_view(hb, &sb2, &cb2));
+    OK(pt_upload_scene(c, &sb2));
+    OK(pt_set_camera(c, &cb2));
+    OK(pt_render_tiles(c, &whole, 1, out.data(), PT_FLAG_STATS));
+    OK(pt_render_tiles(c, &whole, 1, out.data(), PT_FLAG_REF_COUNTS));
+    OK(pt_intersect(c, 4, o.data(), d.data(), mt.data(), hit.data(), t.data(), prim.data(), any.data()));
+    setenv("PT_BVH_BUILD", "ref", 1);
+    OK(pt_upload_scene(c, &sb2));
+    OK(pt_render_tiles(c, &whole, 1, out.data(), 0));
+    unsetenv("PT_BVH_BUILD");
+    pt_host_scene_free(hb);
+  }
   (void)hipFree(dev);
   OK(pt_destroy(c));
   pt_host_scene_free(hs);

@@ -28,6 +28,6 @@ if [ "${1:-build}" = build ]; then
 else
   export ASAN_OPTIONS=detect_leaks=0:verify_asan_link_order=0:abort_on_error=0
   export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1
-  python -c "from dsgpuraytracing_amd import scenes; print(scenes.C1_DAE)" > /dev/null
-  timeout -k 10 180 "$OUT/gpu_driver" assets/CBspheres_lambertian.dae tests/golden/env_sky_64x32.exr
+  BIG=$(python -c "from dsgpuraytracing_amd import scenes; print(scenes.proxy_path(1))")
+  timeout -k 10 300 "$OUT/gpu_driver" assets/CBspheres_lambertian.dae tests/golden/env_sky_64x32.exr "$BIG"
 fi
