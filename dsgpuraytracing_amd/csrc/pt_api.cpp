@@ -165,7 +165,10 @@ struct pt_ctx {
   // the next frame's waves fill the CUs the previous frame's drain leaves
   // idle.  Each resolve runs on the caller's stream after its own render, so
   // the caller's stream order is kept for everything it can observe.
-  static constexpr int kSlots = 2;
+#ifndef PT_RENDER_SLOTS
+#define PT_RENDER_SLOTS 2
+#endif
+  static constexpr int kSlots = PT_RENDER_SLOTS;
   hipStream_t rstream[kSlots] = {};
   hipEvent_t ev_free[kSlots] = {};
   DevBuf<int4> tiles[kSlots];
