@@ -239,7 +239,8 @@ int pt_render_tiles_device(pt_ctx* ctx, const pt_tile* tiles, int32_t n_tiles, f
                            void* stream, uint32_t flags);
 /* Batched BVHAccel::intersect.  Rays: origin o[3n], direction d[3n] (normalised),
  * max_t[n] for the any-hit query.  Outputs (each nullable): nearest hit flag,
- * t, primitive index (BVH order), and the any-hit flag within (0, max_t). */
+ * t, primitive index (the caller's BVH order, whatever tree renders), and the any-hit
+ * flag within (0, max_t). */
 int pt_intersect(pt_ctx* ctx, int64_t n, const double* o, const double* d, const double* max_t,
                  int32_t* hit, float* t, int32_t* prim, int32_t* any_hit);
 /* Statistics of the last render (waits for its kernel-time events). */
