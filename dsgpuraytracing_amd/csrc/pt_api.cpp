@@ -405,6 +405,21 @@ static int build_host_bvh(const pt_scene* s, std::vector<DNode>& dn, std::vector
       out[s2].ref = b2[(size_t)n].ref[s2];
     }
   };
+  // primitives under each binary node (b2 is pre-order: children follow parents)
+  std::vector<double> under(b2.size(), 0.0);
+  for (size_t i = b2.size(); i-- > 0;)
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int r = b2[i].ref[s2];
+      under[i] += r >= 0 ? under[(size_t)r] : (double)(((~r) & 7) + 1);
+    }
+  // which internal child to open next: PT_COLLAPSE=area (default: the largest
+  // surface area), count (the most primitives), sah (area x primitives)
+  const char* cm = std::getenv("PT_COLLAPSE");
+  const int crit = !cm ? 0 : std::strcmp(cm, "count") == 0 ? 1 : std::strcmp(cm, "sah") == 0 ? 2 : 0;
+  auto weight = [&](const Child& c) {
+    const double n = c.ref >= 0 ? under[(size_t)c.ref] : 0.0;
+    return crit == 0 ? (double)area(c) : crit == 1 ? n : (double)area(c) * n;
+  };
   max_stack = 0;
   {
     struct Item4 { int b2node; int64_t parent; int slot; int stack; };
@@ -417,10 +432,10 @@ static int build_host_bvh(const pt_scene* s, std::vector<DNode>& dn, std::vector
       kids(it.b2node, ch);
       while (n < 4) {
         int best = -1;
-        float ba = -1.f;
+        double ba = -1.0;
         for (int k = 0; k < n; ++k)
-          if (ch[k].ref >= 0 && area(ch[k]) > ba) {
-            ba = area(ch[k]);
+          if (ch[k].ref >= 0 && weight(ch[k]) > ba) {
+            ba = weight(ch[k]);
             best = k;
           }
         if (best < 0) break;
