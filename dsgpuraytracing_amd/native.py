@@ -120,6 +120,7 @@ _SIGS = {
     "pt_host_scene_set_envmap": (c_int32, [c_void_p, c_char_p]),
     "pt_host_load_exr": (c_int32, [c_char_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_void_p)]),
     "pt_host_free": (None, [c_void_p]),
+    "pt_host_build_render_tree": (c_int32, [c_void_p, c_void_p, POINTER(c_int64), c_void_p]),
 }
 
 _lib = None

@@ -52,6 +52,14 @@ int pt_host_scene_set_envmap(pt_host_scene* hs, const char* exr_path);
 int pt_host_scene_dump(const pt_host_scene* hs, const char* path);
 void pt_host_scene_free(pt_host_scene* hs);
 
+/* The render tree pt_upload_scene traverses: this library's own
+ * binned-SAH binary BVH over scene's primitives, in pt_bvh_node form (nodes[0] the
+ * root, children by index, leaves of <= 4 primitives as [start, start+range) of the
+ * permuted order).  perm[i] = the scene index of the i-th primitive in that order.
+ * nodes must hold 2*n_prims-1 entries, perm n_prims; *n_nodes receives the count.
+ * Deterministic: independent of the number of host threads used (PT_BUILD_THREADS). */
+int pt_host_build_render_tree(const pt_scene* scene, pt_bvh_node* nodes, int64_t* n_nodes, int64_t* perm);
+
 /* Reads an OpenEXR file into a malloc'd float RGB array (width*height*3, row 0
  * = first scanline = +y for lat-long maps); free it with pt_host_free. */
 int pt_host_load_exr(const char* path, int32_t* width, int32_t* height, float** rgb);

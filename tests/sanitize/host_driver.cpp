@@ -48,6 +48,13 @@ int main(int argc, char** argv) {
           acc += s.prim_type[k] + s.prim_bsdf[k] + s.prim_geom[9 * k + 8] + s.prim_norm[9 * k + 8];
         for (int64_t k = 0; rc == PT_OK && k < s.n_nodes; ++k) acc += s.nodes[k].bb_max[2] + (double)s.nodes[k].right;
         if (rc == PT_OK && dump) rc = pt_host_scene_dump(hs, dump);
+        if (rc == PT_OK) {  // the render tree pt_upload_scene builds (threaded for big meshes)
+          std::vector<pt_bvh_node> tree((size_t)(2 * s.n_prims - 1));
+          std::vector<int64_t> perm((size_t)s.n_prims);
+          int64_t nn = 0;
+          rc = pt_host_build_render_tree(&s, tree.data(), &nn, perm.data());
+          for (int64_t k = 0; rc == PT_OK && k < nn; ++k) acc += tree[(size_t)k].bb_min[0] + (double)perm[(size_t)(k % s.n_prims)];
+        }
         if (acc == 12345.678) std::puts("");
       }
       pt_host_scene_free(hs);

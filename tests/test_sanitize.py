@@ -2,7 +2,7 @@
 libptgpu.so (the reference has no such check; the native host
 scene pipeline parses untrusted COLLADA XML and OpenEXR files).
 
-tests/sanitize/host_driver.cpp is linked with csrc/scene_host.cpp,
+tests/sanitize/host_driver.cpp is linked with csrc/scene_host.cpp, csrc/render_tree.cpp,
 csrc/exr_io.cpp, csrc/image_out.cpp and csrc/pt_error.cpp built with
 -fsanitize=address,undefined (no recovery) and run over every committed
 scene, camera, environment map and the toColor fixture, then over corrupted
@@ -29,9 +29,9 @@ def driver(tmp_path_factory):
         pytest.skip("no g++")
     exe = str(tmp_path_factory.mktemp("san") / "host_driver")
     srcs = [os.path.join(ROOT, "tests", "sanitize", "host_driver.cpp")] + \
-        [os.path.join(CSRC, f) for f in ("scene_host.cpp", "exr_io.cpp", "image_out.cpp", "pt_error.cpp")]
+        [os.path.join(CSRC, f) for f in ("scene_host.cpp", "render_tree.cpp", "exr_io.cpp", "image_out.cpp", "pt_error.cpp")]
     r = subprocess.run([cxx, "-std=c++17", "-O1", "-g"] + SAN + [f"-I{ROOT}/include", f"-I{CSRC}"] + srcs +
-                       ["-lz", "-o", exe], capture_output=True, text=True)
+                       ["-lz", "-pthread", "-o", exe], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-3000:]
     return exe
 

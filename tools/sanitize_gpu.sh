@@ -17,7 +17,7 @@ if [ "${1:-build}" = build ]; then
     hipcc --offload-arch=gfx950 -O1 -g -std=c++17 $SAN $INC -fno-slp-vectorize -x hip -c "$f" -o "$o" &
     objs+=("$o")
   done
-  for f in scene_host exr_io image_out pt_error; do
+  for f in scene_host render_tree exr_io image_out pt_error; do
     o="$OUT/$f.o"
     hipcc -O1 -g -std=c++17 -fsanitize=address,undefined -fno-sanitize-recover=all -fno-gpu-sanitize $INC -xc++ -c "dsgpuraytracing_amd/csrc/$f.cpp" -o "$o" &
     objs+=("$o")
