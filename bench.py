@@ -262,7 +262,7 @@ def main():
     ap.add_argument("--scene-dump", default=None, help="PTDUMP scene instead of the native .dae loader")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
-                    help="N = 1: skip the framed-C3 and single-GPU C4 companion measurements")
+                    help="N = 1: skip the companion measurements (framed C3, single-GPU C4 and C5, C3 over the GPU LBVH)")
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
                     help="default: c3 on one GPU, c4 (the BASELINE multi-GPU config) on N > 1")
     ap.add_argument("--lbvh", action="store_true", help="build the BVH on the GPU (pt_upload_scene_lbvh)")
@@ -505,17 +505,25 @@ def companions(dev0, local, stream, frames):
         sample is traced (the headline's default camera leaves ~75% of the
         frame outside the scene's footprint);
       * c4_single_gpu: BASELINE C4 on this one GPU, the 1-GPU point of the
-        multi-GPU (C4, strong) scaling curve."""
+        multi-GPU (C4, strong) scaling curve;
+      * c5_single_gpu: BASELINE C5 (glass/mirror proxy + environment light)
+        on this one GPU;
+      * c3_lbvh: the headline workload over the GPU-built LBVH
+        (pt_upload_scene_lbvh) instead of the host SAH tree."""
     import torch
 
     from dsgpuraytracing_amd.pathtracer import Device, Scene, tile_fifo
     res = {}
-    for name in ("c3f", "c4"):
+    names = {"c3f": "c3_framed", "c4": "c4_single_gpu", "c5": "c5_single_gpu", "c3": "c3_lbvh"}
+    for name in ("c3f", "c4", "c5", "c3"):
         wl = WORKLOADS[name]
+        lbvh = name == "c3"
         dae, envmap, cam = workload_scene(wl)
         sc = Scene.from_dae(dae, wl["w"], wl["h"], cam_info=cam, envmap=envmap)
         dev = Device(local)
-        dev.upload_scene(sc)
+        t_up = time.perf_counter()
+        dev.upload_scene(sc, gpu_bvh=lbvh)
+        t_up = time.perf_counter() - t_up
         dev.set_camera(sc.camera)
         dev.set_params(wl["w"], wl["h"], wl["spp"], DEPTH, NSL, SEED)
         tl = np.asarray(tile_fifo(wl["w"], wl["h"]), np.int32)
@@ -531,11 +539,12 @@ def companions(dev0, local, stream, frames):
         el = time.perf_counter() - t0
         k, _ = dev.launch_times(frames)
         rays = st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]
-        res["c3_framed" if name == "c3f" else "c4_single_gpu"] = {
+        res[names[name]] = {
             "workload": wl["desc"], "value": round(wl["w"] * wl["h"] * wl["spp"] * frames / el / 1e6, 1),
             "unit": "Mrays/s", "ms_per_step": round(el / frames * 1e3, 3), "kernel_ms": round(float(np.mean(k)), 3),
             "frames": frames, "culled_samples": st["culled_samples"],
-            "ray_casts_per_s_M": round(rays * frames / el / 1e6, 1)}
+            "ray_casts_per_s_M": round(rays * frames / el / 1e6, 1), "upload_s": round(t_up, 4),
+            "bvh": "gpu-lbvh" if lbvh else "own binned SAH (host)"}
         dev.close()
         del fr
     return res

@@ -72,6 +72,9 @@ static_assert(!(PT_PIXEL_ACC && PT_XCD_QUEUES > 1), "the pixel ring needs the si
 #ifndef PT_STACK
 #define PT_STACK 24  // traversal stack entries per lane in LDS (lane-contiguous)
 #endif
+#ifndef PT_REG_TOP
+#define PT_REG_TOP 0  // 1: the top traversal-stack entry lives in a register (pop reads it, the LDS refill is off the critical path)
+#endif
 #ifndef PT_STACK_MAX
 #define PT_STACK_MAX 128  // deepest worst-case stack accepted (entries past PT_STACK spill to global memory)
 #endif

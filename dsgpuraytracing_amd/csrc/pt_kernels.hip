@@ -175,6 +175,9 @@ struct Trav {
   float tmax;
   int node, sp;
   int prim;
+#if PT_REG_TOP
+  int top;  // the stack's top entry (logical entry sp - 1); entries 0 .. sp - 2 are in the stack memory
+#endif
   bool any, found;
 };
 
@@ -188,6 +191,9 @@ __device__ __forceinline__ void trav_init(Trav& tr, float3 o, float3 d, float tm
   tr.tmax = tmax;
   tr.node = 0;
   tr.sp = 0;
+#if PT_REG_TOP
+  tr.top = 0;
+#endif
   tr.any = any;
   tr.found = false;
   tr.prim = -1;
@@ -292,7 +298,14 @@ struct Stack {
 __device__ __forceinline__ bool trav_pop(const Stack& stk, Trav& tr) {
   if (tr.sp == 0) return true;
   --tr.sp;
+#if PT_REG_TOP
+  // continue with the register top; refill it from the entry below, whose
+  // value is needed only at the next push or pop (off this step's critical path)
+  tr.node = tr.top;
+  tr.top = stk.get(tr.sp > 0 ? tr.sp - 1 : 0);
+#else
   tr.node = stk.get(tr.sp);
+#endif
   return false;
 }
 
@@ -324,6 +337,29 @@ __device__ __forceinline__ bool node_order(const Stack& stk, Trav& tr, const flo
   // hits are a sorted prefix, so with room for three entries every candidate
   // is written and the top only advances past hits (no branches).
   int sp = tr.sp;
+#if PT_REG_TOP
+  // the old register top goes to memory (redundant when nothing is pushed),
+  // the farther hits below the new top, the second-nearest hit into the register
+  if (sp + 2 <= PT_STACK) {
+    stk.lds[(sp > 0 ? sp - 1 : 0) * PT_BLOCK] = tr.top;
+    stk.lds[sp * PT_BLOCK] = r3;
+    sp += d3 != kMiss;
+    stk.lds[sp * PT_BLOCK] = r2;
+    sp += d2 != kMiss;
+    const bool h1 = d1 != kMiss;
+    sp += h1;
+    tr.top = h1 ? r1 : tr.top;
+  } else if (d1 != kMiss) {
+    if (sp > 0) stk.put(sp - 1, tr.top);
+    if (d3 != kMiss) stk.put(sp++, r3);
+    if (d2 != kMiss) stk.put(sp++, r2);
+    ++sp;
+    tr.top = r1;
+  }
+  tr.sp = sp;
+  tr.node = r0;
+  return false;
+#endif
   if (sp + 3 <= PT_STACK) {
     stk.lds[sp * PT_BLOCK] = r3;
     sp += d3 != kMiss;
@@ -518,7 +554,12 @@ __device__ __forceinline__ bool node_step2(const DNode2* __restrict__ nodes, con
   bool in1 = tn1 <= tf1;
   if (in0 && in1) {
     bool first0 = tn0 <= tn1;
+#if PT_REG_TOP
+    if (tr.sp > 0) stk.put(tr.sp - 1, tr.top);
+    tr.top = first0 ? e.y : e.x;
+#else
     stk.put(tr.sp, first0 ? e.y : e.x);
+#endif
     ++tr.sp;
     tr.node = first0 ? e.x : e.y;
   } else if (in0) {
