@@ -1,0 +1,74 @@
+"""CPU checks of bench.py's measurement logic (no GPU): the SURVEY §8(d)
+algorithmic-bytes cost model, the roofline views built from the committed PMC
+summary, and the agreement of that summary with the rocprofv3 kernel trace
+committed beside it (profiles/<round>/)."""
+import csv
+import json
+import os
+
+import pytest
+
+import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_algorithmic_bytes_is_the_survey_cost_model():
+    # the C3 counters the round-1 review recomputed by hand: 29.57 GB per launch
+    st = {"node_visits": 392_438_744, "tri_tests": 72_187_422, "sphere_tests": 0, "ext_hits": 19_000_062,
+          "pixels": 1_048_576}
+    want = 64 * 392_438_744 + 48 * 72_187_422 + 4 * 72_187_422 + 36 * 19_000_062 + 12 * 1_048_576
+    assert bench.algorithmic_bytes(st) == want
+    assert abs(want / 1e9 - 29.57) < 0.01
+    # spheres: 16 B per test plus the 4-B primitive index
+    st2 = dict(st, tri_tests=0, sphere_tests=10, node_visits=0, ext_hits=0, pixels=0)
+    assert bench.algorithmic_bytes(st2) == 10 * (16 + 4)
+
+
+def test_roofline_views_are_fractions_and_bound_is_the_largest_measured():
+    pm = bench.profile_summary("c3")
+    assert pm is not None, "profiles/<round>/c3_summary.json missing"
+    kernel_ms, frame_ms = pm["avg_ms"], 1.6
+    alg = 29.5e9
+    r = bench.roofline("c3", kernel_ms, alg, frame_ms)
+    views = r["views"]
+    for k in ("hbm", "l2", "valu", "algorithmic_cache_served"):
+        assert k in views, k
+        assert 0.0 < views[k]["frac"] <= 1.0, (k, views[k])
+        # per-frame fraction = the same counts over the frame interval
+        assert views[k]["frac_per_frame"] == pytest.approx(views[k]["frac"] * kernel_ms / frame_ms, rel=1e-3)
+    measured = {k: views[k]["frac"] for k in ("hbm", "l2", "valu")}
+    assert r["bound"] == max(measured, key=measured.get)
+    assert r["frac"] == views[r["bound"]]["frac"]
+    assert r["traffic"] == pm["hbm_bytes_per_launch"]
+    # HBM bytes from the PMC passes: 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction), in KB
+    assert pm["hbm_bytes_per_launch"] == pytest.approx((2 * pm["fetch_size_kb"] + pm["write_size_kb"]) * 1024,
+                                                       rel=1e-6)
+
+
+def test_pmc_summary_agrees_with_committed_kernel_trace():
+    pm = bench.profile_summary("c3")
+    src = pm["source"] if os.path.isabs(pm.get("source", "")) else os.path.join(ROOT, pm["source"])
+    stats = os.path.join(os.path.dirname(src), "c3_kernel_stats.csv")
+    assert os.path.exists(stats), stats
+    with open(stats) as f:
+        rows = {r["Name"]: r for r in csv.DictReader(f)}
+    name = "void ptk::render_kernel<false, false, false, false, false>(KParams)"
+    assert name in rows
+    avg_ms = float(rows[name]["AverageNs"]) * 1e-6
+    assert avg_ms == pytest.approx(pm["avg_ms"], rel=0.02)
+
+
+def test_committed_bench_lines_keep_the_contract():
+    path = os.path.join(ROOT, "profiles", "r2", "bench_c3_default.jsonl")
+    with open(path) as f:
+        d = json.loads(f.read().strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["metric"] == bench.HEADLINE_METRIC
+    assert d["value"] == pytest.approx(1024 * 1024 * 64 / (d["config"]["render_time_s"] * 1e6), rel=0.02)
+    assert 0.0 < d["roofline"]["frac"] <= 1.0
+    assert d["cpu_baseline"]["kind"] in ("reference", "port") and d["cpu_baseline"]["cores"] >= 1
+    for name in ("c3_framed", "c4_single_gpu", "c5_single_gpu", "c3_lbvh"):
+        assert d["companions"][name]["value"] > 0, name
