@@ -72,6 +72,9 @@ static_assert(!(PT_PIXEL_ACC && PT_XCD_QUEUES > 1), "the pixel ring needs the si
 #ifndef PT_STACK
 #define PT_STACK 24  // traversal stack entries per lane in LDS (lane-contiguous)
 #endif
+#ifndef PT_NLS_RCP
+#define PT_NLS_RCP 1  // 1 (default; C3 +0.5% same-session): the 1/ns_area_light sample weight through v_rcp_f32 instead of an IEEE division
+#endif
 #ifndef PT_REG_TOP
 #define PT_REG_TOP 0  // 1: the top traversal-stack entry lives in a register (pop reads it, the LDS refill is off the critical path)
 #endif

@@ -852,7 +852,9 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
 #if PT_PIXEL_ACC
   int rslot = 0;  // the pixel's accumulator in the wave's ring
 #endif
-  uint32_t rbase = 0, rdim = 0;
+  // the sample's stream and the counter word of its next draw (ptrng::draw_at)
+  uint32_t rbase = 0, rdim = ptrng::kDrawInit;
+#define PT_DRAW() ptrng::draw_at(rbase, (rdim += ptrng::kDrawStep) - ptrng::kDrawStep)
   float3 acc = f3(0, 0, 0);  // the slot's radiance sum: each path contribution is added as it is found
   float3 T = f3(1, 1, 1);    // path throughput
   // path depth (bits 0-7) and the NEE cursor: light sample (8-15), light
@@ -1046,13 +1048,13 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
           float dist, pdf;
           bool lit = true;
           if (ENV && ltype == 4) {  // EnvironmentLight::sample_L (environment_light.cpp:117-128)
-            float r1 = ptrng::draw(rbase, rdim++);
-            float r2 = ptrng::draw(rbase, rdim++);
+            float r1 = PT_DRAW();
+            float r2 = PT_DRAW();
             env_sample(P, r1, r2, wi, pdf);
             dist = 3.0e38f;
           } else if (ltype == 3) {  // AreaLight::sample_L (light.cpp:80-92); grid sampler draws y first
-            float u0 = ptrng::draw(rbase, rdim++);
-            float u1 = ptrng::draw(rbase, rdim++);
+            float u0 = PT_DRAW();
+            float u1 = PT_DRAW();
             float sx = u1 - 0.5f, sy = u0 - 0.5f;
             float3 dv = PT_LIGHT3(li, pos) + PT_LIGHT3(li, dimx) * sx + PT_LIGHT3(li, dimy) * sy - hp;
             float cosL = dot(dv, PT_LIGHT3(li, dir));
@@ -1062,8 +1064,8 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
             pdf = sq * rcp(light_f(li, offsetof(DLight, area) / 4) * fabsf(cosL));  // unnormalised d.dir, as the reference
             lit = cosL < 0.0f;
           } else if (ltype == 1) {  // InfiniteHemisphereLight (light.cpp:34-42)
-            float r1 = ptrng::draw(rbase, rdim++);
-            float r2 = ptrng::draw(rbase, rdim++);
+            float r1 = PT_DRAW();
+            float r2 = PT_DRAW();
             float st = fsqrt(fmaxf(0.0f, 1.0f - r1 * r1));
             wi = f3(st * cos_rev(r2), r1, -st * sin_rev(r2));  // phi = 2 pi r2
             dist = 3.0e38f;
@@ -1078,7 +1080,11 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
             dist = 3.0e38f;
             pdf = 1.0f;
           }
+#if PT_NLS_RCP
+          const float scale = rcp((float)nls);  // v_rcp_f32: exact for 1, 2, 4, ... light samples
+#else
           const float scale = 1.0f / (float)nls;
+#endif
           ++ls;
           emit_last = ls >= nls && li + 1 >= P.n_lights;
           // f() is zero for every BSDF but Diffuse (bsdf.cpp:34-202): nothing to add.
@@ -1117,8 +1123,8 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
           float pdf = 1.0f;
           float3 f;
           if (btype == 0 || btype == 4) {  // cosine hemisphere (sampler.cpp:44-55)
-            float r1 = ptrng::draw(rbase, rdim++);
-            float r2 = ptrng::draw(rbase, rdim++);
+            float r1 = PT_DRAW();
+            float r2 = PT_DRAW();
             float ct = fsqrt(1.0f - r1);  // cos(acos(1 - 2 r1) / 2)
             float stt = fsqrt(r1);
             wi = f3(stt * cos_rev(r2), stt * sin_rev(r2), ct);  // phi = 2 pi r2
@@ -1157,7 +1163,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
               float r1 = (no * ci - ni * co) / (no * ci + ni * co);
               float r2 = (ni * ci - no * co) / (ni * ci + no * co);
               float Fr = 0.5f * (r1 * r1 + r2 * r2);
-              if (ptrng::draw(rbase, rdim++) <= Fr) {
+              if (PT_DRAW() <= Fr) {
                 wi = f3(-wo.x, -wo.y, wo.z);
                 f = PT_BSDF3(bsdf, a) * (1.0f / fmaxf(fabsf(wi.z), 1e-8f));
               } else {
@@ -1167,12 +1173,12 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
           }
           // Russian roulette (pathtracer.cpp:534-541)
           float pterm = fmaxf(1.0f - illum(f), 0.0f);
-          if (ptrng::draw(rbase, rdim++) < pterm) {
+          if (PT_DRAW() < pterm) {
             if (DBG && pix == P.dbg_pix) printf("    RR terminate (p=%.4g)\n", pterm);
             if (emitted) post = 2;
             else finish = true;
           } else {
-            if (DBG && pix == P.dbg_pix) printf("    bounce wi=(%.6g %.6g %.6g) pdf %.5g p %.4g dim %u\n", wi.x, wi.y, wi.z, pdf, pterm, rdim);
+            if (DBG && pix == P.dbg_pix) printf("    bounce wi=(%.6g %.6g %.6g) pdf %.5g p %.4g dim word %08x\n", wi.x, wi.y, wi.z, pdf, pterm, rdim);
             T = mul(T, f * (fabsf(wi.z) * rcp(pdf * (1.0f - pterm))));
             float3 v = normalize(fr.to_world(wi));
             const float3 bo = offset_ray(hp, dot(v, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng);
@@ -1392,10 +1398,10 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
       // jittered pixel position of raytrace_pixel (pathtracer.cpp:571-575)
       while (mode == M_CAMERA) {
         rbase = ptrng::stream_base(P.seed, (uint32_t)pix, (uint32_t)sample + P.sample_base);
-        rdim = 0;
+        rdim = ptrng::kDrawInit;
         const int py = pix / P.W, px = pix - py * P.W;
-        float ry = ptrng::draw(rbase, rdim++);  // UniformGridSampler2D draws y first
-        float rx = ptrng::draw(rbase, rdim++);
+        float ry = PT_DRAW();  // UniformGridSampler2D draws y first
+        float rx = PT_DRAW();
         float fx = ((float)px + rx) * P.inv_w;
         float fy = ((float)py + ry) * P.inv_h;
         float3 sp = f3((0.5f - fx) * P.cam_ax, (0.5f - fy) * P.cam_ay, 1.0f);

@@ -34,10 +34,18 @@ PT_HD uint32_t stream_base(uint32_t seed, uint32_t pixel, uint32_t sample) {
   return lowbias32(h ^ (sample * 0x85EBCA6BU));
 }
 
-// Draw k of a stream as a 24-bit uniform in [0, 1), exact in float.
-PT_HD float draw(uint32_t base, uint32_t k) {
-  uint32_t h = lowbias32(base ^ (k * 0xC2B2AE35U + 0x27D4EB2FU));
+// Counter word of draw k: k * kDrawStep + kDrawInit (mod 2^32).  The kernel
+// keeps the word itself and adds kDrawStep per draw (no integer multiply,
+// a quarter-rate VALU op on CDNA), bit-identical to draw(base, k).
+constexpr uint32_t kDrawStep = 0xC2B2AE35U, kDrawInit = 0x27D4EB2FU;
+
+// The draw with counter word kc as a 24-bit uniform in [0, 1), exact in float.
+PT_HD float draw_at(uint32_t base, uint32_t kc) {
+  uint32_t h = lowbias32(base ^ kc);
   return (float)(h >> 8) * (1.0f / 16777216.0f);
 }
+
+// Draw k of a stream.
+PT_HD float draw(uint32_t base, uint32_t k) { return draw_at(base, k * kDrawStep + kDrawInit); }
 
 }  // namespace ptrng
