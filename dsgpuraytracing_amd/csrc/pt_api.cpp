@@ -820,6 +820,8 @@ int pt_set_params(pt_ctx* c, const pt_params* p) {
   if (p->max_depth > 254 || p->ns_area_light > 255)  // packed in 8 bits each in the kernel's path state
     return fail(PT_E_INVALID, "pt_set_params: max_depth must be <= 254 and ns_area_light <= 255");
   if ((int64_t)p->width * p->height > (int64_t)1 << 30) return fail(PT_E_INVALID, "pt_set_params: frame too large");
+  if (p->width > 65535 || p->height > 65535)  // pixel coordinates are packed in 16 bits each in the kernel
+    return fail(PT_E_INVALID, "pt_set_params: width and height must be <= 65535");
   c->params = *p;
   c->have_params = true;
   return PT_OK;
@@ -1063,6 +1065,13 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   HIPCHK(c->partial[slot].reserve((size_t)(npx * P.n_groups) * 3));
   P.partial = c->partial[slot].p;
 #endif
+  auto log2_exact = [](int v) {  // log2(v) for a power of two, else -1
+    int k = 0;
+    while ((1 << k) < v && k < 30) ++k;
+    return (1 << k) == v ? k : -1;
+  };
+  P.group_shift = log2_exact(P.group_spp);
+  P.ngroup_shift = log2_exact(P.n_groups);
   int64_t max_grid = std::max<int64_t>(1, (slots + PT_BLOCK - 1) / PT_BLOCK);
   int grid = (int)std::min<int64_t>(want, max_grid);
   if (stats && (size_t)grid * PT_WAVE_TRACE + PT_STATS_SLOTS > c->stats.n) grid = (int)((c->stats.n - PT_STATS_SLOTS) / PT_WAVE_TRACE);

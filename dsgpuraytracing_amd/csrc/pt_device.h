@@ -72,6 +72,9 @@ static_assert(!(PT_PIXEL_ACC && PT_XCD_QUEUES > 1), "the pixel ring needs the si
 #ifndef PT_STACK
 #define PT_STACK 24  // traversal stack entries per lane in LDS (lane-contiguous)
 #endif
+#ifndef PT_INT_SHORTCUTS
+#define PT_INT_SHORTCUTS 1  // group / slot arithmetic by shifts for power-of-two sizes, pixel coordinates packed (W, H <= 65535)
+#endif
 #ifndef PT_NLS_RCP
 #define PT_NLS_RCP 1  // 1 (default; C3 +0.5% same-session): the 1/ns_area_light sample weight through v_rcp_f32 instead of an IEEE division
 #endif
@@ -152,6 +155,8 @@ struct KParams {
   int n_tiles;     // 32x32 (or smaller) tiles: 1024 pixels each
   int group_spp;   // samples per work slot (a slot is one pixel's sample group)
   int n_groups;    // ceil(spp / group_spp): slots per pixel
+  int group_shift;   // log2(group_spp) when a power of two, else -1 (shifts instead of divisions)
+  int ngroup_shift;  // log2(n_groups) when a power of two, else -1
   const DNode* nodes;
   const DNode2* nodes2;  // the binary tree (reference-count launch only)
   const DPrim* prims;

@@ -916,6 +916,25 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
   }
 
   const uint32_t n_groups = (uint32_t)P.n_groups;
+#if PT_INT_SHORTCUTS
+  // group arithmetic by shifts when the sizes are powers of two (the usual
+  // case; wave-uniform branches), the exact divisions otherwise
+  auto group_of = [&](int s) -> int { return P.group_shift >= 0 ? s >> P.group_shift : s / P.group_spp; };
+  auto group_starts = [&](int s) -> bool {
+    return P.group_shift >= 0 ? (s & (P.group_spp - 1)) == 0 : s % P.group_spp == 0;
+  };
+  auto pixel_of_slot = [&](uint32_t slot) -> uint32_t {
+    return P.ngroup_shift >= 0 ? slot >> P.ngroup_shift : slot / n_groups;
+  };
+  // `pix` holds the pixel's coordinates (x | y << 16, W, H <= 65535) and its
+  // index is rebuilt with one multiply-add: no division per camera ray
+  auto pix_index = [&](int p) -> int { return (p & 0xffff) + (int)((uint32_t)p >> 16) * P.W; };
+#else
+  auto group_of = [&](int s) -> int { return s / P.group_spp; };
+  auto group_starts = [&](int s) -> bool { return s % P.group_spp == 0; };
+  auto pixel_of_slot = [&](uint32_t slot) -> uint32_t { return slot / n_groups; };
+  auto pix_index = [&](int p) -> int { return p; };
+#endif
 #if PT_PIXEL_ACC
   // A sample of this lane's pixel finished (`sample` already advanced).  The
   // lane sums its group's samples in float (in sample order, as the group
@@ -926,7 +945,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
   auto sample_done = [&]() {
     if (sample < P.spp && sample % P.group_spp != 0) return;  // the group goes on
     if (n_groups == 1u) {
-      store3(P.fb + 3 * (size_t)pix, acc * (float)(1.0 / (double)P.spp));
+      store3(P.fb + 3 * (size_t)pix_index(pix), acc * (float)(1.0 / (double)P.spp));
       return;
     }
     __hip_atomic_fetch_add((lds_u64*)&ring[rslot].s[0], to_fixed32(acc.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -936,7 +955,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
     if (done == n_groups - 1u) {  // the pixel's last group: every add above is in
       const double k = 2.3283064365386963e-10 / (double)P.spp;  // 2^-32 / spp
-      store3(P.fb + 3 * (size_t)pix, f3((float)((double)ring[rslot].s[0] * k), (float)((double)ring[rslot].s[1] * k),
+      store3(P.fb + 3 * (size_t)pix_index(pix), f3((float)((double)ring[rslot].s[0] * k), (float)((double)ring[rslot].s[1] * k),
                                         (float)((double)ring[rslot].s[2] * k)));
       ring[rslot].s[0] = ring[rslot].s[1] = ring[rslot].s[2] = 0ull;
       ring[rslot].count = 0u;
@@ -947,7 +966,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
 #else
   // partial-sum slot of a finished group: (pixel, group of the last sample)
   auto slot_of = [&](int p, int s_next) -> size_t {
-    return (size_t)p * n_groups + (uint32_t)((s_next - 1) / P.group_spp);
+    return (size_t)pix_index(p) * n_groups + (uint32_t)group_of(s_next - 1);
   };
 #endif
   const uint32_t total_slots = (uint32_t)P.n_blocks * 64u * n_groups;
@@ -966,7 +985,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
       int stage;            // 0: NEE loop, 1: BSDF step, 2: none
       if (shadow) {
         if (!found) acc = acc + pend;  // unoccluded (the light sample was already counted)
-        if (DBG && pix == P.dbg_pix) printf("    shadow %s (pend %.6g) prim %d t %.9g\n", found ? "occluded" : "clear", pend.x, tr.prim, tr.tmax);
+        if (DBG && pix_index(pix) == P.dbg_pix) printf("    shadow %s (pend %.6g) prim %d t %.9g\n", found ? "occluded" : "clear", pend.x, tr.prim, tr.tmax);
         stage = 0;
         if (PT_EARLY_BOUNCE && post == 1) {  // the bounce was sampled with the last light sample
           trav_init(tr, hp, ns, 3.0e38f, false);
@@ -1023,7 +1042,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         if ((meta & 1) && dot(tr.d, ns) > 0.0f) ns = f3(0, 0, 0) - ns;
         ng = normalize(ng);
         if (includeLe) acc = acc + mul(T, PT_BSDF3(bsdf, e));
-        if (DBG && pix == P.dbg_pix) printf("  depth %d hit prim %d bsdf %d t=%.9g n=(%.6g %.6g %.6g) T=(%.5g)\n", (int)(cur & 0xffu), tr.prim, bsdf, tr.tmax, ns.x, ns.y, ns.z, T.x);
+        if (DBG && pix_index(pix) == P.dbg_pix) printf("  depth %d hit prim %d bsdf %d t=%.9g n=(%.6g %.6g %.6g) T=(%.5g)\n", (int)(cur & 0xffu), tr.prim, bsdf, tr.tmax, ns.x, ns.y, ns.z, T.x);
         cur &= 0xffu;  // NEE starts at light 0, sample 0
         stage = 0;
       }
@@ -1097,7 +1116,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
           // shadow ray (pathtracer.cpp:497-504): delta lights offset EPS_N along n
           float3 so = delta ? hp + ns * 5e-3f : offset_ray(hp, dot(wi, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng);
           trav_init(tr, so, wi, dist * 0.999f, true);
-          if (DBG && pix == P.dbg_pix) printf("    shadow o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) maxt=%.9g cos %.4g pdf %.4g\n", so.x, so.y, so.z, wi.x, wi.y, wi.z, tr.tmax, cos_t, pdf);
+          if (DBG && pix_index(pix) == P.dbg_pix) printf("    shadow o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) maxt=%.9g cos %.4g pdf %.4g\n", so.x, so.y, so.z, wi.x, wi.y, wi.z, tr.tmax, cos_t, pdf);
           emitted = true;
           if (STATS) n_shadow++;
           break;
@@ -1174,11 +1193,11 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
           // Russian roulette (pathtracer.cpp:534-541)
           float pterm = fmaxf(1.0f - illum(f), 0.0f);
           if (PT_DRAW() < pterm) {
-            if (DBG && pix == P.dbg_pix) printf("    RR terminate (p=%.4g)\n", pterm);
+            if (DBG && pix_index(pix) == P.dbg_pix) printf("    RR terminate (p=%.4g)\n", pterm);
             if (emitted) post = 2;
             else finish = true;
           } else {
-            if (DBG && pix == P.dbg_pix) printf("    bounce wi=(%.6g %.6g %.6g) pdf %.5g p %.4g dim word %08x\n", wi.x, wi.y, wi.z, pdf, pterm, rdim);
+            if (DBG && pix_index(pix) == P.dbg_pix) printf("    bounce wi=(%.6g %.6g %.6g) pdf %.5g p %.4g dim word %08x\n", wi.x, wi.y, wi.z, pdf, pterm, rdim);
             T = mul(T, f * (fabsf(wi.z) * rcp(pdf * (1.0f - pterm))));
             float3 v = normalize(fr.to_world(wi));
             const float3 bo = offset_ray(hp, dot(v, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng);
@@ -1203,7 +1222,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
 #if PT_PIXEL_ACC
         sample_done();
 #endif
-        if (sample < P.spp && sample % P.group_spp != 0) {
+        if (sample < P.spp && !group_starts(sample)) {
           mode = M_CAMERA;
         } else {
 #if !PT_PIXEL_ACC
@@ -1274,12 +1293,16 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
               if (STATS && w_empty == 0ull) w_empty = wall_clock64();
             }
           } else {
-            uint32_t bq = slot / n_groups;
+            uint32_t bq = pixel_of_slot(slot);
             uint32_t g = slot - bq * n_groups;
             int4 b = P.blocks[bq >> 6];
             int qx = (int)(bq & 7u), qy = (int)((bq >> 3) & 7u);
             if (qx < b.z && qy < b.w) {
+#if PT_INT_SHORTCUTS
+              pix = (b.x + qx) | ((b.y + qy) << 16);
+#else
               pix = b.x + qx + (b.y + qy) * P.W;
+#endif
               sample = (int)g * P.group_spp;
               acc = f3(0, 0, 0);
               if (STATS) slot_t0 = wall_clock64();
@@ -1362,12 +1385,16 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
             // Blocks are <= 8x8 pixel rectangles of the tiles, clipped to the
             // scene's screen footprint (pixels outside are written 0 by
             // resolve_kernel: every ray through them misses the root box).
-            uint32_t bq = slot / n_groups;
+            uint32_t bq = pixel_of_slot(slot);
             uint32_t g = slot - bq * n_groups;
             int4 b = P.blocks[bq >> 6];
             int qx = (int)(bq & 7u), qy = (int)((bq >> 3) & 7u);
             if (qx < b.z && qy < b.w) {
+#if PT_INT_SHORTCUTS
+              pix = (b.x + qx) | ((b.y + qy) << 16);
+#else
               pix = b.x + qx + (b.y + qy) * P.W;
+#endif
               sample = (int)g * P.group_spp;
               acc = f3(0, 0, 0);
 #if PT_PIXEL_ACC
@@ -1397,9 +1424,14 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
       // ---- camera rays: Camera::generate_ray (camera.cpp:113-129) at the
       // jittered pixel position of raytrace_pixel (pathtracer.cpp:571-575)
       while (mode == M_CAMERA) {
+#if PT_INT_SHORTCUTS
+        const int px = pix & 0xffff, py = (int)((uint32_t)pix >> 16);
+        rbase = ptrng::stream_base(P.seed, (uint32_t)(px + py * P.W), (uint32_t)sample + P.sample_base);
+#else
         rbase = ptrng::stream_base(P.seed, (uint32_t)pix, (uint32_t)sample + P.sample_base);
-        rdim = ptrng::kDrawInit;
         const int py = pix / P.W, px = pix - py * P.W;
+#endif
+        rdim = ptrng::kDrawInit;
         float ry = PT_DRAW();  // UniformGridSampler2D draws y first
         float rx = PT_DRAW();
         float fx = ((float)px + rx) * P.inv_w;
@@ -1409,7 +1441,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         float3 d = normalize(f3(0, 0, 0) - wsp);
         trav_init(tr, wsp + ld3(P.cam_pos), d, 3.0e38f, false);
         if (STATS) n_cam++;
-        if (DBG && pix == P.dbg_pix) printf("pixel (%d,%d) sample %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g)\n", px, py, sample, tr.o.x, tr.o.y, tr.o.z, d.x, d.y, d.z);
+        if (DBG && pix_index(pix) == P.dbg_pix) printf("pixel (%d,%d) sample %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g)\n", px, py, sample, tr.o.x, tr.o.y, tr.o.z, d.x, d.y, d.z);
         if (box_hit(tr, P.root_lo, P.root_hi)) {
           T = f3(1, 1, 1);
           cur = 0;  // depth 0
@@ -1424,7 +1456,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
 #if PT_PIXEL_ACC
         sample_done();
 #endif
-        if (sample >= P.spp || sample % P.group_spp == 0) {
+        if (sample >= P.spp || group_starts(sample)) {
 #if !PT_PIXEL_ACC
           store3_stream(P.partial + 3 * slot_of(pix, sample), acc);
 #endif

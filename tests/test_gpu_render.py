@@ -448,6 +448,11 @@ def test_hip_error_paths():
         dev.set_params(8, 8, 1, 4, 256, 1)
     assert e.value.code == native.PT_E_INVALID
     dev.set_params(8, 8, 1, 254, 255, 1)
+    # pixel coordinates are packed in 16 bits each
+    with pytest.raises(native.PtError) as e:
+        dev.set_params(65536, 1, 1, 4, 1, 1)
+    assert e.value.code == native.PT_E_INVALID
+    dev.set_params(65535, 1, 1, 4, 1, 1)
 
 
 def test_hip_packed_tiles_match_frame():
