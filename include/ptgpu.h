@@ -150,11 +150,11 @@ typedef struct pt_scene {
 
 /* Integrator settings (PathTracer members) and frame size. */
 typedef struct pt_params {
-  int32_t width;
-  int32_t height;
+  int32_t width;         /* 1 .. 65535 (and width * height <= 2^30) */
+  int32_t height;        /* 1 .. 65535 */
   int32_t spp;           /* ns_aa */
-  int32_t max_depth;     /* max_ray_depth */
-  int32_t ns_area_light; /* ns_area_light */
+  int32_t max_depth;     /* max_ray_depth, 0 .. 254 */
+  int32_t ns_area_light; /* ns_area_light, 1 .. 255 */
   uint32_t seed;         /* counter-RNG key: (seed, pixel, sample) */
   uint32_t sample_base;  /* first sample index of this pass: samples sample_base .. sample_base+spp-1
                             are rendered and averaged (0 = the reference's single pass; progressive
