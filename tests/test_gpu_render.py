@@ -66,6 +66,23 @@ def test_hip_near_exact_vs_restatement_counter_rng(restate, scene, w, h, spp, m,
     assert np.isfinite(got).all()
 
 
+@pytest.mark.parametrize("group", ["1", "3", "4", "5", "12"])
+def test_hip_sample_groups_match_restatement(restate, monkeypatch, group):
+    """Work slots of `group` samples (PT_SAMPLE_GROUP) at 12 spp: power-of-two
+    and other group sizes and group counts (12, 4, 3, 3 ragged, 1 groups per
+    pixel) take both the shift and the division paths of the kernel's slot
+    arithmetic (PT_INT_SHORTCUTS).  A grouping only changes the float summation
+    order of a pixel, so every one is near-exact against the restatement."""
+    monkeypatch.setenv("PT_SAMPLE_GROUP", group)
+    spp = 12
+    got, _ = gpu_render("c1_default_64x64", 64, 64, spp, 4, 1, seed=11)
+    ref, _ = restate.render(golden("c1_default_64x64.scene.ptd"), 64, 64, spp, 4, 1, 11, rng_mode=1, threads=4)
+    frac, rel_mean = near_exact_report(got, ref)
+    print(f"group {group}: {frac*100:.3f}% pixels within 1e-3, image-mean rel diff {rel_mean:.2e}")
+    assert frac >= 0.995, frac
+    assert rel_mean <= 1e-3, rel_mean
+
+
 def test_hip_statistical_vs_reference_golden():
     """GPU (counter RNG) vs the reference binary (glibc rand), 128x128 @ 64 spp.
     Tolerance: mean per-pixel RGB-L2 distance <= 1.10 x the reference's own
