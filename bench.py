@@ -92,6 +92,18 @@ def algorithmic_bytes(st: dict) -> float:
             + 36.0 * st["ext_hits"] + 12.0 * st["pixels"])
 
 
+def lib_sha256(path=None) -> str:
+    """sha256 of the libptgpu.so this process loads (PT_LIB or the in-tree one)."""
+    import hashlib
+    from dsgpuraytracing_amd import native
+    path = path or (os.path.abspath(os.environ["PT_LIB"]) if os.environ.get("PT_LIB") else native.LIB_PATH)
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
 def profile_summary(workload: str):
     """PMC summary of the render kernel on this workload (tools/profile_summary.py
     -> profiles/<round>/<workload>_summary.json; the newest round wins)."""
@@ -108,58 +120,68 @@ def profile_summary(workload: str):
     return None
 
 
-def roofline(workload: str, kernel_ms: float, alg_bytes: float, frame_ms: float = 0.0) -> dict:
+def roofline(workload: str, frame_ms: float, alg_bytes: float, isolated_ms: float = 0.0,
+             pipelined_ms: float = 0.0, lib_sha: str | None = None) -> dict:
     """Roofline of the dominant kernel (render_kernel).  Per-launch counts come
-    from the committed PMC summary of the same workload (they are a property
-    of the workload, not of the clock); rates divide them by the kernel time
-    measured live in this run (HIP events on the launch stream).  Views:
+    from the committed PMC summary of the same workload and library (they are a
+    property of the workload and the build, not of the clock; `pmc_stale` is
+    true when the summary was collected on a different libptgpu.so than the one
+    this run loaded).  Views:
       hbm   -- (2 x FETCH_SIZE + WRITE_SIZE) bytes (gfx950 correction,
                MI355X_MICROARCH.md §HBM) vs 8 TB/s;
       l2    -- (TCC_HIT + TCC_MISS) requests x 128 B vs 34.5 TB/s (an upper
                bound of the bytes the L2 served);
       valu  -- SQ_INSTS_VALU wave-instructions vs 2 per CU per cycle;
       algorithmic -- the §8(d) cost-model bytes, cache-served, vs the L2 roof.
-    `bound` names the measured view with the highest fraction; the kernel is
-    latency-bound below all of them (SQ_WAIT_ANY, see pmc).  Consecutive
-    renders overlap (the render pipeline of pt_api.cpp), so a launch lasts
-    longer than the frame interval: each view also gives frac_per_frame, the
-    same counts over the measured ms_per_step."""
-    t = kernel_ms * 1e-3
+    Rates: `frac` (and `achieved`) divide the counts of one frame's launch by
+    the measured frame interval ms_per_step (`frame_ms`) -- consecutive frames
+    overlap on the GPU (pt_api.cpp's two-slot render pipeline), so the frame
+    interval, not an event span, is the time one launch's work occupies the
+    chip; `frac_isolated` divides them by the kernel's duration when it runs
+    alone (`isolated_ms`: HIP events around lone, synchronised frames; the
+    PT_PIPELINE=0 rocprofv3 kernel trace in profiles/ agrees with it).
+    `pipelined_launch_ms` is the HIP-event span of a launch in the timed
+    region: it includes waiting for the other render slot's CUs and is not a
+    kernel duration.  `bound` names the measured view with the highest
+    fraction; the kernel is latency-bound below all of them (SQ_WAIT_ANY)."""
+    t = frame_ms * 1e-3
+    ti = isolated_ms * 1e-3 if isolated_ms > 0 else None
     pm = profile_summary(workload)
-    views = {"algorithmic_cache_served": {
-        "bytes_per_launch": alg_bytes, "achieved": round(alg_bytes / t / 1e9, 1), "peak": L2_PEAK_GBS,
-        "unit": "GB/s", "frac": round(alg_bytes / t / 1e9 / L2_PEAK_GBS, 4)}}
+    views = {}
+
+    def view(name, per_launch, peak, unit, key="bytes_per_launch", **extra):
+        a = per_launch / t / 1e9
+        v = {key: per_launch, "achieved": round(a, 1), "peak": peak, "unit": unit, "frac": round(a / peak, 4)}
+        if ti:
+            v["frac_isolated"] = round(per_launch / ti / 1e9 / peak, 4)
+        v.update(extra)
+        views[name] = v
+
+    view("algorithmic_cache_served", alg_bytes, L2_PEAK_GBS, "GB/s")
     hbm_bytes = None
     if pm:
         if "hbm_bytes_per_launch" in pm:
             hbm_bytes = pm["hbm_bytes_per_launch"]
-            a = hbm_bytes / t / 1e9
-            views["hbm"] = {"bytes_per_launch": hbm_bytes, "achieved": round(a, 1), "peak": HBM_PEAK_GBS,
-                            "unit": "GB/s", "frac": round(a / HBM_PEAK_GBS, 4)}
+            view("hbm", hbm_bytes, HBM_PEAK_GBS, "GB/s")
         tcc = pm.get("tcc", {})
         if "TCC_HIT_sum" in tcc and "TCC_MISS_sum" in tcc:
-            b = (tcc["TCC_HIT_sum"] + tcc["TCC_MISS_sum"]) * L2_LINE
-            a = b / t / 1e9
-            views["l2"] = {"bytes_per_launch": b, "achieved": round(a, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(a / L2_PEAK_GBS, 4), "hit_rate": round(pm.get("l2_hit_rate", 0.0), 4)}
+            view("l2", (tcc["TCC_HIT_sum"] + tcc["TCC_MISS_sum"]) * L2_LINE, L2_PEAK_GBS, "GB/s",
+                 hit_rate=round(pm.get("l2_hit_rate", 0.0), 4))
         sq = pm.get("sq", {})
         if "SQ_INSTS_VALU" in sq:
-            a = sq["SQ_INSTS_VALU"] / t / 1e9
-            views["valu"] = {"insts_per_launch": sq["SQ_INSTS_VALU"], "achieved": round(a, 1),
-                             "peak": VALU_PEAK_GINST, "unit": "G wave-instructions/s",
-                             "frac": round(a / VALU_PEAK_GINST, 4)}
-    if frame_ms > 0:
-        for v in views.values():
-            v["frac_per_frame"] = round(v["frac"] * kernel_ms / frame_ms, 4)
+            view("valu", sq["SQ_INSTS_VALU"], VALU_PEAK_GINST, "G wave-instructions/s", key="insts_per_launch")
     measured = [k for k in ("hbm", "l2", "valu") if k in views]
     bound = max(measured, key=lambda k: views[k]["frac"]) if measured else "algorithmic_cache_served"
     v = views[bound]
     out = {"bound": bound, "achieved": v["achieved"], "peak": v["peak"], "unit": v["unit"], "frac": v["frac"],
-           "traffic": hbm_bytes, "kernel_ms": round(kernel_ms, 4), "views": views}
+           "frac_isolated": v.get("frac_isolated"), "traffic": hbm_bytes, "duration_ms": round(frame_ms, 4),
+           "isolated_kernel_ms": round(isolated_ms, 4) if isolated_ms else None,
+           "pipelined_launch_ms": round(pipelined_ms, 4) if pipelined_ms else None, "views": views}
     if pm:
         out["pmc"] = {k: (round(pm[k], 4) if isinstance(pm.get(k), float) else pm.get(k))
-                      for k in ("avg_ms", "sq_wait_any_frac", "sq_wait_inst_any_frac", "sq_active_inst_any_frac",
-                                "valu_issue_util", "l2_hit_rate", "source")}
+                      for k in ("avg_ms", "isolated_avg_ms", "sq_wait_any_frac", "sq_wait_inst_any_frac",
+                                "sq_active_inst_any_frac", "valu_issue_util", "l2_hit_rate", "source", "lib_sha256")}
+        out["pmc_stale"] = bool(lib_sha) and pm.get("lib_sha256") != lib_sha
     return out
 
 
@@ -278,7 +300,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from dsgpuraytracing_amd.dist import TileExchange, init_from_env, shard_tiles
+    from dsgpuraytracing_amd.dist import RankFailure, StepGuard, TileExchange, check_value_knobs, init_from_env, shard_tiles
     # PT_DIST_BACKEND=gloo + PT_BENCH_DEVICE=0: rehearsal of the N-rank flow
     # with every rank on one GPU (the exchange then stages through host memory)
     backend = os.environ.get("PT_DIST_BACKEND", "nccl")
@@ -292,6 +314,23 @@ def main():
     # finished frame.
     torch.cuda.set_stream(torch.cuda.Stream(device=local))
     rank, world, _ = init_from_env(backend)
+    try:
+        bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExchange, check_value_knobs, shard_tiles)
+    except RankFailure as e:
+        # every rank raises it (dist.agree_status): report, leave the group, exit non-zero
+        print(f"[bench rank {rank}] aborted: {e}", file=sys.stderr, flush=True)
+        if rank == 0:
+            print(json.dumps({"metric": HEADLINE_METRIC, "value": None, "error": str(e), "n_gpus": world}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(3)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExchange, check_value_knobs, shard_tiles):
+    import torch
+    import torch.distributed as dist
 
     global W, H, SPP
     workload = args.workload or ("c3" if world == 1 else "c4")
@@ -344,10 +383,14 @@ def main():
             frame.mul_(1.0 / world)
 
     xev = []  # (start, end) events around each timed step's exchange
+    # A rank whose render fails keeps joining the exchanges; guard.check() (a
+    # collective at the synchronisation points) then stops every rank with the
+    # failing rank's error (dsgpuraytracing_amd.dist.RankFailure).
+    guard = StepGuard()
 
     def step(stats=False, timed=False):
         if ex is None:  # the whole tile FIFO straight into the frame (one GPU, or this rank's pass)
-            dev.render_tiles_device(mine_arr, frame.data_ptr(), stream, stats=stats)
+            guard.run(dev.render_tiles_device, mine_arr, frame.data_ptr(), stream, stats=stats)
             if weak:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -357,7 +400,7 @@ def main():
                 if timed:
                     xev.append((e0, e1))
         else:  # this rank's tiles into its packed buffer, then one gather onto rank 0
-            dev.render_tiles_device(mine_arr, ex.packed.data_ptr(), stream, stats=stats, packed=True)
+            guard.run(dev.render_tiles_device, mine_arr, ex.packed.data_ptr(), stream, stats=stats, packed=True)
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
             ex.exchange(frame)
@@ -365,14 +408,18 @@ def main():
             e1.record()
             if timed:
                 xev.append((e0, e1))
-        return dev.stats() if stats else None
+        return guard.run(dev.stats) if stats else None
 
     # counters for the roofline's algorithmic bytes: the reference's binary BVH
     # (SURVEY.md §8(d) cost model); and the launch's own counters (4-wide BVH)
     st_counts = step(stats="ref")
     st_perf = step(stats=True)
+    guard.check()
+    # the ranks must group each pixel's samples alike (bit-identical frame)
+    knobs = check_value_knobs({"group_spp": st_perf["group_spp"]})
     for _ in range(args.warmup):
         step()
+    guard.check()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -383,6 +430,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    guard.check()
     # HIP events recorded around every launch on its stream (the timed ones)
     kernel_ms, resolve_ms = dev.launch_times(args.steps)
     xchg_ms = float(np.mean([a.elapsed_time(b) for a, b in xev])) if xev else 0.0
@@ -400,17 +448,21 @@ def main():
 
     host_ms = None
     single_ms = None
+    iso_ms = 0.0
     if world == 1:
         # one frame alone, synchronised on both sides (no overlap with a
-        # neighbouring frame): the wall-clock render time of ONE frame
+        # neighbouring frame): the wall-clock render time of ONE frame, and
+        # the render kernel's own duration (HIP events around a launch that
+        # shares the GPU with nothing)
         lat = []
-        for _ in range(3):
+        for _ in range(5):
             torch.cuda.synchronize()
             t0s = time.perf_counter()
             step()
             torch.cuda.synchronize()
             lat.append(time.perf_counter() - t0s)
         single_ms = float(np.median(lat)) * 1e3
+        iso_ms = float(np.median(dev.launch_times(5)[0]))
         # the drop-in pt_render_tiles path: output copied to a host buffer (PCIe-inclusive)
         host = np.zeros((H, W, 3), np.float32)
         dev.render_tiles(mine_arr, host)
@@ -452,7 +504,8 @@ def main():
                        "bvh": "gpu-lbvh" if args.lbvh else ("reference-sah (host)" if os.environ.get("PT_BVH_BUILD") == "ref" else "own binned SAH, 128 bins, C_isect 1 (host)"),
                        "upload_s": round(t_up, 4),
                        "host_output_ms_per_frame": None if host_ms is None else round(host_ms, 3)},
-            "roofline": roofline(workload, avg_ms, algorithmic_bytes(st_counts), elapsed / frames * 1e3),
+            "roofline": roofline(workload, elapsed / frames * 1e3, algorithmic_bytes(st_counts), isolated_ms=iso_ms,
+                                 pipelined_ms=avg_ms, lib_sha=lib_sha256()),
             "resolve_ms": round(float(np.mean(resolve_ms)), 4),
             "counters": {k: st_counts[k] for k in ("camera_rays", "bounce_rays", "shadow_rays", "node_visits",
                                                    "tri_tests", "sphere_tests", "ext_hits", "culled_samples")},
@@ -460,7 +513,7 @@ def main():
                                                         "leaf_steps", "wave_rounds", "queue_atomics", "shade_clocks",
                                                         "hitshade_clocks", "trav_clocks", "max_wave_clocks",
                                                         "wave_wall_sum", "wave_wall_max", "section_clocks", "wave_span",
-                                                        "lane_iters", "uniform_node_steps")},
+                                                        "lane_iters", "partial_bytes")},
             "launch": {"grid_blocks": s_get(dev, "grid_blocks"), "block": 64,
                        "blocks_per_cu_query": s_get(dev, "blocks_per_cu"),
                        "bvh_nodes": s_get(dev, "bvh_nodes"), "bvh_stack": s_get(dev, "bvh_stack"),
@@ -475,6 +528,10 @@ def main():
             out["exchange_ms"] = round(xchg_ms, 4)
         if world == 1 and not args.no_extras and workload == "c3" and not args.scene_dump:
             out["companions"] = companions(dev, local, stream, max(2, min(args.steps, 5)))
+        out["dist"] = {"backend": backend if world > 1 else None,
+                       "world_size": dist.get_world_size() if dist.is_initialized() else 1,
+                       "timeout_s": float(os.environ.get("PT_DIST_TIMEOUT", "120")) if world > 1 else None,
+                       "value_knobs": knobs}
         if world == 1 and not args.no_cpu_baseline:
             try:
                 dp = dump_path
@@ -491,8 +548,6 @@ def main():
             except Exception as e:  # reported, never silently replaced
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 def s_get(dev, key):

@@ -176,8 +176,7 @@ struct pt_ctx {
   std::vector<int4> tiles_host[kSlots];  // what `tiles` holds
   DevBuf<int4> blocks[kSlots];           // footprint-clipped 8x8 pixel blocks of the tiles
   std::vector<int4> blocks_host[kSlots];
-  DevBuf<float> partial[kSlots];   // per-slot sample-group sums (PT_PIXEL_ACC 0)
-  DevBuf<float> fb[kSlots];        // per-slot pixel means written by the render (PT_PIXEL_ACC 1)
+  DevBuf<float> partial[kSlots];   // per-slot sample-group sums
   DevBuf<int> spill[kSlots];       // traversal stack entries beyond PT_STACK
   DevBuf<uint32_t> counter[kSlots];
   int64_t culled_px = 0;         // pixels of the last launch outside the footprint
@@ -198,6 +197,7 @@ struct pt_ctx {
   pt_stats last{};
   int grid_plain = 0, grid_stats = 0;
   int bpc_plain = 0, bpc_stats = 0, n_cu = 0;
+  int bpc_variant[4] = {0, 0, 0, 0};  // plain builds: [env * 2 + gtab] (the common one is bpc_plain)
 };
 
 extern "C" {
@@ -228,8 +228,9 @@ int pt_create(int device, pt_ctx** out) {
   // work queue needs no co-residency (no grid barrier), so a wrong occupancy
   // answer only costs speed; never size below 8 waves per CU.
   c->n_cu = prop.multiProcessorCount;
-  HIPCHK(ptk_render_occupancy(&c->bpc_plain, false));
-  HIPCHK(ptk_render_occupancy(&c->bpc_stats, true));
+  HIPCHK(ptk_render_occupancy(&c->bpc_plain, false, false, false));
+  HIPCHK(ptk_render_occupancy(&c->bpc_stats, true, false, false));
+  for (int v = 0; v < 4; ++v) HIPCHK(ptk_render_occupancy(&c->bpc_variant[v], false, (v & 2) != 0, (v & 1) != 0));
   c->grid_plain = std::max(8, c->bpc_plain) * c->n_cu;
   c->grid_stats = std::max(8, c->bpc_stats) * c->n_cu;
   // counters + one trace record per wave of the largest stats grid
@@ -260,7 +261,6 @@ int pt_destroy(pt_ctx* c) {
     c->blocks[k].release();
     c->spill[k].release();
     c->partial[k].release();
-    c->fb[k].release();
     c->counter[k].release();
     if (c->ev_free[k]) (void)hipEventDestroy(c->ev_free[k]);
     if (c->rstream[k]) (void)hipStreamDestroy(c->rstream[k]);
@@ -362,7 +362,10 @@ static int build_host_bvh(const pt_scene* s, std::vector<DNode>& dn, std::vector
     set_box(d, 0, root);
     for (int k = 0; k < 3; ++k) d.lo[1][k] = d.hi[1][k] = INFINITY;
     d.ref[0] = cursor(root.first, root.count);
-    d.ref[1] = 0;
+    // the empty child is a leaf cursor (never entered: its box is at +inf),
+    // never a node reference -- node 0 as its own child would be opened and
+    // pushed forever by the collapse below
+    d.ref[1] = cursor(0, 1);
     b2.push_back(d);
   } else {
     // explicit DFS: (subtree, parent node, side)
@@ -493,42 +496,6 @@ static int build_host_bvh(const pt_scene* s, std::vector<DNode>& dn, std::vector
     }
     std::fprintf(stderr, "[pt] BVH4: %zu nodes, stack %d, SAH node steps %.3f leaf steps %.3f (per root-box ray)\n",
                  dn.size(), max_stack, (nodes + root) / root, leaves / root);
-  }
-  // Breadth-first order (PT_BVH_ORDER=bfs; the default when the kernel
-  // stages a treelet): the top levels become the first nodes, which the
-  // render kernel copies into LDS (PT_TREELET).  Parents still precede their
-  // children, so every reference stays forward.
-  {
-    const char* ord = std::getenv("PT_BVH_ORDER");
-    const bool bfs = ord ? std::strcmp(ord, "bfs") == 0 : PT_TREELET > 0;
-    if (bfs && dn.size() > 1) {
-      std::vector<int> order, newid(dn.size(), -1);
-      order.reserve(dn.size());
-      order.push_back(0);
-      for (size_t q = 0; q < order.size(); ++q) {
-        const DNode& d = dn[(size_t)order[q]];
-        for (int k = 0; k < 4; ++k) {
-          const int r = (&d.ref.x)[k];
-          if (!std::isinf((&d.lox.x)[k]) && r > 0 && r < (int)dn.size() && newid[(size_t)r] < 0) {
-            newid[(size_t)r] = -2;  // queued
-            order.push_back(r);
-          }
-        }
-      }
-      if (order.size() == dn.size()) {
-        for (size_t q = 0; q < order.size(); ++q) newid[(size_t)order[q]] = (int)q;
-        std::vector<DNode> bn(dn.size());
-        for (size_t q = 0; q < order.size(); ++q) {
-          DNode d = dn[(size_t)order[q]];
-          for (int k = 0; k < 4; ++k) {
-            int& r = (&d.ref.x)[k];
-            if (!std::isinf((&d.lox.x)[k]) && r >= 0) r = newid[(size_t)r];
-          }
-          bn[q] = d;
-        }
-        dn.swap(bn);
-      }
-    }
   }
   // Traversal termination rests on this: node references only point forward
   // (pre-order), so a ray can never re-enter a node it has left.
@@ -932,13 +899,13 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.spp = c->params.spp;
   P.max_depth = c->params.max_depth;
   P.ns_area = c->params.ns_area_light;
+  P.nls_scale = (float)(1.0 / (double)P.ns_area);
   P.seed = c->params.seed;
   P.sample_base = c->params.sample_base;
   P.n_lights = c->n_lights;
   P.n_bsdfs = c->n_bsdfs;
   P.n_tiles = (int)tl.size();
   P.nodes = c->nodes.p;
-  P.n_treelet = (int)std::min<size_t>(c->n_nodes4, (size_t)PT_TREELET);
   P.nodes2 = c->nodes2.p;
   P.prims = c->prims.p;
   P.norms = c->norms.p;
@@ -1012,7 +979,11 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   // Work slots are (pixel, group of group_spp samples): small enough that
   // the dynamic queue balances the waves (a whole pixel per slot left the
   // launch waiting on a few waves holding 64-sample pixels).
-  int64_t want = stats ? c->grid_stats : c->grid_plain;
+  // the launch fills the GPU with the resident waves of the kernel variant it
+  // runs (environment light / global tables; the STATS build for counters)
+  const bool gtab = c->n_bsdfs > PT_LDS_BSDFS || c->n_lights > PT_LDS_LIGHTS || std::getenv("PT_FORCE_GLOBAL_TABLES");
+  int64_t want = stats ? c->grid_stats
+                       : (int64_t)std::max(8, c->bpc_variant[(c->env_w > 0 ? 2 : 0) + (gtab ? 1 : 0)]) * c->n_cu;
   if (const char* g = std::getenv("PT_WAVES_PER_CU")) {  // tuning knob
     int w = std::atoi(g);
     if (w > 0) want = (int64_t)w * c->n_cu;
@@ -1034,37 +1005,25 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   }
   P.group_spp = std::min(P.group_spp, P.spp);
   const int64_t npx = (int64_t)P.W * P.H;
-#if PT_PIXEL_ACC
-  // On-chip pixel sums: a pixel is either one work slot (its lane renders
-  // every sample) or >= 16 slots (a wave's chunk then holds at most 8 pixels
-  // of its PT_RING-pixel accumulator ring).  The grouping no longer decides
-  // any pixel's value: the ring sums in exact fixed point.
-  P.n_groups = (P.spp + P.group_spp - 1) / P.group_spp;
-  if (P.n_groups > 1 && P.n_groups < 16) {
-    P.group_spp = P.spp;
-    P.n_groups = 1;
-  }
-  const int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
-  if (slots + want * std::max<int64_t>(PT_CHUNK_MAX, P.n_groups) >= (int64_t)UINT32_MAX)
-    return fail(PT_E_INVALID, "frame too large for one launch");
-  HIPCHK(c->fb[slot].reserve((size_t)npx * 3));
-  P.fb = c->fb[slot].p;
-#else
   // 32-bit slot and partial indices (the queue head may overshoot by one
-  // chunk per wave); the per-pixel group sums stay within 4 GiB
+  // chunk per wave); the per-pixel group sums of one render slot stay within
+  // 4 GiB.  The fallback that doubles the group also looks at the FRAME only
+  // (its 8x8 blocks as the whole-frame tile FIFO cuts them), so a tile split
+  // groups each pixel's samples exactly as the whole frame does.
+  const int64_t frame_blocks = (int64_t)((P.W + 7) / 8) * ((P.H + 7) / 8);
   for (;;) {
     P.n_groups = (P.spp + P.group_spp - 1) / P.group_spp;
-    int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
-    bool fits = slots + want * PT_CHUNK_MAX < (int64_t)UINT32_MAX && npx * P.n_groups * 12 <= (4ll << 30);
+    const bool fits = frame_blocks * 64 * P.n_groups + want_plain * PT_CHUNK_MAX < (int64_t)UINT32_MAX &&
+                      npx * P.n_groups * 12 <= (4ll << 30);
     if (fits || P.n_groups == 1) break;
     P.group_spp *= 2;
   }
-  int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
+  const int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
   if (slots + want * PT_CHUNK_MAX >= (int64_t)UINT32_MAX || npx * P.n_groups >= (int64_t)UINT32_MAX)
     return fail(PT_E_INVALID, "frame too large for one launch");
   HIPCHK(c->partial[slot].reserve((size_t)(npx * P.n_groups) * 3));
   P.partial = c->partial[slot].p;
-#endif
+  c->last.partial_bytes = (int64_t)npx * P.n_groups * 12;
   auto log2_exact = [](int v) {  // log2(v) for a power of two, else -1
     int k = 0;
     while ((1 << k) < v && k < 30) ++k;
@@ -1075,7 +1034,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   int64_t max_grid = std::max<int64_t>(1, (slots + PT_BLOCK - 1) / PT_BLOCK);
   int grid = (int)std::min<int64_t>(want, max_grid);
   if (stats && (size_t)grid * PT_WAVE_TRACE + PT_STATS_SLOTS > c->stats.n) grid = (int)((c->stats.n - PT_STATS_SLOTS) / PT_WAVE_TRACE);
-  grid = std::max(PT_WG_WAVES, grid - grid % PT_WG_WAVES);  // whole workgroups of PT_WG_WAVES waves
+  grid = std::max(1, grid);
   P.stack_spill = nullptr;
   if (c->bvh_stack > PT_STACK) {  // worst-case depth beyond the LDS stack
     HIPCHK(c->spill[slot].reserve((size_t)(c->bvh_stack - PT_STACK) * grid * PT_BLOCK));
@@ -1097,7 +1056,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   HIPCHK(hipEventRecord(c->ev_free[slot], s));
   c->last.grid_blocks = grid;
   c->last.group_spp = P.group_spp;
-  c->last.blocks_per_cu = stats ? c->bpc_stats : c->bpc_plain;
+  c->last.blocks_per_cu = (int32_t)(want / std::max(1, c->n_cu));
   int64_t px = 0;
   for (const int4& t : tl) px += (int64_t)t.z * t.w;
   c->last.pixels = px;
@@ -1153,7 +1112,6 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags, bool sync) {
     c->last.hitshade_clocks = (int64_t)v[16];
     for (int k = 0; k < 4; ++k) c->last.section_clocks[k] = (int64_t)v[17 + k];
     for (int k = 0; k < 4; ++k) c->last.lane_iters[k] = (int64_t)v[27 + k];
-    c->last.uniform_node_steps = (int64_t)v[31];
     for (int k = 0; k < 3; ++k) c->last.wave_span[k] = (int64_t)(v[22 + k] - v[21]);
     for (int k = 0; k < 2; ++k) c->last.wave_span[3 + k] = v[25 + k] ? (int64_t)(v[25 + k] - v[21]) : -1;
     c->last.counters_valid = 1;

@@ -7,32 +7,6 @@
 #ifndef PT_BLOCK
 #define PT_BLOCK 64  // one wave64 per workgroup: the persistent queue is per wave
 #endif
-#ifndef PT_WG_WAVES
-#define PT_WG_WAVES 1  // waves per render workgroup (> 1: the workgroup shares an LDS treelet)
-#endif
-#ifndef PT_TREELET
-#define PT_TREELET 0  // BVH4 nodes (the first ones, breadth-first: the top levels) staged in LDS
-#endif
-#ifndef PT_ROOT_LDS
-#define PT_ROOT_LDS 1  // fresh rays take their root step from an LDS copy of the root node (C3 +2%)
-#endif
-#ifndef PT_EARLY_BOUNCE
-#define PT_EARLY_BOUNCE 0  // 1: the bounce is sampled with the last light sample and its ray starts where the shadow ray ends (C3 -9%: shading code growth, SGPR spills)
-#endif
-#ifndef PT_SCALAR_NODE
-#define PT_SCALAR_NODE 0  // 1: node steps whose lanes all stand at one node read it through the scalar cache (C3: 3% of node steps; measured -0.5%)
-#endif
-#ifndef PT_LEAF_MASK
-#define PT_LEAF_MASK 0  // 1: one-primitive leaf steps skip the second primitive's loads (measured -2%: the branch costs more)
-#endif
-#ifndef PT_PIXEL_ACC
-#define PT_PIXEL_ACC 0  // 1: pixel sums accumulated on chip (per-wave LDS ring, fixed point); 0: group sums in HBM
-#endif
-#ifndef PT_RING
-#define PT_RING 32  // pixels per wave's accumulator ring (power of two)
-#endif
-#define PT_RING_FREE 0xffffffffu
-static_assert((PT_RING & (PT_RING - 1)) == 0 && PT_RING >= 16 && PT_RING <= 64, "PT_RING: power of two in [16, 64]");
 #ifndef PT_CHUNK
 #define PT_CHUNK 128  // smallest claim of work slots a wave takes from the queue per atomic
 #endif
@@ -43,12 +17,7 @@ static_assert((PT_RING & (PT_RING - 1)) == 0 && PT_RING >= 16 && PT_RING <= 64, 
 #define PT_CHUNK_DIV 8u  // a claim is ~1/(PT_CHUNK_DIV * waves) of the slots still unclaimed
 #endif
 static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand");
-#ifndef PT_XCD_QUEUES
-#define PT_XCD_QUEUES 1  // work queues (8: one per XCD, banded; measured slower on C3)
-#endif
-#define PT_QUEUE_WORDS (32 * 8)  // queue heads 128 B apart (room for 8)
-static_assert(PT_XCD_QUEUES >= 1 && PT_XCD_QUEUES <= 8, "at most 8 queues");
-static_assert(!(PT_PIXEL_ACC && PT_XCD_QUEUES > 1), "the pixel ring needs the single work queue");
+#define PT_QUEUE_WORDS 32  // the work-queue head, alone in its 128-B line
 #ifndef PT_GROUP_SPP
 #define PT_GROUP_SPP 4  // default samples per work slot (C3 +3.3% over 2; 8 or more: C3 -4%, C5 -10%)
 #endif
@@ -71,15 +40,6 @@ static_assert(!(PT_PIXEL_ACC && PT_XCD_QUEUES > 1), "the pixel ring needs the si
 #define PT_WAVE_TRACE 9
 #ifndef PT_STACK
 #define PT_STACK 24  // traversal stack entries per lane in LDS (lane-contiguous)
-#endif
-#ifndef PT_INT_SHORTCUTS
-#define PT_INT_SHORTCUTS 1  // group / slot arithmetic by shifts for power-of-two sizes, pixel coordinates packed (W, H <= 65535)
-#endif
-#ifndef PT_NLS_RCP
-#define PT_NLS_RCP 1  // 1 (default; C3 +0.5% same-session): the 1/ns_area_light sample weight through v_rcp_f32 instead of an IEEE division
-#endif
-#ifndef PT_REG_TOP
-#define PT_REG_TOP 0  // 1: the top traversal-stack entry lives in a register (pop reads it, the LDS refill is off the critical path)
 #endif
 #ifndef PT_STACK_MAX
 #define PT_STACK_MAX 128  // deepest worst-case stack accepted (entries past PT_STACK spill to global memory)
@@ -112,16 +72,6 @@ struct alignas(16) DPrim {
   float4 v0, e1, e2;
 };
 
-// One pixel's accumulator in a wave's LDS ring (PT_PIXEL_ACC): the sums of
-// its samples in unsigned 32.32 fixed point (exact, so any order and any
-// grouping of the samples gives the same bits), the samples counted so far,
-// and whether the slot is taken.
-struct alignas(16) PxAcc {
-  unsigned long long s[3];
-  uint32_t count;
-  uint32_t owner;
-};
-
 struct alignas(16) DBsdf {
   int type;
   float a[3];  // albedo / reflectance
@@ -147,6 +97,7 @@ struct KParams {
   float c2w_col0[3], c2w_col1[3], c2w_col2[3];
   float cam_ax, cam_ay;  // screenW/screenDist, screenH/screenDist
   int W, H, spp, max_depth, ns_area;
+  float nls_scale;     // (float)(1.0 / ns_area): an area light sample's weight (pathtracer.cpp:481)
   float inv_w, inv_h;  // 1/W, 1/H
   uint32_t seed;
   uint32_t sample_base;  // first sample index of the pass (RNG keys)
@@ -173,13 +124,11 @@ struct KParams {
   const int4* tiles;  // (x, y, w, h)
   float* out;         // W*H*3, or n_tiles*1024*3 when packed
   int packed;         // PT_FLAG_PACKED: tile i's pixel (x, y) -> out[3 * (i*1024 + (y-ty)*32 + (x-tx))]
-  float* partial;     // PT_PIXEL_ACC 0: W*H*n_groups*3, each sample group's sum, resolved into `out` in group order
-  float* fb;          // PT_PIXEL_ACC 1: W*H*3, each traced pixel's mean, written by the lane completing it
+  float* partial;     // W*H*n_groups*3: each sample group's sum, resolved into `out` in group order
   const int4* blocks;  // (x, y, w<=8, h<=8): footprint-clipped pixel blocks of the tiles
   int n_blocks;
   uint32_t* work_counter;
   unsigned long long* stats;  // counters (PT_FLAG_STATS / PT_FLAG_REF_COUNTS)
-  int n_treelet;               // BVH4 nodes [0, n_treelet) read from the workgroup's LDS copy
   int* stack_spill;           // traversal stack entries beyond PT_STACK (null if the BVH never needs them)
   int dbg_pix;                // diagnostic printf trace of one pixel (-1: off)
   int shade_batch;            // leave the traversal phase once this many lanes finished their ray
@@ -215,4 +164,4 @@ extern "C" hipError_t ptk_launch_resolve(const KParams* P, hipStream_t s);
 extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prims, const float* o, const float* d,
                                            const float* maxt, int64_t n, int32_t* hit, float* t, int32_t* prim,
                                            int32_t* anyhit, int* spill, const int* prim_map, hipStream_t s);
-extern "C" hipError_t ptk_render_occupancy(int* blocks_per_cu, bool stats);
+extern "C" hipError_t ptk_render_occupancy(int* waves_per_cu, bool stats, bool env, bool gtab);

@@ -70,27 +70,6 @@ __device__ __forceinline__ void store3(float* p, float3 v) {
   p[1] = v.y;
   p[2] = v.z;
 }
-// Group sums stream through memory once (written by the render, read once by
-// the resolve): non-temporal stores / loads keep them from evicting the scene
-// (nodes, primitives, normals) from the per-XCD L2s (PT_NT_PARTIAL).
-#ifndef PT_NT_PARTIAL
-#define PT_NT_PARTIAL 0  // 1: non-temporal group-sum stores / resolve loads (C3 -0.4%, L2 hit 84 -> 79%: left off)
-#endif
-__device__ __forceinline__ void store3_stream(float* p, float3 v) {
-  if (PT_NT_PARTIAL) {
-    __builtin_nontemporal_store(v.x, p);
-    __builtin_nontemporal_store(v.y, p + 1);
-    __builtin_nontemporal_store(v.z, p + 2);
-  } else {
-    store3(p, v);
-  }
-}
-__device__ __forceinline__ float3 ld3_stream(const float* p) {
-  if (PT_NT_PARTIAL)
-    return f3(__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1), __builtin_nontemporal_load(p + 2));
-  return f3(p[0], p[1], p[2]);
-}
-
 // Pixel q (0..1023) of a tile in 8x8 blocks (4 blocks per row); (-1,-1) when
 // it lies outside a ragged tile.
 __device__ __forceinline__ int2 tile_pixel(int4 tile, uint32_t q) {
@@ -142,15 +121,8 @@ __device__ __forceinline__ Frame make_frame(float3 n) {
 
 // Materialises loaded values in VGPRs at this point (an empty asm that
 // "modifies" them): the loads must be issued before it and cannot be sunk
-// into later branches.
-// PT_LOAD_FENCE bit 0: node steps, bit 1: leaf steps.
-#ifndef PT_LOAD_FENCE
-#define PT_LOAD_FENCE 3
-#endif
+// into later branches (node steps, leaf steps and the hit record).
 #define PT_FENCE4(v) asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w))
-#ifndef PT_HIT_FENCE
-#define PT_HIT_FENCE 1
-#endif
 
 struct RayState {
   float3 o, d;
@@ -175,9 +147,6 @@ struct Trav {
   float tmax;
   int node, sp;
   int prim;
-#if PT_REG_TOP
-  int top;  // the stack's top entry (logical entry sp - 1); entries 0 .. sp - 2 are in the stack memory
-#endif
   bool any, found;
 };
 
@@ -191,9 +160,6 @@ __device__ __forceinline__ void trav_init(Trav& tr, float3 o, float3 d, float tm
   tr.tmax = tmax;
   tr.node = 0;
   tr.sp = 0;
-#if PT_REG_TOP
-  tr.top = 0;
-#endif
   tr.any = any;
   tr.found = false;
   tr.prim = -1;
@@ -298,14 +264,7 @@ struct Stack {
 __device__ __forceinline__ bool trav_pop(const Stack& stk, Trav& tr) {
   if (tr.sp == 0) return true;
   --tr.sp;
-#if PT_REG_TOP
-  // continue with the register top; refill it from the entry below, whose
-  // value is needed only at the next push or pop (off this step's critical path)
-  tr.node = tr.top;
-  tr.top = stk.get(tr.sp > 0 ? tr.sp - 1 : 0);
-#else
   tr.node = stk.get(tr.sp);
-#endif
   return false;
 }
 
@@ -337,29 +296,6 @@ __device__ __forceinline__ bool node_order(const Stack& stk, Trav& tr, const flo
   // hits are a sorted prefix, so with room for three entries every candidate
   // is written and the top only advances past hits (no branches).
   int sp = tr.sp;
-#if PT_REG_TOP
-  // the old register top goes to memory (redundant when nothing is pushed),
-  // the farther hits below the new top, the second-nearest hit into the register
-  if (sp + 2 <= PT_STACK) {
-    stk.lds[(sp > 0 ? sp - 1 : 0) * PT_BLOCK] = tr.top;
-    stk.lds[sp * PT_BLOCK] = r3;
-    sp += d3 != kMiss;
-    stk.lds[sp * PT_BLOCK] = r2;
-    sp += d2 != kMiss;
-    const bool h1 = d1 != kMiss;
-    sp += h1;
-    tr.top = h1 ? r1 : tr.top;
-  } else if (d1 != kMiss) {
-    if (sp > 0) stk.put(sp - 1, tr.top);
-    if (d3 != kMiss) stk.put(sp++, r3);
-    if (d2 != kMiss) stk.put(sp++, r2);
-    ++sp;
-    tr.top = r1;
-  }
-  tr.sp = sp;
-  tr.node = r0;
-  return false;
-#endif
   if (sp + 3 <= PT_STACK) {
     stk.lds[sp * PT_BLOCK] = r3;
     sp += d3 != kMiss;
@@ -377,18 +313,6 @@ __device__ __forceinline__ bool node_order(const Stack& stk, Trav& tr, const flo
   return false;
 }
 
-#ifndef PT_OCTANT
-#define PT_OCTANT 1
-#endif
-// the ENV (environment light) build: octant-selected node loads / node load
-// fence (round 1: they made it spill; on the round-2 code both together C5 +2.5%)
-#ifndef PT_ENV_OCT
-#define PT_ENV_OCT 1
-#endif
-#ifndef PT_ENV_FENCE
-#define PT_ENV_FENCE 1
-#endif
-
 typedef __attribute__((address_space(3))) const char lds_cchar;
 typedef float pt_v4f __attribute__((ext_vector_type(4)));
 typedef int pt_v4i __attribute__((ext_vector_type(4)));
@@ -402,127 +326,54 @@ __device__ __forceinline__ int4 lds_i4(lds_cchar* p) {
   return make_int4(v.x, v.y, v.z, v.w);
 }
 
-template <bool STATS, bool FENCE = (PT_LOAD_FENCE & 1) != 0, bool OCT = PT_OCTANT != 0, bool TREE = false>
+// Node step.  Near/far planes are chosen by the ray's direction signs through
+// the load addresses: for inv.x >= 0 the near x plane is lo (offset 0), else
+// hi (offset 16).  The slab test then needs no per-child min/max pairs:
+// tn = max(near planes, 0), tf = min(far planes, tmax).  ROOT: the node is the
+// workgroup's LDS copy of the root (`root`, ds_read_b128); otherwise the seven
+// 16-B global loads are all issued before the first wait (register fence).
+template <bool STATS, bool ROOT = false>
 __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, const Stack& stk, Trav& tr,
-                                          Counters& ct, lds_cchar* tree = nullptr, int n_tree = 0) {
+                                          Counters& ct, lds_cchar* root = nullptr) {
   const float kRobust = PT_ROBUST;
   const float3 o = tr.o, inv = tr.inv;
   const float kMiss = 3.0e38f;
   float d[4];
-  if constexpr (OCT) {
-  // Near/far planes chosen by the ray's direction signs through the load
-  // addresses: for inv.x >= 0 the near x plane is lo (offset 0), else hi
-  // (offset 16).  The slab test then needs no per-child min/max pairs:
-  // tn = max(near planes, 0), tf = min(far planes, tmax).
-  {
+  const uint32_t sx = (__float_as_uint(inv.x) >> 27) & 16u, sy = (__float_as_uint(inv.y) >> 27) & 16u,
+                 sz = (__float_as_uint(inv.z) >> 27) & 16u;
+  float4 nx, fx, ny, fy, nz, fz;
+  int4 rf;
+  if constexpr (ROOT) {
+    nx = lds_f4(root + sx);
+    fx = lds_f4(root + (sx ^ 16u));
+    ny = lds_f4(root + (32u + sy));
+    fy = lds_f4(root + (32u + (sy ^ 16u)));
+    nz = lds_f4(root + (64u + sz));
+    fz = lds_f4(root + (64u + (sz ^ 16u)));
+    rf = lds_i4(root + 96u);
+  } else {
     const char* nb = (const char*)nodes;
     const uint32_t base = (uint32_t)tr.node << 7;
-    const uint32_t sx = (__float_as_uint(inv.x) >> 27) & 16u, sy = (__float_as_uint(inv.y) >> 27) & 16u,
-                   sz = (__float_as_uint(inv.z) >> 27) & 16u;
-    float4 nx, fx, ny, fy, nz, fz;
-    int4 rf;
-    if (TREE && tr.node < n_tree) {  // top levels: the workgroup's LDS copy (ds_read_b128)
-      nx = lds_f4(tree + (base + sx));
-      fx = lds_f4(tree + (base + (sx ^ 16u)));
-      ny = lds_f4(tree + (base + 32u + sy));
-      fy = lds_f4(tree + (base + 32u + (sy ^ 16u)));
-      nz = lds_f4(tree + (base + 64u + sz));
-      fz = lds_f4(tree + (base + 64u + (sz ^ 16u)));
-      rf = lds_i4(tree + (base + 96u));
-    } else {
-      nx = *(const float4*)(nb + (base + sx));
-      fx = *(const float4*)(nb + (base + (sx ^ 16u)));
-      ny = *(const float4*)(nb + (base + 32u + sy));
-      fy = *(const float4*)(nb + (base + 32u + (sy ^ 16u)));
-      nz = *(const float4*)(nb + (base + 64u + sz));
-      fz = *(const float4*)(nb + (base + 64u + (sz ^ 16u)));
-      rf = *(const int4*)(nb + (base + 96u));
-#if PT_DIAG_EXTRA_LOAD
-      // diagnostic only: one more 16-B load per node step (the node's pad),
-      // to measure how the kernel's time responds to vector-memory traffic
-      int4 px = *(const int4*)(nb + (base + 112u));
-      asm volatile("" ::"v"(px.x), "v"(px.y), "v"(px.z), "v"(px.w));
-#endif
-      if (FENCE) {
-        PT_FENCE4(fz);
-        PT_FENCE4(rf);
-      }
-    }
-    if (STATS) ct.nodes++;
-    const float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
-    const float* NX = &nx.x; const float* FX = &fx.x; const float* NY = &ny.x;
-    const float* FY = &fy.x; const float* NZ = &nz.x; const float* FZ = &fz.x;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float tn = fmaxf(fmaxf(fmaf(NX[k], inv.x, -oi.x), fmaf(NY[k], inv.y, -oi.y)),
-                             fmaxf(fmaf(NZ[k], inv.z, -oi.z), 0.0f));
-      const float tf = fminf(fminf(fmaf(FX[k], inv.x, -oi.x), fmaf(FY[k], inv.y, -oi.y)),
-                             fminf(fmaf(FZ[k], inv.z, -oi.z), tr.tmax)) * kRobust;
-      d[k] = tn <= tf ? tn : kMiss;
-    }
-    return node_order(stk, tr, d, rf);
-  }
-  }
-  const DNode* nd = nodes + tr.node;
-  float4 lx = nd->lox, hx = nd->hix, ly = nd->loy, hy = nd->hiy, lz = nd->loz, hz = nd->hiz;
-  int4 rf = nd->ref;
-  if (FENCE) {  // all seven loads issued before the first wait (see leaf_step)
-    PT_FENCE4(hz);
+    nx = *(const float4*)(nb + (base + sx));
+    fx = *(const float4*)(nb + (base + (sx ^ 16u)));
+    ny = *(const float4*)(nb + (base + 32u + sy));
+    fy = *(const float4*)(nb + (base + 32u + (sy ^ 16u)));
+    nz = *(const float4*)(nb + (base + 64u + sz));
+    fz = *(const float4*)(nb + (base + 64u + (sz ^ 16u)));
+    rf = *(const int4*)(nb + (base + 96u));
+    PT_FENCE4(fz);
     PT_FENCE4(rf);
   }
   if (STATS) ct.nodes++;
   const float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
-  // (v_pk_fma_f32 over the SoA child pairs measured -2%: the broadcast
-  // operand pairs cost registers and moves)
-  const float* LX = &lx.x; const float* HX = &hx.x; const float* LY = &ly.x;
-  const float* HY = &hy.x; const float* LZ = &lz.x; const float* HZ = &hz.x;
+  const float* NX = &nx.x; const float* FX = &fx.x; const float* NY = &ny.x;
+  const float* FY = &fy.x; const float* NZ = &nz.x; const float* FZ = &fz.x;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    float ax = fmaf(LX[k], inv.x, -oi.x), bx = fmaf(HX[k], inv.x, -oi.x);
-    float ay = fmaf(LY[k], inv.y, -oi.y), by = fmaf(HY[k], inv.y, -oi.y);
-    float az = fmaf(LZ[k], inv.z, -oi.z), bz = fmaf(HZ[k], inv.z, -oi.z);
-    float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
-    float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tr.tmax)) * kRobust;
-    d[k] = tn <= tf ? tn : kMiss;
-  }
-  return node_order(stk, tr, d, rf);
-}
-
-// Node step of a wave whose node-stepping lanes all stand at the same node
-// `n` (wave-uniform, an SGPR): the node is read through the scalar cache
-// (constant address space: s_load, no vector-memory instruction, no texture
-// addresser cycles -- the path the per-lane node fetches saturate) and every
-// lane tests the four children against its own ray.  The direction signs may
-// differ per lane, so the slab test takes per-axis min/max here.
-typedef __attribute__((address_space(4))) const float4 cst_f4;
-typedef __attribute__((address_space(4))) const int4 cst_i4;
-template <bool STATS>
-__device__ __forceinline__ bool node_step_uniform(const DNode* __restrict__ nodes, int n, const Stack& stk, Trav& tr,
-                                                  Counters& ct) {
-  const float kRobust = PT_ROBUST;
-  const float kMiss = 3.0e38f;
-  // two s_load_dwordx16 (the 128-B node)
-  typedef float pt_v16f __attribute__((ext_vector_type(16)));
-  typedef __attribute__((address_space(4))) const pt_v16f cst_v16;
-  cst_v16* np = (cst_v16*)((const char*)nodes + ((size_t)(uint32_t)n << 7));
-  const pt_v16f A = np[0], B = np[1];
-  const float4 lx = make_float4(A[0], A[1], A[2], A[3]), hx = make_float4(A[4], A[5], A[6], A[7]);
-  const float4 ly = make_float4(A[8], A[9], A[10], A[11]), hy = make_float4(A[12], A[13], A[14], A[15]);
-  const float4 lz = make_float4(B[0], B[1], B[2], B[3]), hz = make_float4(B[4], B[5], B[6], B[7]);
-  const int4 rf = make_int4(__float_as_int(B[8]), __float_as_int(B[9]), __float_as_int(B[10]), __float_as_int(B[11]));
-  if (STATS) ct.nodes++;
-  const float3 o = tr.o, inv = tr.inv;
-  const float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
-  const float* LX = &lx.x; const float* HX = &hx.x; const float* LY = &ly.x;
-  const float* HY = &hy.x; const float* LZ = &lz.x; const float* HZ = &hz.x;
-  float d[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    float ax = fmaf(LX[k], inv.x, -oi.x), bx = fmaf(HX[k], inv.x, -oi.x);
-    float ay = fmaf(LY[k], inv.y, -oi.y), by = fmaf(HY[k], inv.y, -oi.y);
-    float az = fmaf(LZ[k], inv.z, -oi.z), bz = fmaf(HZ[k], inv.z, -oi.z);
-    float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
-    float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tr.tmax)) * kRobust;
+    const float tn = fmaxf(fmaxf(fmaf(NX[k], inv.x, -oi.x), fmaf(NY[k], inv.y, -oi.y)),
+                           fmaxf(fmaf(NZ[k], inv.z, -oi.z), 0.0f));
+    const float tf = fminf(fminf(fmaf(FX[k], inv.x, -oi.x), fmaf(FY[k], inv.y, -oi.y)),
+                           fminf(fmaf(FZ[k], inv.z, -oi.z), tr.tmax)) * kRobust;
     d[k] = tn <= tf ? tn : kMiss;
   }
   return node_order(stk, tr, d, rf);
@@ -554,12 +405,7 @@ __device__ __forceinline__ bool node_step2(const DNode2* __restrict__ nodes, con
   bool in1 = tn1 <= tf1;
   if (in0 && in1) {
     bool first0 = tn0 <= tn1;
-#if PT_REG_TOP
-    if (tr.sp > 0) stk.put(tr.sp - 1, tr.top);
-    tr.top = first0 ? e.y : e.x;
-#else
     stk.put(tr.sp, first0 ? e.y : e.x);
-#endif
     ++tr.sp;
     tr.node = first0 ? e.x : e.y;
   } else if (in0) {
@@ -584,26 +430,14 @@ __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const
   const bool two = n >= 2;
   const int pb = two ? pa + 1 : pa;
   float4 a0 = prims[pa].v0, a1 = prims[pa].e1, a2 = prims[pa].e2;
-#if PT_LEAF_MASK
-  // a one-primitive step issues no second triple of loads (vector-memory
-  // address cycles are counted per active lane)
-  float4 b0 = a0, b1 = a1, b2 = a2;
-  if (two) {
-    b0 = prims[pb].v0;
-    b1 = prims[pb].e1;
-    b2 = prims[pb].e2;
-  }
-#else
   float4 b0 = prims[pb].v0, b1 = prims[pb].e1, b2 = prims[pb].e2;
-#endif
   // One memory round trip per leaf step: without the fence the compiler sinks
   // the first primitive's e2 load into the triangle branch (a second
   // dependent L2 trip).  The fence makes the last-issued loads' values live
-  // here, so every load is issued before the one wait.
-  if (PT_LOAD_FENCE & 2) {
-    PT_FENCE4(a2);
-    PT_FENCE4(b2);
-  }
+  // here, so every load is issued before the one wait.  (Skipping the second
+  // triple for one-primitive steps measured -2%: the branch costs more.)
+  PT_FENCE4(a2);
+  PT_FENCE4(b2);
   if (prim_test<STATS>(a0, a1, a2, pa, tr, ct)) return true;
   if (two && prim_test<STATS>(b0, b1, b2, pb, tr, ct)) return true;
   if (n > 2) {
@@ -726,26 +560,13 @@ __device__ __forceinline__ void env_sample(const KParams& P, float r1, float r2,
   wi = f3(-st * sp, ct, st * cp);
 }
 
-// Unsigned 32.32 fixed point of a sample's radiance (PT_PIXEL_ACC): integer
-// sums are exact, so a pixel's value does not depend on the order or grouping
-// in which its samples are added.  Clamped to [0, 2^31) (NaN -> 0); the
-// fraction is truncated at 2^-32.
-__device__ __forceinline__ unsigned long long to_fixed32(float v) {
-  v = fminf(fmaxf(v, 0.0f), 2147483520.0f);
-  const uint32_t hi = (uint32_t)v;
-  const uint32_t lo = (uint32_t)((v - (float)hi) * 4294967296.0f);
-  return ((unsigned long long)hi << 32) | lo;
-}
-typedef __attribute__((address_space(3))) PxAcc lds_acc;
-typedef __attribute__((address_space(3))) unsigned long long lds_u64;
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-
-#ifndef PT_DRAIN_NO_ATOMIC
-#define PT_DRAIN_NO_ATOMIC 1
-#endif
-
 // Lane modes of the persistent kernel.
 enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
+
+// Wave-clock sections of the STATS build: every shader clock of a wave's
+// lifetime falls in exactly one (pt_stats.shade_clocks + trav_clocks = the
+// waves' summed lifetimes; section_clocks = S_HIT .. S_FETCH).
+enum : int { S_HIT = 0, S_NEE = 1, S_BSDF = 2, S_FETCH = 3, S_CAMERA = 4, S_TRAV = 5, S_OTHER = 6, S_N = 7 };
 
 // DBG: diagnostic build that printf-traces the pixel P.dbg_pix (PT_DEBUG_PIXEL=x,y)
 // Occupancy target: 5 waves per SIMD = at most 96 VGPRs (512 / 5, granule 8)
@@ -762,47 +583,18 @@ enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 // memory; the common build reads them from LDS through address-space-typed
 // pointers, never through FLAT accesses).
 template <bool STATS, bool DBG, bool BIN, bool ENV, bool GTAB>
-__global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void render_kernel(KParams P) {
-  // one PT_STACK x 64 region of the LDS stack per wave (lane-contiguous rows)
-  __shared__ int s_stack[PT_WG_WAVES * PT_STACK * PT_BLOCK];
-  const int lane = threadIdx.x & 63;
-  const uint32_t wave_id = blockIdx.x * PT_WG_WAVES + (threadIdx.x >> 6);  // the persistent wave
-  const uint32_t n_waves = gridDim.x * PT_WG_WAVES;
+__global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel(KParams P) {
+  // the wave's PT_STACK x 64 LDS stack (lane-contiguous rows)
+  __shared__ int s_stack[PT_STACK * PT_BLOCK];
+  const int lane = threadIdx.x;
+  const uint32_t wave_id = blockIdx.x;  // the persistent wave (one per workgroup)
+  const uint32_t n_waves = gridDim.x;
   const uint32_t gid = wave_id * PT_BLOCK + lane;
-  const Stack stk{(lds_int*)(s_stack + (threadIdx.x >> 6) * (PT_STACK * PT_BLOCK) + lane),
-                  P.stack_spill ? P.stack_spill + gid : nullptr, n_waves * PT_BLOCK};
-  // BVH4 treelet: the first n_treelet nodes (the top levels, breadth-first
-  // order) copied once per workgroup; node steps on them read LDS
-  __shared__ DNode s_tree[PT_TREELET > 0 ? PT_TREELET : 1];
-  if (PT_TREELET > 0) {
-    const int nt = min(P.n_treelet, PT_TREELET) * (int)(sizeof(DNode) / 16);
-    for (int k = threadIdx.x; k < nt; k += PT_BLOCK * PT_WG_WAVES)
-      ((float4*)s_tree)[k] = ((const float4*)P.nodes)[k];
-  }
-  const int n_tree = PT_TREELET > 0 ? min(P.n_treelet, PT_TREELET) : 0;
-#if PT_ROOT_LDS
-  // The BVH4 root, which every ray visits first: one LDS copy per workgroup,
-  // so the root step of a fresh ray costs no vector-memory traffic (below).
-  // PT_ROOT_LDS >= 2: also the root's (up to four) internal children, slots 1-4
-  __shared__ DNode s_root[PT_ROOT_LDS >= 2 ? 5 : 1];
-  if (!BIN && threadIdx.x < (int)(sizeof(DNode) / 16)) ((float4*)s_root)[threadIdx.x] = ((const float4*)P.nodes)[threadIdx.x];
-#if PT_ROOT_LDS >= 2
-  int4 top_ref = make_int4(-1, -1, -1, -1);  // the root's children as LDS slots 1-4 (-1: leaf / empty)
-  if constexpr (!BIN) {
-    const int4 rr = P.nodes[0].ref;  // wave-uniform
-    const float4 lx = P.nodes[0].lox;
-    const int r[4] = {rr.x, rr.y, rr.z, rr.w};
-    const float l[4] = {lx.x, lx.y, lx.z, lx.w};
-    int t[4];
-    for (int k = 0; k < 4; ++k) {
-      t[k] = (r[k] > 0 && !__builtin_isinf(l[k])) ? r[k] : -1;
-      if (t[k] > 0 && threadIdx.x < (int)(sizeof(DNode) / 16))
-        ((float4*)(s_root + 1 + k))[threadIdx.x] = ((const float4*)(P.nodes + t[k]))[threadIdx.x];
-    }
-    top_ref = make_int4(t[0], t[1], t[2], t[3]);
-  }
-#endif
-#endif
+  const Stack stk{(lds_int*)(s_stack + lane), P.stack_spill ? P.stack_spill + gid : nullptr, n_waves * PT_BLOCK};
+  // The BVH4 root, which every ray visits first: one LDS copy per wave, so
+  // the root step of a fresh ray costs no vector-memory traffic (C3 +2%).
+  __shared__ DNode s_root;
+  if (!BIN && lane < (int)(sizeof(DNode) / 16)) ((float4*)&s_root)[lane] = ((const float4*)P.nodes)[lane];
 
   // Material and light tables are read by every shading step: keep small
   // ones in LDS (the usual case); larger ones stay in global memory.
@@ -811,9 +603,9 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
   typedef __attribute__((address_space(3))) const float lds_f;
   if (!GTAB) {
     const int nb = P.n_bsdfs * (int)(sizeof(DBsdf) / 4);
-    for (int k = threadIdx.x; k < nb; k += PT_BLOCK * PT_WG_WAVES) ((float*)s_bsdf)[k] = ((const float*)P.bsdfs)[k];
+    for (int k = lane; k < nb; k += PT_BLOCK) ((float*)s_bsdf)[k] = ((const float*)P.bsdfs)[k];
     const int nl = P.n_lights * (int)(sizeof(DLight) / 4);
-    for (int k = threadIdx.x; k < nl; k += PT_BLOCK * PT_WG_WAVES) ((float*)s_light)[k] = ((const float*)P.lights)[k];
+    for (int k = lane; k < nl; k += PT_BLOCK) ((float*)s_light)[k] = ((const float*)P.lights)[k];
   }
   // Table fields are read where they are used (address-space-typed ds_read
   // loads in the LDS build), never copied whole into registers: every value
@@ -828,30 +620,28 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
   };
 #define PT_BSDF3(i, field) f3(bsdf_f(i, offsetof(DBsdf, field) / 4), bsdf_f(i, offsetof(DBsdf, field) / 4 + 1), bsdf_f(i, offsetof(DBsdf, field) / 4 + 2))
 #define PT_LIGHT3(i, field) f3(light_f(i, offsetof(DLight, field) / 4), light_f(i, offsetof(DLight, field) / 4 + 1), light_f(i, offsetof(DLight, field) / 4 + 2))
-#if PT_PIXEL_ACC
-  // The wave's ring of pixel accumulators: a pixel's samples are summed on
-  // chip and the lane that completes the pixel writes its mean, so no
-  // per-group sums go through HBM.  A wave claims whole pixels (every group
-  // of a pixel is rendered by this wave) and only when the ring has room.
-  __shared__ PxAcc s_ring[PT_WG_WAVES * PT_RING];
-  lds_acc* const ring = (lds_acc*)(s_ring + (threadIdx.x >> 6) * PT_RING);
-  if (lane < PT_RING) {
-    ring[lane].s[0] = ring[lane].s[1] = ring[lane].s[2] = 0ull;
-    ring[lane].count = 0u;
-    ring[lane].owner = PT_RING_FREE;
-  }
-#endif
+  // STATS: the wave's clock sections and its last stamp, in LDS.  A stamp is
+  // written by the first ACTIVE lane, so stamps inside divergent shading code
+  // account the wave's time whichever lanes took the branch.
+  __shared__ unsigned long long s_clk[STATS ? S_N + 1 : 1];
+  if (STATS && lane <= S_N) s_clk[lane] = lane == S_N ? clock64() : 0ull;
   __syncthreads();
+#define PT_STAMP(k)                                                  \
+  if (STATS) {                                                       \
+    const unsigned long long t_ = clock64();                         \
+    if (lane == __builtin_amdgcn_readfirstlane(lane)) {              \
+      s_clk[k] += t_ - s_clk[S_N];                                   \
+      s_clk[S_N] = t_;                                               \
+    }                                                                \
+  }
 
   // ---- per-lane state
   int mode = M_FETCH;
   bool shadow = false;  // the ray in flight is a shadow ray
-  // the work slot (pixel, sample group) this lane renders: its pixel and
-  // current sample; the group is sample / group_spp
+  // the work slot (pixel, sample group) this lane renders: its pixel as packed
+  // coordinates (x | y << 16; W, H <= 65535) and its current sample; the
+  // group is sample / group_spp
   int pix = 0, sample = 0;
-#if PT_PIXEL_ACC
-  int rslot = 0;  // the pixel's accumulator in the wave's ring
-#endif
   // the sample's stream and the counter word of its next draw (ptrng::draw_at)
   uint32_t rbase = 0, rdim = ptrng::kDrawInit;
 #define PT_DRAW() ptrng::draw_at(rbase, (rdim += ptrng::kDrawStep) - ptrng::kDrawStep)
@@ -867,42 +657,18 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
   float3 hp = f3(0, 0, 0), ns = f3(0, 0, 1), ng = f3(0, 0, 1);
   int bsdf = 0;
   float3 pend = f3(0, 0, 0);  // NEE contribution awaiting its shadow ray
-  // PT_EARLY_BOUNCE: what follows the shadow ray in flight -- 0: the shading
-  // round (more light samples, then the bounce), 1: the bounce ray already
-  // sampled (origin in hp, direction in ns), 2: the end of the sample
-  int post = 0;
   Trav tr;
   trav_init(tr, f3(0, 0, 0), f3(0, 0, 1), 0.0f, false);
   Counters ct = {0, 0, 0};
   uint32_t n_cam = 0, n_bounce = 0, n_shadow = 0, n_hits = 0;
   uint32_t n_titer = 0, n_rounds = 0;  // wave-level traversal steps / shading rounds (lane 0)
   uint32_t n_leafit = 0;               // of the traversal steps: leaf steps
-  uint32_t n_uninode = 0;              // of the traversal steps: wave-uniform node steps (PT_SCALAR_NODE)
   // traversal lane-iterations: at the other step kind, finished and waiting
   // for the shading round, retired, stepping a leaf
   uint32_t l_other = 0, l_ready = 0, l_dead = 0, l_leaf = 0;
   uint32_t n_atomics = 0;              // work-queue atomics (lane 0)
   uint32_t chunk_next = 0, chunk_end = 0;  // the wave's private range of work slots
   uint32_t seen = 0;                       // queue head after this wave's last claim
-#if PT_PIXEL_ACC
-  // ring bookkeeping (wave-uniform): the ring position of the next claimed
-  // pixel, and of the current chunk's first pixel + that chunk's first slot
-  uint32_t px_seq = 0, cur_px = 0, cur_first = 0, old_px = 0, old_first = 0;
-#endif
-#if PT_XCD_QUEUES > 1
-  // the wave's current queue (its XCD's first) and how many it found exhausted
-  uint32_t qcur = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) % PT_XCD_QUEUES, qtried = 0;
-#endif
-  unsigned long long cyc_shade = 0, cyc_trav = 0;  // shader clocks per phase (lane 0)
-  unsigned long long cyc_hitshade = 0;              // of which: shading before the refill
-  unsigned long long cyc_sec[4] = {0, 0, 0, 0};     // of which: hit record, NEE, bounce, refill fetch
-#define PT_STAMP(k)                                 \
-  if (STATS) {                                      \
-    unsigned long long t_ = clock64();              \
-    cyc_sec[k] += lane == 0 ? t_ - t_mark : 0ull;   \
-    t_mark = t_;                                    \
-  }
-  unsigned long long t_mark = STATS ? clock64() : 0ull;
   const unsigned long long w_start = STATS ? wall_clock64() : 0ull;
   unsigned long long w_empty = 0ull;  // when this wave first found the queue empty
   unsigned long long slot_t0 = 0ull, slot_lat_sum = 0ull, slot_lat_max = 0ull;  // work-slot latency (wall ticks)
@@ -916,7 +682,6 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
   }
 
   const uint32_t n_groups = (uint32_t)P.n_groups;
-#if PT_INT_SHORTCUTS
   // group arithmetic by shifts when the sizes are powers of two (the usual
   // case; wave-uniform branches), the exact divisions otherwise
   auto group_of = [&](int s) -> int { return P.group_shift >= 0 ? s >> P.group_shift : s / P.group_spp; };
@@ -926,55 +691,14 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
   auto pixel_of_slot = [&](uint32_t slot) -> uint32_t {
     return P.ngroup_shift >= 0 ? slot >> P.ngroup_shift : slot / n_groups;
   };
-  // `pix` holds the pixel's coordinates (x | y << 16, W, H <= 65535) and its
-  // index is rebuilt with one multiply-add: no division per camera ray
+  // the pixel index from the packed coordinates: one multiply-add, no
+  // division per camera ray
   auto pix_index = [&](int p) -> int { return (p & 0xffff) + (int)((uint32_t)p >> 16) * P.W; };
-#else
-  auto group_of = [&](int s) -> int { return s / P.group_spp; };
-  auto group_starts = [&](int s) -> bool { return s % P.group_spp == 0; };
-  auto pixel_of_slot = [&](uint32_t slot) -> uint32_t { return slot / n_groups; };
-  auto pix_index = [&](int p) -> int { return p; };
-#endif
-#if PT_PIXEL_ACC
-  // A sample of this lane's pixel finished (`sample` already advanced).  The
-  // lane sums its group's samples in float (in sample order, as the group
-  // layout fixed per frame dictates); at the end of the group, one-group
-  // pixels (the lane rendered every sample) write the mean, otherwise the
-  // group sum goes into the ring in exact fixed point and the lane that
-  // brings the pixel's count of groups to n_groups writes its mean.
-  auto sample_done = [&]() {
-    if (sample < P.spp && sample % P.group_spp != 0) return;  // the group goes on
-    if (n_groups == 1u) {
-      store3(P.fb + 3 * (size_t)pix_index(pix), acc * (float)(1.0 / (double)P.spp));
-      return;
-    }
-    __hip_atomic_fetch_add((lds_u64*)&ring[rslot].s[0], to_fixed32(acc.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_add((lds_u64*)&ring[rslot].s[1], to_fixed32(acc.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_add((lds_u64*)&ring[rslot].s[2], to_fixed32(acc.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const uint32_t done = __hip_atomic_fetch_add((lds_u32*)&ring[rslot].count, 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (done == n_groups - 1u) {  // the pixel's last group: every add above is in
-      const double k = 2.3283064365386963e-10 / (double)P.spp;  // 2^-32 / spp
-      store3(P.fb + 3 * (size_t)pix_index(pix), f3((float)((double)ring[rslot].s[0] * k), (float)((double)ring[rslot].s[1] * k),
-                                        (float)((double)ring[rslot].s[2] * k)));
-      ring[rslot].s[0] = ring[rslot].s[1] = ring[rslot].s[2] = 0ull;
-      ring[rslot].count = 0u;
-      ring[rslot].owner = PT_RING_FREE;
-    }
-    acc = f3(0, 0, 0);
-  };
-#else
   // partial-sum slot of a finished group: (pixel, group of the last sample)
   auto slot_of = [&](int p, int s_next) -> size_t {
     return (size_t)pix_index(p) * n_groups + (uint32_t)group_of(s_next - 1);
   };
-#endif
   const uint32_t total_slots = (uint32_t)P.n_blocks * 64u * n_groups;
-  // first slot of queue part q (part PT_XCD_QUEUES ends at total_slots)
-  auto q_start = [&](uint32_t q) -> uint32_t {
-    return (uint32_t)(((uint64_t)total_slots * q) / PT_XCD_QUEUES);
-  };
-  (void)q_start;
   const int batch = P.shade_batch;
 
   for (;;) {
@@ -982,21 +706,11 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
     if (mode == M_SHADE) {
       const bool found = tr.found;
       bool finish = false;  // the sample is complete
-      int stage;            // 0: NEE loop, 1: BSDF step, 2: none
+      int stage;            // 0: NEE (+ bounce), 2: none
       if (shadow) {
         if (!found) acc = acc + pend;  // unoccluded (the light sample was already counted)
         if (DBG && pix_index(pix) == P.dbg_pix) printf("    shadow %s (pend %.6g) prim %d t %.9g\n", found ? "occluded" : "clear", pend.x, tr.prim, tr.tmax);
         stage = 0;
-        if (PT_EARLY_BOUNCE && post == 1) {  // the bounce was sampled with the last light sample
-          trav_init(tr, hp, ns, 3.0e38f, false);
-          shadow = false;
-          mode = M_TRAV;
-          stage = 3;
-        } else if (PT_EARLY_BOUNCE && post == 2) {
-          finish = true;
-          stage = 2;
-        }
-        post = 0;
       } else if (!found) {
         // miss: the environment map if there is one and includeLe (pathtracer.cpp:411-427)
         if (ENV && includeLe) acc = acc + mul(T, env_dir(P, tr.d));
@@ -1007,19 +721,14 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         // ---- hit record (Intersection, trace_ray lines 435-456).  Hit points
         // are rebuilt from the primitive (barycentrics / sphere reprojection),
         // not o + t*d, so their error is relative to the primitive and the
-        // 256-ulp origin offset always clears the surface.
+        // 256-ulp origin offset always clears the surface.  The whole record
+        // and the vertex normals are fetched in one memory round trip
+        // (unfenced, the e1/e2 and normal loads wait behind the meta branch).
         DPrim pr = P.prims[tr.prim];
-#if PT_HIT_FENCE
-        // the whole record and the vertex normals in one memory round trip
-        // (unfenced, the e1/e2 and normal loads wait behind the meta branch)
-        float nnv[9];
-        for (int k = 0; k < 9; ++k) nnv[k] = P.norms[9 * (size_t)tr.prim + k];
+        float nn[9];
+        for (int k = 0; k < 9; ++k) nn[k] = P.norms[9 * (size_t)tr.prim + k];
         PT_FENCE4(pr.e2);
-        asm volatile("" : "+v"(nnv[8]));
-        const float* nn = nnv;
-#else
-        const float* nn = P.norms + 9 * (size_t)tr.prim;
-#endif
+        asm volatile("" : "+v"(nn[8]));
         const int meta = __float_as_int(pr.v0.w);  // (bsdf << 1) | is_triangle
         bsdf = meta >> 1;
         if (meta & 1) {
@@ -1046,13 +755,14 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         cur &= 0xffu;  // NEE starts at light 0, sample 0
         stage = 0;
       }
-      PT_STAMP(0);
+      PT_STAMP(S_HIT);
       if (stage < 2) {
         const int btype = __float_as_int(bsdf_f(bsdf, 0));
         const Frame fr = make_frame(ns);
         bool emitted = false;
-        bool emit_last = false;  // the shadow ray emitted is the vertex's last light sample
-        // ---- next-event estimation over all lights (pathtracer.cpp:469-523)
+        // ---- next-event estimation over all lights (pathtracer.cpp:469-523),
+        // one light sample per shading round: the lane leaves with the sample's
+        // shadow ray and resumes at the cursor when it returns
         int li = (int)(cur >> 16), ls = (int)((cur >> 8) & 0xffu);
         while (li < P.n_lights) {
           const int ltype = __float_as_int(light_f(li, 0));
@@ -1099,13 +809,9 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
             dist = 3.0e38f;
             pdf = 1.0f;
           }
-#if PT_NLS_RCP
-          const float scale = rcp((float)nls);  // v_rcp_f32: exact for 1, 2, 4, ... light samples
-#else
-          const float scale = 1.0f / (float)nls;
-#endif
+          // (float)(1.0 / num_light_samples) (pathtracer.cpp:481), from the host
+          const float scale = delta ? 1.0f : P.nls_scale;
           ++ls;
-          emit_last = ls >= nls && li + 1 >= P.n_lights;
           // f() is zero for every BSDF but Diffuse (bsdf.cpp:34-202): nothing to add.
           if (btype != 0 || !lit) continue;
           float cos_t = fmaxf(0.0f, fr.to_local(wi).z);
@@ -1122,20 +828,12 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
           break;
         }
         cur = (cur & 0xffu) | ((uint32_t)ls << 8) | ((uint32_t)li << 16);
-        PT_STAMP(1);
+        PT_STAMP(S_NEE);
         if (emitted) {
           shadow = true;
           mode = M_TRAV;
-        }
-        // Without PT_EARLY_BOUNCE the bounce waits for the shading round after
-        // the vertex's last shadow ray.  With it, the bounce is sampled now,
-        // together with the last light sample (the same draws in the same
-        // order: every light draw precedes it), and the lane starts the bounce
-        // ray right where its shadow ray ends, inside the traversal loop.
-        if (emitted && !(PT_EARLY_BOUNCE && emit_last)) {
         } else if ((int)(cur & 0xffu) >= P.max_depth) {
-          if (emitted) post = 2;
-          else finish = true;
+          finish = true;
         } else {
           // ---- indirect bounce (pathtracer.cpp:527-552)
           float3 wi;
@@ -1194,49 +892,32 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
           float pterm = fmaxf(1.0f - illum(f), 0.0f);
           if (PT_DRAW() < pterm) {
             if (DBG && pix_index(pix) == P.dbg_pix) printf("    RR terminate (p=%.4g)\n", pterm);
-            if (emitted) post = 2;
-            else finish = true;
+            finish = true;
           } else {
             if (DBG && pix_index(pix) == P.dbg_pix) printf("    bounce wi=(%.6g %.6g %.6g) pdf %.5g p %.4g dim word %08x\n", wi.x, wi.y, wi.z, pdf, pterm, rdim);
             T = mul(T, f * (fabsf(wi.z) * rcp(pdf * (1.0f - pterm))));
             float3 v = normalize(fr.to_world(wi));
             const float3 bo = offset_ray(hp, dot(v, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng);
-            if (emitted) {  // after the shadow ray (tr holds it now)
-              hp = bo;
-              ns = v;
-              post = 1;
-            } else {
-              trav_init(tr, bo, v, 3.0e38f, false);
-              shadow = false;
-              mode = M_TRAV;
-            }
+            trav_init(tr, bo, v, 3.0e38f, false);
+            shadow = false;
+            mode = M_TRAV;
             includeLe = btype == 1 || btype == 2 || btype == 3;
             ++cur;  // depth + 1
             if (STATS) n_bounce++;
           }
         }
       }
-      PT_STAMP(2);
       if (finish) {
         ++sample;
-#if PT_PIXEL_ACC
-        sample_done();
-#endif
         if (sample < P.spp && !group_starts(sample)) {
           mode = M_CAMERA;
         } else {
-#if !PT_PIXEL_ACC
-          store3_stream(P.partial + 3 * slot_of(pix, sample), acc);
-#endif
+          store3(P.partial + 3 * slot_of(pix, sample), acc);
           PT_SLOT_DONE();
           mode = M_FETCH;
         }
       }
-    }
-    if (STATS) {
-      unsigned long long t = clock64();
-      cyc_hitshade += lane == 0 ? t - t_mark : 0ull;
-      t_mark = t;
+      PT_STAMP(S_BSDF);
     }
     // ---- refill: wave-aggregated pixel fetch (one atomic per wave per round)
     // and camera rays.  Camera rays that miss the scene's root box carry zero
@@ -1246,7 +927,6 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
     for (;;) {
       bool need = mode == M_FETCH;
       unsigned long long m = __ballot(need);
-      bool blocked = false;  // PT_PIXEL_ACC: the ring has no room for a new chunk's pixels
       if (m != 0ull) {
         // Lanes are served from the wave's private chunk of consecutive slots;
         // one atomic refills it.  Guided self-scheduling: a chunk is about
@@ -1254,73 +934,12 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         // PT_CHUNK and PT_CHUNK_MAX, so early chunks are large (few atomics on
         // the one queue head, which sits memory-side since the XCD L2s are
         // not coherent) and the tail is handed out 64 slots at a time.
+        // (One queue per XCD over bands of the frame measured C3 -9%.)
         uint32_t cnt = (uint32_t)__popcll(m);
         uint32_t avail = chunk_end - chunk_next;
         uint32_t nbase = 0, csize = 0;
-#if PT_XCD_QUEUES > 1
-        // Per-XCD queues: the slot range is split into PT_XCD_QUEUES
-        // contiguous parts (horizontal bands of the footprint), and a wave
-        // claims from the part of its own XCD first, so each XCD's L2 holds
-        // the geometry its band sees; an exhausted part sends the wave to the
-        // next one (stealing), and the wave retires once all were exhausted.
-        uint32_t limit = chunk_end;  // first slot past the chunk handed out now
         if (cnt > avail) {
-          if (qtried >= PT_XCD_QUEUES) {
-            nbase = limit = total_slots;
-          } else {
-            const uint32_t q_lo = q_start(qcur), q_hi = q_start(qcur + 1);
-            csize = PT_CHUNK;
-            uint32_t old = 0;
-            if (lane == 0) old = atomicAdd(P.work_counter + 32 * qcur, csize);
-            old = __builtin_amdgcn_readfirstlane(__shfl(old, 0));  // wave-uniform: an SGPR
-            if (STATS) n_atomics += lane == 0;
-            nbase = q_lo + min(old, q_hi - q_lo);
-            limit = q_lo + min(old + csize, q_hi - q_lo);
-            if (old + csize >= q_hi - q_lo) {  // this part is exhausted after this chunk
-              qcur = qcur + 1 == PT_XCD_QUEUES ? 0u : qcur + 1;
-              ++qtried;
-            }
-          }
-        }
-        if (need) {
-          uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-          uint32_t slot = rank < avail ? chunk_next + rank : nbase + (rank - avail);
-          if (rank >= avail && slot >= limit) {
-            // nothing for this lane in this claim: it retries from the next
-            // part, or retires when every part was exhausted
-            if (qtried >= PT_XCD_QUEUES) {
-              mode = M_DONE;
-              if (STATS && w_empty == 0ull) w_empty = wall_clock64();
-            }
-          } else {
-            uint32_t bq = pixel_of_slot(slot);
-            uint32_t g = slot - bq * n_groups;
-            int4 b = P.blocks[bq >> 6];
-            int qx = (int)(bq & 7u), qy = (int)((bq >> 3) & 7u);
-            if (qx < b.z && qy < b.w) {
-#if PT_INT_SHORTCUTS
-              pix = (b.x + qx) | ((b.y + qy) << 16);
-#else
-              pix = b.x + qx + (b.y + qy) * P.W;
-#endif
-              sample = (int)g * P.group_spp;
-              acc = f3(0, 0, 0);
-              if (STATS) slot_t0 = wall_clock64();
-              mode = M_CAMERA;
-            }
-          }
-        }
-        if (cnt > avail) {  // wave-uniform
-          chunk_next = min(nbase + (cnt - avail), limit);
-          chunk_end = limit;
-        } else {
-          chunk_next += cnt;
-        }
-#else
-        bool claimed = false;  // PT_PIXEL_ACC: this refill took a new chunk (the ring bookkeeping moved)
-        (void)claimed;
-        if (cnt > avail) {
-          if (PT_DRAIN_NO_ATOMIC && seen >= total_slots) {
+          if (seen >= total_slots) {
             // This wave already saw the queue drained: every further claim
             // would fail.  No atomic -- in the drain, one per wave per round
             // on the single queue head (memory-side, serialised, slower from
@@ -1330,53 +949,16 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
           } else {
             const uint32_t left = total_slots - seen;
             csize = min((uint32_t)PT_CHUNK_MAX, max((uint32_t)PT_CHUNK, left / (PT_CHUNK_DIV * n_waves))) & ~63u;
-#if PT_PIXEL_ACC
-            uint32_t k_px = 0;  // pixels of the new chunk
-            if (n_groups > 1u) {
-              // whole pixels per chunk (every chunk starts on a pixel), and
-              // only when their ring slots are free
-              csize = (csize + n_groups - 1u) / n_groups * n_groups;
-              k_px = csize / n_groups;
-              const bool busy = lane < (int)k_px && ring[(px_seq + (uint32_t)lane) & (PT_RING - 1)].owner != PT_RING_FREE;
-              blocked = __ballot(busy) != 0ull;
-            }
-            if (!blocked) {
-#endif
-              if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
-              nbase = __builtin_amdgcn_readfirstlane(__shfl(nbase, 0));  // wave-uniform: an SGPR
-              seen = nbase + csize;
-              if (STATS) n_atomics += lane == 0;
-#if PT_PIXEL_ACC
-              if (n_groups > 1u) {
-                // take the ring slots of the chunk's (existing) pixels
-                if (lane < (int)k_px) {
-                  const uint32_t bq = nbase / n_groups + (uint32_t)lane;
-                  if (bq * n_groups < total_slots) {
-                    const int4 b = P.blocks[bq >> 6];
-                    if ((int)(bq & 7u) < b.z && (int)((bq >> 3) & 7u) < b.w)
-                      ring[(px_seq + (uint32_t)lane) & (PT_RING - 1)].owner = bq;
-                  }
-                }
-                old_px = cur_px;
-                old_first = cur_first;
-                cur_px = px_seq;
-                cur_first = nbase;
-                px_seq = __builtin_amdgcn_readfirstlane(px_seq + k_px);
-                claimed = true;
-              }
-            } else {
-              csize = 0;
-            }
-#endif
+            if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
+            nbase = __builtin_amdgcn_readfirstlane(__shfl(nbase, 0));  // wave-uniform: an SGPR
+            seen = nbase + csize;
+            if (STATS) n_atomics += lane == 0;
           }
         }
         if (need) {
           uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-          const bool from_old = rank < avail;
-          uint32_t slot = from_old ? chunk_next + rank : nbase + (rank - avail);
-          if (!from_old && blocked) {
-            // no slot this round: the lane stays M_FETCH until the ring has room
-          } else if (slot >= total_slots) {
+          uint32_t slot = rank < avail ? chunk_next + rank : nbase + (rank - avail);
+          if (slot >= total_slots) {
             mode = M_DONE;
             if (STATS && w_empty == 0ull) w_empty = wall_clock64();
           } else {
@@ -1390,47 +972,28 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
             int4 b = P.blocks[bq >> 6];
             int qx = (int)(bq & 7u), qy = (int)((bq >> 3) & 7u);
             if (qx < b.z && qy < b.w) {
-#if PT_INT_SHORTCUTS
               pix = (b.x + qx) | ((b.y + qy) << 16);
-#else
-              pix = b.x + qx + (b.y + qy) * P.W;
-#endif
               sample = (int)g * P.group_spp;
               acc = f3(0, 0, 0);
-#if PT_PIXEL_ACC
-              // the ring slot of the slot's pixel: pixels of a chunk take
-              // consecutive ring positions from the chunk's first one
-              const bool in_cur = !from_old || !claimed;
-              const uint32_t base_px = in_cur ? cur_px : old_px, first = in_cur ? cur_first : old_first;
-              rslot = (int)((base_px + (slot - first) / n_groups) & (PT_RING - 1));
-#endif
               if (STATS) slot_t0 = wall_clock64();
               mode = M_CAMERA;
             }
           }
         }
-        if (cnt > avail && !blocked) {  // wave-uniform
+        if (cnt > avail) {  // wave-uniform
           chunk_next = nbase + (cnt - avail);
           chunk_end = nbase + csize;
           if (csize == 0) chunk_next = chunk_end = total_slots;  // drained: nothing left to hand out
-        } else if (cnt > avail) {  // blocked: the old chunk is used up, no new one yet
-          chunk_next = chunk_end;
         } else {
           chunk_next += cnt;
         }
-#endif
       }
-      PT_STAMP(3);
+      PT_STAMP(S_FETCH);
       // ---- camera rays: Camera::generate_ray (camera.cpp:113-129) at the
       // jittered pixel position of raytrace_pixel (pathtracer.cpp:571-575)
       while (mode == M_CAMERA) {
-#if PT_INT_SHORTCUTS
         const int px = pix & 0xffff, py = (int)((uint32_t)pix >> 16);
         rbase = ptrng::stream_base(P.seed, (uint32_t)(px + py * P.W), (uint32_t)sample + P.sample_base);
-#else
-        rbase = ptrng::stream_base(P.seed, (uint32_t)pix, (uint32_t)sample + P.sample_base);
-        const int py = pix / P.W, px = pix - py * P.W;
-#endif
         rdim = ptrng::kDrawInit;
         float ry = PT_DRAW();  // UniformGridSampler2D draws y first
         float rx = PT_DRAW();
@@ -1453,50 +1016,29 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         // miss: the sample sees the environment (includeLe) or nothing
         if (ENV) acc = acc + env_dir(P, d);
         ++sample;
-#if PT_PIXEL_ACC
-        sample_done();
-#endif
         if (sample >= P.spp || group_starts(sample)) {
-#if !PT_PIXEL_ACC
-          store3_stream(P.partial + 3 * slot_of(pix, sample), acc);
-#endif
+          store3(P.partial + 3 * slot_of(pix, sample), acc);
           PT_SLOT_DONE();
           mode = M_FETCH;
         }
       }
-      // (blocked: let the wave's other paths progress; the claim is retried next round)
-      if (__ballot(mode == M_FETCH) == 0ull || blocked) break;
+      PT_STAMP(S_CAMERA);
+      if (__ballot(mode == M_FETCH) == 0ull) break;
     }
     // ================= traversal phase =================
     // Step every in-flight ray one node at a time; leave as soon as `batch`
     // lanes have finished their ray, so finished lanes are refilled together
     // (coherent shading) while the others keep their traversal state.
     if (__ballot(mode == M_TRAV) == 0ull) break;  // every lane is M_DONE
-#if PT_ROOT_LDS
     // Fresh rays (node 0: references only point forward, so no ray returns
     // to the root) take their root step here, all together, from the LDS
     // copy: the wave's first traversal iteration no longer waits on a global
     // load for them.
     if constexpr (!BIN) {
       if (mode == M_TRAV && tr.node == 0) {
-        if (node_step<STATS, false, PT_OCTANT != 0 && (!ENV || PT_ENV_OCT), true>(P.nodes, stk, tr, ct, (lds_cchar*)s_root, 1))
-          mode = M_SHADE;
+        if (node_step<STATS, true>(P.nodes, stk, tr, ct, (lds_cchar*)&s_root)) mode = M_SHADE;
       }
-#if PT_ROOT_LDS >= 2
-      // ...and every ray at one of the root's children (fresh rays after
-      // their root step, or one popped back to it) takes that step from LDS too
-      const int k1 = tr.node == top_ref.x ? 1 : tr.node == top_ref.y ? 2 : tr.node == top_ref.z ? 3
-                   : tr.node == top_ref.w ? 4 : 0;
-      if (mode == M_TRAV && tr.node > 0 && k1 > 0) {
-        const int nd = tr.node;
-        tr.node = 0;  // the LDS slot as node 0 of a one-node "tree" at s_root + k1
-        if (node_step<STATS, false, PT_OCTANT != 0 && (!ENV || PT_ENV_OCT), true>(P.nodes, stk, tr, ct, (lds_cchar*)(s_root + k1), 1))
-          mode = M_SHADE;
-        (void)nd;
-      }
-#endif
     }
-#endif
     // Once the queue is drained, lanes retire (M_DONE): shade when 3/4 of the
     // lanes still working are ready, not when `batch` of 64 are, or the tail
     // would wait for the slowest ray of the wave at every bounce.
@@ -1504,12 +1046,7 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
     int round_batch = min(batch, (3 * alive + 3) / 4);
     if (P.drain_div > 0 && seen >= total_slots)  // the queue is drained: latency, not throughput
       round_batch = max(1, alive / P.drain_div);
-    if (STATS) {
-      n_rounds += lane == 0;
-      unsigned long long t = clock64();
-      cyc_shade += lane == 0 ? t - t_mark : 0ull;
-      t_mark = t;
-    }
+    if (STATS) n_rounds += lane == 0;
     if (STATS) r_rounds += mode == M_TRAV;
     for (;;) {
       if (STATS) n_titer += lane == 0;
@@ -1535,39 +1072,11 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
       if (leaf_iter) {
         if (at_leaf) done = leaf_step<STATS>(P.prims, stk, tr, ct);
         if (STATS) n_leafit += lane == 0;
-      } else {
-        if (trav && !at_leaf) {
-          if constexpr (BIN) {
-            done = node_step2<STATS>(P.nodes2, stk, tr, ct);
-          } else {
-#if PT_SCALAR_NODE
-            // every node-stepping lane at one node: fetch it through the
-            // scalar cache (coherent camera and shadow rays high in the tree)
-            const int n0 = __builtin_amdgcn_readfirstlane(tr.node);
-            if (__ballot(tr.node != n0) == 0ull) {
-              if (STATS) n_uninode += lane == __builtin_amdgcn_readfirstlane(lane);
-              done = node_step_uniform<STATS>(P.nodes, n0, stk, tr, ct);
-            } else
-#endif
-            done = node_step<STATS, (PT_LOAD_FENCE & 1) != 0 && (!ENV || PT_ENV_FENCE), PT_OCTANT != 0 && (!ENV || PT_ENV_OCT),
-                             (PT_TREELET > 0) && !ENV>(P.nodes, stk, tr, ct, (lds_cchar*)s_tree, n_tree);
-          }
-        }
+      } else if (trav && !at_leaf) {
+        if constexpr (BIN) done = node_step2<STATS>(P.nodes2, stk, tr, ct);
+        else done = node_step<STATS>(P.nodes, stk, tr, ct);
       }
       if (done) mode = M_SHADE;
-#if PT_EARLY_BOUNCE
-      // a shadow ray ended whose bounce is already sampled: add the light
-      // sample and go on with the bounce ray, no shading round
-      if (__ballot(done && shadow && post == 1) != 0ull) {
-        if (done && shadow && post == 1) {
-          if (!tr.found) acc = acc + pend;
-          trav_init(tr, hp, ns, 3.0e38f, false);
-          shadow = false;
-          post = 0;
-          mode = M_TRAV;
-        }
-      }
-#endif
       if (STATS && done) {
         ray_steps_max = max(ray_steps_max, r_steps);
         ray_idle_max = max(ray_idle_max, r_idle);
@@ -1578,17 +1087,14 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
       unsigned long long busy = __ballot(mode == M_TRAV);
       if (busy == 0ull || __popcll(ready) >= round_batch) break;
     }
-    if (STATS) {
-      unsigned long long t = clock64();
-      cyc_trav += lane == 0 ? t - t_mark : 0ull;
-      t_mark = t;
-    }
+    PT_STAMP(S_TRAV);
   }
 
   if (STATS) {
-    unsigned long long v[13] = {n_cam,   n_bounce, n_shadow,  ct.nodes,  ct.tris,  ct.spheres, n_hits,
-                                n_titer, n_rounds, n_leafit,  n_atomics, cyc_shade + cyc_hitshade, cyc_trav};
-    for (int k = 0; k < 13; ++k) {
+    PT_STAMP(S_OTHER);
+    unsigned long long v[11] = {n_cam, n_bounce, n_shadow, ct.nodes, ct.tris, ct.spheres, n_hits,
+                                n_titer, n_rounds, n_leafit, n_atomics};
+    for (int k = 0; k < 11; ++k) {
       unsigned long long s = v[k];
       for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
       if (lane == 0) atomicAdd(P.stats + k, s);
@@ -1598,11 +1104,6 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
       unsigned long long s = li[k];
       for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
       if (lane == 0) atomicAdd(P.stats + 27 + k, s);
-    }
-    {
-      unsigned long long s = n_uninode;
-      for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
-      if (lane == 0) atomicAdd(P.stats + 31, s);
     }
     // load balance: the slowest wave bounds the launch
     w_empty = w_empty ? w_empty : ~0ull;
@@ -1621,9 +1122,16 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
       ray_rounds_max = max(ray_rounds_max, (uint32_t)__shfl_xor((int)ray_rounds_max, off));
     }
     if (lane == 0) {
+      // wave clocks: every section of the wave's lifetime, traversal apart
+      const unsigned long long trav = s_clk[S_TRAV];
+      const unsigned long long hitshade = s_clk[S_HIT] + s_clk[S_NEE] + s_clk[S_BSDF];
+      const unsigned long long shade = hitshade + s_clk[S_FETCH] + s_clk[S_CAMERA] + s_clk[S_OTHER];
+      atomicAdd(P.stats + 11, shade);
+      atomicAdd(P.stats + 12, trav);
+      atomicMax(P.stats + 13, shade + trav);
+      atomicAdd(P.stats + 16, hitshade);
+      for (int k = 0; k < 4; ++k) atomicAdd(P.stats + 17 + k, s_clk[S_HIT + k]);
       unsigned long long w = wall_clock64() - w_start;
-      atomicMax(P.stats + 13, cyc_shade + cyc_hitshade + cyc_trav);
-      atomicAdd(P.stats + 16, cyc_hitshade);
       const unsigned long long w_end = wall_clock64();  // launch shape: first/last wave start and end
       atomicMin(P.stats + 21, w_start);
       atomicMax(P.stats + 22, w_start);
@@ -1633,7 +1141,6 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
         atomicMin(P.stats + 25, w_empty);
         atomicMax(P.stats + 26, w_empty);
       }
-      for (int k = 0; k < 4; ++k) atomicAdd(P.stats + 17 + k, cyc_sec[k]);
       atomicAdd(P.stats + 14, w);
       atomicMax(P.stats + 15, w);
       // per-wave trace (pt_get_wave_trace): start, first empty queue, end,
@@ -1656,17 +1163,13 @@ __global__ __launch_bounds__(PT_BLOCK * PT_WG_WAVES, PT_MIN_WAVES_PER_SIMD) void
 // Lanes that resolve one pixel: the pixel's groups are read as one coalesced
 // run (the per-pixel partials are n_groups * 12 B contiguous).
 __host__ __device__ __forceinline__ int resolve_team(int n_groups) {
-  if (PT_PIXEL_ACC) return 1;  // the render wrote each pixel's mean: a copy per lane
   int k = 1;
   while (k < n_groups && k < 64) k <<= 1;
   return k;
 }
 
 #if !PT_ENV_TU  // (pt_kernels_env.hip emits only the ENV render kernels)
-// PT_PIXEL_ACC: copies each traced pixel's mean from the slot framebuffer the
-// render wrote (and 0 for pixels outside the footprint) to the caller's
-// output, frame or packed layout.  Otherwise:
-// sums each pixel's sample groups in a fixed order (so the sum is a fixed
+// Sums each pixel's sample groups in a fixed order (so the sum is a fixed
 // function of the pixel, independent of scheduling and of the tile -> GPU
 // assignment) and writes the pixel's average, SampleBuffer-style
 // (pathtracer.cpp:577-581).  A team of k lanes (power of two) per pixel: lane
@@ -1683,18 +1186,14 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
   int2 xy = live ? tile_pixel(tile, tq & 1023u) : make_int2(-1, -1);
   float3 acc = f3(0, 0, 0);
   if (xy.x >= 0 && !culled(P, xy.x, xy.y)) {
-#if PT_PIXEL_ACC
-    acc = ld3(P.fb + 3 * ((size_t)xy.x + (size_t)xy.y * (size_t)P.W));
-#else
     const float* p = P.partial + 3 * ((size_t)xy.x + (size_t)xy.y * (size_t)P.W) * (size_t)P.n_groups;
-    for (int g = j; g < P.n_groups; g += k) acc = acc + ld3_stream(p + 3 * g);
-#endif
+    for (int g = j; g < P.n_groups; g += k) acc = acc + ld3(p + 3 * g);
   }
   // team lanes are consecutive, aligned, and all reach the shuffles
   for (int off = 1; off < k; off <<= 1)
     acc = acc + f3(__shfl_xor(acc.x, off), __shfl_xor(acc.y, off), __shfl_xor(acc.z, off));
   if (xy.x < 0 || j != 0) return;
-  const float inv_spp = PT_PIXEL_ACC ? 1.0f : (float)(1.0 / (double)P.spp);
+  const float inv_spp = (float)(1.0 / (double)P.spp);
   const size_t o = P.packed ? (size_t)(tq & ~1023u) + (size_t)((xy.y - tile.y) * 32 + (xy.x - tile.x))
                             : (size_t)xy.x + (size_t)xy.y * (size_t)P.W;
   store3(P.out + 3 * o, acc * inv_spp);
@@ -1732,8 +1231,8 @@ __global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __rest
 // ------------------------------------------------------------------ launchers
 template <bool ENV, bool GTAB>
 static void launch_render(const KParams* P, int waves, bool stats, bool ref_counts, hipStream_t s) {
-  const int grid = (waves + PT_WG_WAVES - 1) / PT_WG_WAVES;  // workgroups of PT_WG_WAVES waves
-  const dim3 blk(PT_BLOCK * PT_WG_WAVES);
+  const int grid = waves;  // one wave per workgroup
+  const dim3 blk(PT_BLOCK);
   if (ref_counts)
     hipLaunchKernelGGL((ptk::render_kernel<true, false, true, ENV, GTAB>), dim3(grid), blk, 0, s, *P);
   else if (P->dbg_pix >= 0)
@@ -1753,6 +1252,15 @@ extern "C" hipError_t ptk_launch_render_env(const KParams* P, int grid, bool sta
   if (gtab) launch_render<true, true>(P, grid, stats, ref_counts, s);
   else launch_render<true, false>(P, grid, stats, ref_counts, s);
   return hipGetLastError();
+}
+extern "C" hipError_t ptk_render_occupancy_env(int* waves_per_cu, bool gtab) {
+  int blocks = 0;
+  hipError_t e = gtab ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                            &blocks, ptk::render_kernel<false, false, false, true, true>, PT_BLOCK, 0)
+                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                            &blocks, ptk::render_kernel<false, false, false, true, false>, PT_BLOCK, 0);
+  *waves_per_cu = blocks;
+  return e;
 }
 #else
 extern "C" hipError_t ptk_launch_render_env(const KParams* P, int grid, bool stats, bool ref_counts, bool gtab,
@@ -1783,14 +1291,20 @@ extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prim
   return hipGetLastError();
 }
 
-// Resident render WAVES per CU (workgroups per CU x PT_WG_WAVES).
-extern "C" hipError_t ptk_render_occupancy(int* waves_per_cu, bool stats) {
+// Resident render waves (one-wave workgroups) per CU of the plain build of
+// each variant (env, gtab) or of the STATS build of the common variant.
+template <bool STATS, bool ENV, bool GTAB>
+static hipError_t occupancy(int* waves_per_cu) {
   int blocks = 0;
-  hipError_t e = stats ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                             &blocks, ptk::render_kernel<true, false, false, false, false>, PT_BLOCK * PT_WG_WAVES, 0)
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                             &blocks, ptk::render_kernel<false, false, false, false, false>, PT_BLOCK * PT_WG_WAVES, 0);
-  *waves_per_cu = blocks * PT_WG_WAVES;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, ptk::render_kernel<STATS, false, false, ENV, GTAB>,
+                                                              PT_BLOCK, 0);
+  *waves_per_cu = blocks;
   return e;
+}
+extern "C" hipError_t ptk_render_occupancy_env(int* waves_per_cu, bool gtab);
+extern "C" hipError_t ptk_render_occupancy(int* waves_per_cu, bool stats, bool env, bool gtab) {
+  if (env) return ptk_render_occupancy_env(waves_per_cu, gtab);
+  if (stats) return occupancy<true, false, false>(waves_per_cu);
+  return gtab ? occupancy<false, false, true>(waves_per_cu) : occupancy<false, false, false>(waves_per_cu);
 }
 #endif  // PT_ENV_TU

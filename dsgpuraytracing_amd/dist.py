@@ -137,15 +137,116 @@ def render_sharded(render_packed: Callable[[List[Tile], object], None], frame, t
     """Render this rank's share of `tiles` and assemble the frame on `dst`.
     `render_packed(mine, packed)` writes tile mine[i]'s pixels into packed[i]
     (PT_FLAG_PACKED layout).  Pass a TileExchange to reuse its buffers and
-    index maps across frames."""
+    index maps across frames.  A rank whose render raises still joins the
+    exchange, then every rank raises RankFailure naming it (the status check
+    comes after the gather, so no rank is left waiting in it)."""
     h, w = frame.shape[0], frame.shape[1]
     ex = exchange or TileExchange(tiles, w, h, rank, world, frame.device, dst=dst, group=group)
-    render_packed(ex.mine, ex.packed)
-    return ex.exchange(frame)
+    guard = StepGuard(group)
+    guard.run(render_packed, ex.mine, ex.packed)
+    ex.exchange(frame)
+    guard.check()
+    return frame
 
 
-def init_from_env(backend: str):
-    """torch.distributed init for `torchrun`-style env (RANK/WORLD_SIZE/MASTER_*)."""
+# Environment knobs of libptgpu.so that change pixel VALUES (not only speed):
+# the sample grouping fixes each pixel's float summation order, the render
+# tree decides ties between equidistant primitives.  Ranks that disagree on
+# them would assemble a frame that is not the 1-GPU frame bit for bit.
+VALUE_KNOBS = ("PT_SAMPLE_GROUP", "PT_WAVES_PER_CU", "PT_BVH_BUILD", "PT_COLLAPSE", "PT_LIB")
+DEFAULT_TIMEOUT_S = 120
+
+
+class RankFailure(RuntimeError):
+    """Raised on EVERY rank when any rank failed (`failed` = [(rank, message)]).
+
+    The reference exits the process on any device error
+    (cuda_src/setup.cu:139-143, 173-177), which in a multi-process job would
+    leave the other ranks blocked in the frame exchange until the process-group
+    timeout.  Here a failing rank keeps taking part in the collectives of the
+    frame it failed in, the ranks agree on a status at the next check point,
+    and all of them raise this with the failing rank's pt_last_error."""
+
+    def __init__(self, failed):
+        self.failed = list(failed)
+        super().__init__("; ".join(f"rank {r}: {m}" for r, m in self.failed))
+
+
+def _flag_device(group=None):
+    import torch
+    import torch.distributed as dist
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+
+
+def agree_status(err, group=None):
+    """Collective: every rank passes its error message (None = fine).  Raises
+    RankFailure on every rank if any rank failed; one int32 MAX all-reduce when
+    all are fine."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        if err:
+            raise RankFailure([(0, err)])
+        return
+    flag = torch.tensor([1 if err else 0], dtype=torch.int32, device=_flag_device(group))
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    if int(flag.item()):
+        msgs = [None] * dist.get_world_size(group)
+        dist.all_gather_object(msgs, err, group=group)
+        raise RankFailure([(r, m) for r, m in enumerate(msgs) if m])
+
+
+class StepGuard:
+    """Runs a rank's per-frame work without letting an exception leave the
+    collective schedule: the first failure is recorded (and the work skipped
+    from then on), the rank keeps joining the exchanges, and `check()` -- a
+    collective, called at the caller's synchronisation points -- turns any
+    rank's failure into RankFailure everywhere."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.err = None
+
+    def run(self, fn, *args, **kw):
+        if self.err is not None:
+            return None
+        try:
+            return fn(*args, **kw)
+        except Exception as e:  # recorded, surfaced on every rank by check()
+            self.err = f"{type(e).__name__}: {e}"
+            return None
+
+    def check(self):
+        agree_status(self.err, self.group)
+
+
+def check_value_knobs(extra=None, group=None):
+    """Collective: refuse to render a split frame when the ranks' value knobs
+    (VALUE_KNOBS, plus `extra`, e.g. the sample grouping a launch chose)
+    differ.  Returns this rank's fingerprint."""
+    import os
+
+    import torch.distributed as dist
+
+    mine = {k: os.environ.get(k) for k in VALUE_KNOBS}
+    if extra:
+        mine.update(extra)
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return mine
+    allv = [None] * dist.get_world_size(group)
+    dist.all_gather_object(allv, mine, group=group)
+    bad = [(r, f"value knobs {v} differ from rank 0's {allv[0]}") for r, v in enumerate(allv) if v != allv[0]]
+    if bad:
+        raise RankFailure(bad)
+    return mine
+
+
+def init_from_env(backend: str, timeout_s: float | None = None):
+    """torch.distributed init for `torchrun`-style env (RANK/WORLD_SIZE/MASTER_*).
+    A finite timeout (PT_DIST_TIMEOUT seconds, default 120) bounds how long a
+    rank waits in a collective for a peer that died."""
+    import datetime
     import os
 
     import torch.distributed as dist
@@ -153,11 +254,15 @@ def init_from_env(backend: str):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("PT_DIST_TIMEOUT", DEFAULT_TIMEOUT_S))
+    timeout = datetime.timedelta(seconds=timeout_s)
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":  # RCCL: bind the group to this rank's GPU (eager communicator init)
             import torch
-            dist.init_process_group(backend, device_id=torch.device("cuda", torch.cuda.current_device()))
+            dist.init_process_group(backend, timeout=timeout,
+                                    device_id=torch.device("cuda", torch.cuda.current_device()))
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
     return rank, world, local

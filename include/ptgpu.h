@@ -183,18 +183,22 @@ typedef struct pt_stats {
   int64_t wave_rounds;     /* wave-level shading/refill rounds */
   int64_t culled_samples;  /* samples of pixels outside the scene's screen footprint (radiance 0, not traced) */
   int64_t queue_atomics;   /* work-queue atomics issued */
-  int64_t shade_clocks;    /* shader clocks summed over waves: refill + shading phases */
+  int64_t shade_clocks;    /* shader clocks summed over waves: everything but traversal (shading, refill,
+                              camera rays, loop overhead); shade_clocks + trav_clocks = the waves' summed
+                              lifetimes.  All *_clocks come from the PT_FLAG_STATS build of the kernel,
+                              which runs slower than the plain build (counters and clock stamps) */
   int64_t trav_clocks;     /* shader clocks summed over waves: traversal phases */
   int64_t max_wave_clocks; /* shader clocks of the slowest wave */
   int64_t wave_wall_sum;   /* wave lifetimes summed, device wall-clock ticks */
   int64_t wave_wall_max;   /* longest wave lifetime, device wall-clock ticks */
   int64_t leaf_steps;      /* of wave_trav_steps: leaf (primitive) steps */
-  int64_t hitshade_clocks; /* of shade_clocks: hit records, NEE and bounces (the rest is refill) */
+  int64_t hitshade_clocks; /* of shade_clocks: hit records, NEE and bounces = section_clocks[0..2] */
   double resolve_ms;       /* device time of the sample-group resolve kernel */
   int32_t bvh_stack;       /* worst-case traversal stack entries of the uploaded BVH */
   int64_t bvh_nodes;       /* 4-wide BVH nodes uploaded */
-  int64_t section_clocks[4]; /* of shade_clocks: hit record, light sampling, BSDF sampling, queue fetch
-                                (the rest: camera rays) */
+  int64_t section_clocks[4]; /* of shade_clocks: hit record, light sampling, BSDF sampling + sample
+                                completion, queue fetch (the rest of shade_clocks: camera rays and loop
+                                overhead) */
   int64_t wave_span[5];    /* wall-clock ticks after the first wave started: last wave start,
                               first wave end, last wave end, first and last time a wave found
                               the work queue empty (launch ramp, queue drain and tail) */
@@ -202,8 +206,9 @@ typedef struct pt_stats {
   int64_t lane_iters[4];   /* traversal lane-iterations (64 per wave iteration) spent at the other
                               step kind, finished and waiting for the shading round, retired
                               (queue drained), stepping a leaf; node steps = node_visits */
-  int64_t uniform_node_steps; /* of wave_trav_steps: node steps whose lanes all stood at one node
-                                 (read through the scalar cache, PT_SCALAR_NODE builds) */
+  int64_t reserved0;       /* 0 (was uniform_node_steps of a removed experimental build) */
+  int64_t partial_bytes;   /* device bytes of the sample-group sums one render slot holds for the last
+                              launch's frame (W*H*ceil(spp/group_spp)*12; two slots pipeline renders) */
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */

@@ -28,19 +28,24 @@ def test_algorithmic_bytes_is_the_survey_cost_model():
 def test_roofline_views_are_fractions_and_bound_is_the_largest_measured():
     pm = bench.profile_summary("c3")
     assert pm is not None, "profiles/<round>/c3_summary.json missing"
-    kernel_ms, frame_ms = pm["avg_ms"], 1.6
+    frame_ms = 1.6
+    iso_ms = pm.get("isolated_avg_ms") or 2.0
     alg = 29.5e9
-    r = bench.roofline("c3", kernel_ms, alg, frame_ms)
+    r = bench.roofline("c3", frame_ms, alg, isolated_ms=iso_ms, pipelined_ms=2.3, lib_sha=pm.get("lib_sha256"))
     views = r["views"]
     for k in ("hbm", "l2", "valu", "algorithmic_cache_served"):
         assert k in views, k
         assert 0.0 < views[k]["frac"] <= 1.0, (k, views[k])
-        # per-frame fraction = the same counts over the frame interval
-        assert views[k]["frac_per_frame"] == pytest.approx(views[k]["frac"] * kernel_ms / frame_ms, rel=1e-3, abs=2e-4)  # both rounded to 4 places
+        # the headline fraction is per frame (counts over ms_per_step); the
+        # isolated one is the same counts over the kernel's own duration
+        assert views[k]["frac_isolated"] == pytest.approx(views[k]["frac"] * frame_ms / iso_ms, rel=1e-3, abs=2e-4)
     measured = {k: views[k]["frac"] for k in ("hbm", "l2", "valu")}
     assert r["bound"] == max(measured, key=measured.get)
     assert r["frac"] == views[r["bound"]]["frac"]
+    assert r["duration_ms"] == frame_ms  # no duration above ms_per_step
     assert r["traffic"] == pm["hbm_bytes_per_launch"]
+    assert r["pmc_stale"] is False
+    assert bench.roofline("c3", frame_ms, alg, lib_sha="0" * 64)["pmc_stale"] is True
     # HBM bytes from the PMC passes: 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction), in KB
     assert pm["hbm_bytes_per_launch"] == pytest.approx((2 * pm["fetch_size_kb"] + pm["write_size_kb"]) * 1024,
                                                        rel=1e-6)

@@ -83,3 +83,96 @@ def test_packed_index_layout():
     k = int(np.nonzero(dst == 65 * 40 + 33)[0][0])
     assert src[k] == 1024 + 1 * 32 + 1
     assert len(set(dst.tolist())) == len(dst)
+
+
+def _fail_worker(rank, world, port, out_dir, fail_rank):
+    """Renders a few frames through render_sharded; `fail_rank`'s renderer
+    raises in frame 1 (as a PtError from libptgpu.so would)."""
+    import sys
+    import time
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from dsgpuraytracing_amd.dist import RankFailure, init_from_env
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    init_from_env("gloo", timeout_s=20)
+    frame = torch.zeros((H, W, 3), dtype=torch.float32)
+    t0 = time.time()
+    code = 0
+    try:
+        for k in range(3):
+            def render(tiles, packed):
+                if rank == fail_rank and k == 1:
+                    raise RuntimeError("ptgpu error -2: hipErrorIllegalAddress (injected)")
+                packed.fill_(float(rank + 1))
+            render_sharded(render, frame, tile_fifo(W, H), rank, world)
+        msg = "no failure"
+    except RankFailure as e:
+        msg = f"RankFailure frame {k}: {e} failed={e.failed}"
+        code = 3
+    with open(os.path.join(out_dir, f"rank{rank}.txt"), "w") as f:
+        f.write(f"{time.time() - t0:.3f}\n{msg}\n")
+    dist.destroy_process_group()
+    sys.exit(code)
+
+
+@pytest.mark.parametrize("world,fail_rank", [(2, 1), (3, 0)])
+def test_failing_rank_stops_every_rank(tmp_path, world, fail_rank):
+    """SURVEY §5 / VERDICT r2: a per-rank failure surfaces as an error from the
+    exchange step on EVERY rank, promptly (not a process-group timeout), with
+    the failing rank's message; every process exits non-zero."""
+    import time
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    ps = [ctx.Process(target=_fail_worker, args=(r, world, port, str(tmp_path), fail_rank)) for r in range(world)]
+    t0 = time.time()
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(60)
+    assert all(not p.is_alive() for p in ps), "a rank is still blocked"
+    assert [p.exitcode for p in ps] == [3] * world
+    assert time.time() - t0 < 45
+    for r in range(world):
+        secs, msg = open(tmp_path / f"rank{r}.txt").read().splitlines()
+        assert msg.startswith("RankFailure frame 1:"), msg
+        assert f"rank {fail_rank}: RuntimeError: ptgpu error -2" in msg
+        assert float(secs) < 15  # seconds, far below the 20 s group timeout
+
+
+def _knob_worker(rank, world, port, out_dir):
+    import sys
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from dsgpuraytracing_amd.dist import RankFailure, check_value_knobs
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if rank == 1:
+        os.environ["PT_SAMPLE_GROUP"] = "8"
+    else:
+        os.environ.pop("PT_SAMPLE_GROUP", None)
+    code = 0
+    try:
+        check_value_knobs({"group_spp": 4})
+        msg = "ok"
+    except RankFailure as e:
+        msg = str(e)
+        code = 3
+    with open(os.path.join(out_dir, f"knob{rank}.txt"), "w") as f:
+        f.write(msg)
+    dist.destroy_process_group()
+    sys.exit(code)
+
+
+def test_value_knobs_must_agree(tmp_path):
+    """PT_SAMPLE_GROUP changes each pixel's float summation order: ranks that
+    differ would break the bit-identity of the assembled frame, so the split
+    refuses to start."""
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    ps = [ctx.Process(target=_knob_worker, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(60)
+    assert [p.exitcode for p in ps] == [3, 3]
+    for r in range(2):
+        assert "PT_SAMPLE_GROUP" in open(tmp_path / f"knob{r}.txt").read()

@@ -11,10 +11,14 @@ as well: finite and non-negative radiance, determinism, and that a tile split
 
 The sampled tiles are chosen FROM THE ORACLE, never by hand: a 1-spp
 restatement render of the whole frame (C3: 0.15 s, C5: 1 s on 8 threads) gives
-every tile's coverage, the candidates are the full 32x32 tiles in which every
-pixel saw radiance, and k of them are taken at evenly spaced ranks.  The
-precondition (every chosen reference tile is lit) is asserted before the GPU
-render.
+every tile's coverage.  Two kinds are taken, each at evenly spaced ranks of
+its candidates: LIT tiles (every pixel saw radiance) and MIXED tiles (both
+black and lit pixels: the silhouettes of the scene box and of the geometry,
+where fp32-vs-fp64 decisions, the integer-ulp origin offsets and the screen
+footprint's 1-px margin act).  The precondition (every chosen reference tile
+is lit somewhere) is asserted before the GPU render.  The screen-footprint
+cull of the headline frame is also checked against tracing every sample, at
+full size (C3 at 64 spp, C4 at a reduced spp).
 
 Tolerance (SURVEY.md §8(c) criterion 2), for every config: >= 99.5% of
 pixels within 1e-3 relative and the (sampled-tile) image mean within 0.1%.
@@ -70,17 +74,26 @@ def near_exact(a, b):
     return float((diff <= 1e-3 * scale).mean())
 
 
-def lit_tiles(restate, dump, w, h, k, seed=1):
-    """k full 32x32 tiles, every pixel of which receives radiance in a 1-spp
-    restatement render, at evenly spaced ranks of the tile FIFO order."""
+def oracle_tiles(restate, dump, w, h, k, kind="lit", seed=1):
+    """k 32x32 tiles of the frame at evenly spaced ranks of the tile FIFO
+    order, chosen from a 1-spp restatement render: kind "lit" = full tiles
+    every pixel of which receives radiance; "mixed" = tiles (ragged edge
+    tiles included) holding both black and lit pixels."""
     one, _ = restate.render(dump, w, h, 1, 4, 1, seed, rng_mode=1, threads=8)
     cand = []
     for x, y, _, _ in tile_fifo(w, h):
-        if x + 32 <= w and y + 32 <= h and (one[y:y + 32, x:x + 32].max(axis=2) > 0).all():
+        lit = one[y:y + 32, x:x + 32].max(axis=2) > 0
+        if kind == "lit" and x + 32 <= w and y + 32 <= h and lit.all():
             cand.append((x, y))
-    assert len(cand) >= k, f"only {len(cand)} fully lit tiles"
+        elif kind == "mixed" and lit.any() and not lit.all():
+            cand.append((x, y))
+    assert len(cand) >= k, f"only {len(cand)} {kind} tiles"
     pick = np.linspace(0, len(cand) - 1, k).round().astype(int)
     return [cand[i] for i in pick]
+
+
+def lit_tiles(restate, dump, w, h, k, seed=1):
+    return oracle_tiles(restate, dump, w, h, k, "lit", seed)
 
 
 @pytest.mark.parametrize("name", ["c1", "c2"])
@@ -101,20 +114,23 @@ def test_fullframe_near_exact_vs_oracle(tmp_path, restate, name):
     assert rel_mean <= 1e-3, rel_mean
 
 
-# (name, tiles sampled, per-pixel near-exact fraction: SURVEY's 99.5% throughout)
-@pytest.mark.parametrize("name,k,min_close", [
-    ("c3", 8, 0.995),
-    ("c4", 6, 0.995),
-    ("c5", 4, 0.995),
+# (name, lit tiles, mixed tiles, per-pixel near-exact fraction: SURVEY's 99.5% throughout).
+# C5 has an environment light: no pixel is black, so it has no mixed tiles
+# (its silhouettes are inside the lit tiles).
+@pytest.mark.parametrize("name,k,k_mixed,min_close", [
+    ("c3", 8, 6, 0.995),
+    ("c4", 6, 6, 0.995),
+    ("c5", 4, 0, 0.995),
 ])
-def test_fullsize_sampled_tiles_match_oracle(tmp_path, restate, name, k, min_close):
+def test_fullsize_sampled_tiles_match_oracle(tmp_path, restate, name, k, k_mixed, min_close):
     dae, envmap, w, h, spp = _workload(name)
     dump = str(tmp_path / f"{name}.ptd")
     scene_loader.dump_dae(dae, w, h, dump, envmap=envmap)
     tiles = lit_tiles(restate, dump, w, h, k)
+    mixed = oracle_tiles(restate, dump, w, h, k_mixed, "mixed") if k_mixed else []
     tw = (w + 31) // 32
     refs = []
-    for x, y in tiles:   # the oracle first: its precondition is checked before the GPU runs
+    for x, y in tiles + mixed:   # the oracle first: its precondition is checked before the GPU runs
         t = (y // 32) * tw + x // 32
         ref, _ = restate.render(dump, w, h, spp, 4, 1, 1, rng_mode=1, threads=8, tile_begin=t, tile_end=t + 1)
         b = ref[y:y + 32, x:x + 32]
@@ -124,15 +140,57 @@ def test_fullsize_sampled_tiles_match_oracle(tmp_path, restate, name, k, min_clo
     img = np.zeros((h, w, 3), np.float32)
     dev.render_tiles(tile_fifo(w, h), img)
     assert np.isfinite(img).all() and (img >= 0).all()
-    got = np.stack([img[y:y + 32, x:x + 32] for x, y in tiles])
-    ref = np.stack(refs)
-    closes = [near_exact(a, b) for a, b in zip(got, ref)]
-    close = near_exact(got, ref)
-    rel_mean = abs(got.mean() - ref.mean()) / ref.mean()
-    print(f"{name}: tiles {tiles}\n  per-tile {np.round(closes, 4).tolist()}\n"
-          f"  {close * 100:.3f}% pixels within 1e-3, sampled-tile mean rel diff {rel_mean:.2e}")
-    assert close >= min_close, closes
-    assert rel_mean <= 1e-3, rel_mean
+    for kind, sel, rf in (("lit", tiles, refs[:len(tiles)]), ("mixed", mixed, refs[len(tiles):])):
+        if not sel:
+            continue
+        got = [img[y:y + 32, x:x + 32] for x, y in sel]
+        closes = [near_exact(a, b) for a, b in zip(got, rf)]
+        gflat = np.concatenate([a.reshape(-1, 3) for a in got])
+        rflat = np.concatenate([b.reshape(-1, 3) for b in rf])
+        close = near_exact(gflat, rflat)
+        rel_mean = abs(gflat.mean() - rflat.mean()) / rflat.mean()
+        # the black pixels of mixed tiles are black on both sides (exact)
+        black = rflat.max(axis=1) == 0
+        print(f"{name} {kind}: tiles {sel}\n  per-tile {np.round(closes, 4).tolist()}\n"
+              f"  {close * 100:.3f}% pixels within 1e-3, sampled-tile mean rel diff {rel_mean:.2e}, "
+              f"{int(black.sum())} black reference pixels")
+        assert close >= min_close, (kind, closes)
+        assert rel_mean <= 1e-3, (kind, rel_mean)
+        assert (gflat[black] == 0).mean() >= min_close, kind
+
+
+@pytest.mark.parametrize("name,spp", [("c3", 64), ("c4", 16)])
+def test_footprint_cull_exact_at_full_size(monkeypatch, name, spp):
+    """The headline's default camera leaves most of the frame outside the
+    scene box's screen footprint (pt_api.cpp screen_footprint): those samples
+    are not traced (camera.cpp:113-129 rays that miss the root box see
+    nothing, pathtracer.cpp:421-426).  The culled frame must equal the frame
+    traced sample by sample (PT_NO_FOOTPRINT_CULL=1) bit for bit, edges and
+    silhouettes included; C4 at a reduced spp (the cull does not depend on it)."""
+    dae, envmap, w, h, _ = _workload(name)
+    dev = _device(dae, envmap, w, h, spp, seed=5)
+    monkeypatch.delenv("PT_NO_FOOTPRINT_CULL", raising=False)
+    culled = np.zeros((h, w, 3), np.float32)
+    dev.render_tiles(tile_fifo(w, h), culled, stats=True)
+    st = dev.stats()
+    monkeypatch.setenv("PT_NO_FOOTPRINT_CULL", "1")
+    traced = np.zeros_like(culled)
+    dev.render_tiles(tile_fifo(w, h), traced, stats=True)
+    st2 = dev.stats()
+    print(f"{name}: culled {st['culled_samples']} of {w * h * spp} samples; camera rays {st['camera_rays']} "
+          f"vs {st2['camera_rays']} traced")
+    assert st["culled_samples"] > 0 and st2["culled_samples"] == 0
+    assert st["camera_rays"] + st["culled_samples"] == st2["camera_rays"]
+    assert np.array_equal(culled, traced)
+    # ... and the same for the plain (counter-free) build
+    plain_traced = np.zeros_like(culled)
+    dev.render_tiles(tile_fifo(w, h), plain_traced)
+    monkeypatch.delenv("PT_NO_FOOTPRINT_CULL")
+    plain = np.zeros_like(culled)
+    dev.render_tiles(tile_fifo(w, h), plain)
+    assert np.array_equal(plain, plain_traced)
+    assert np.array_equal(plain, culled)
+    assert culled.mean() > 0
 
 
 def test_c3_fullsize_deterministic_and_split():

@@ -278,6 +278,80 @@ def test_hip_oversize_leaf_split_matches_reference_bvh(monkeypatch, name):
     assert frac >= 0.995 and rel_mean <= 1e-3, (frac, rel_mean)
 
 
+def _tiny_scene(name, which):
+    """The scene's primitives `which` only (in that order) under a one-leaf
+    BVH: the smallest trees the upload must handle (a root that is
+    a single leaf used to loop forever in the BVH4 collapse)."""
+    d = dict(ptdump.read(golden(f"{name}.scene.ptd")))
+    which = np.asarray(which)
+    d["prim_type"] = np.ascontiguousarray(d["prim_type"][which])
+    d["prim_bsdf"] = np.ascontiguousarray(d["prim_bsdf"][which])
+    if "prim_orig" in d:
+        d["prim_orig"] = np.arange(len(which), dtype=np.int32)
+    g = d["prim_geom"].reshape(-1, 9)[which]
+    d["prim_geom"] = np.ascontiguousarray(g.reshape(-1))
+    d["prim_norm"] = np.ascontiguousarray(d["prim_norm"].reshape(-1, 9)[which].reshape(-1))
+    lo, hi = np.full(3, np.inf), np.full(3, -np.inf)
+    for t, q in zip(d["prim_type"], g):
+        if t == native.PRIM_TRIANGLE:
+            v = q.reshape(3, 3)
+            lo, hi = np.minimum(lo, v.min(0)), np.maximum(hi, v.max(0))
+        else:
+            lo, hi = np.minimum(lo, q[:3] - abs(q[3])), np.maximum(hi, q[:3] + abs(q[3]))
+    d["node_bb"] = np.concatenate([lo, hi]).astype(np.float64)
+    d["node_info"] = np.array([0, len(which), -1, -1], dtype=np.int64)
+    return d
+
+
+@pytest.mark.parametrize("build", ["sah", "ref", "lbvh"])
+@pytest.mark.parametrize("name,kind", [("c1_default_64x64", "one triangle"), ("CBspheres_64x64", "one sphere"),
+                                       ("CBspheres_64x64", "four primitives")])
+def test_hip_tiny_scenes_upload_and_match_restatement(monkeypatch, restate, tmp_path, build, name, kind):
+    """1-primitive and 4-primitive scenes (one-leaf trees on every build path)
+    upload, answer ray queries as the restatement does, and render near-exactly."""
+    from dsgpuraytracing_amd.pathtracer import Device
+    base = ptdump.read(golden(f"{name}.scene.ptd"))
+    types = np.asarray(base["prim_type"])
+    if kind == "one triangle":
+        which = [int(np.nonzero(types == native.PRIM_TRIANGLE)[0][0])]
+    elif kind == "one sphere":
+        which = [int(np.nonzero(types == native.PRIM_SPHERE)[0][0])]
+    else:
+        which = [int(np.nonzero(types == native.PRIM_SPHERE)[0][0])] + \
+                [int(i) for i in np.nonzero(types == native.PRIM_TRIANGLE)[0][:3]]
+    d = _tiny_scene(name, which)
+    path = str(tmp_path / "tiny.ptd")
+    ptdump.write(path, d)
+    if build == "ref":
+        monkeypatch.setenv("PT_BVH_BUILD", "ref")
+    else:
+        monkeypatch.delenv("PT_BVH_BUILD", raising=False)
+    sc = Scene(native.SceneArrays(d))
+    dev = Device(0)
+    dev.upload_scene(sc, gpu_bvh=build == "lbvh")
+    rng = np.random.default_rng(11)
+    m = 2048
+    c = (d["node_bb"][:3] + d["node_bb"][3:]) / 2
+    o = c + rng.normal(size=(m, 3)) * 3.0
+    dr = c + rng.normal(size=(m, 3)) * 0.3 - o
+    dr /= np.linalg.norm(dr, axis=1, keepdims=True)
+    maxt = rng.uniform(0.5, 6.0, m)
+    hit, t, prim, anyh = dev.intersect(o, dr, maxt)
+    rh, rt, rp, _, ra = restate.intersect(path, o.reshape(-1), dr.reshape(-1), maxt)
+    assert hit.sum() > 10, kind
+    assert (hit == rh).mean() >= 0.995 and (anyh == ra).mean() >= 0.995
+    both = (hit == 1) & (rh == 1)
+    assert (prim[both] == rp[both]).mean() >= 0.99
+    dev.set_camera(sc.camera)
+    dev.set_params(32, 32, 4, 4, 1, 3)
+    img = np.zeros((32, 32, 3), np.float32)
+    dev.render_tiles([(0, 0, 32, 32)], img)
+    ref, _ = restate.render(path, 32, 32, 4, 4, 1, 3, rng_mode=1, threads=2)
+    frac, rel_mean = near_exact_report(img, ref)
+    assert np.isfinite(img).all()
+    assert frac >= 0.995, (kind, build, frac)
+
+
 def _deep_chain_scene(n=96):
     """n parallel squares-as-triangles stacked along z, under a CHAIN BVH
     (node k: left = leaf {prim k}, right = node k+1).  Rays travelling -z

@@ -1,17 +1,23 @@
 """Summarise a rocprofv3 profiling session of bench.py into profiles/<round>/.
 
 Reads the passes written by tools/profile_session.sh under gpurun_out/prof/:
-  kt/     --kernel-trace --stats      (per-kernel average duration)
+  kt/     --kernel-trace --stats      (per-kernel average duration, render pipeline on:
+                                       consecutive launches overlap)
+  kt_iso/ --kernel-trace --stats      with PT_PIPELINE=0 (every launch alone: the kernel's
+                                       own duration, bench.py's isolated_kernel_ms)
   fetch/  --pmc FETCH_SIZE            (KB; doubled per MI355X_MICROARCH.md §HBM)
   write/  --pmc WRITE_SIZE            (KB)
   sq/     --pmc SQ_*                  (quad-cycle units for *_CYCLES / WAIT / ACTIVE)
   tcc/    --pmc TCC_HIT_sum TCC_MISS_sum
 and writes <out>/<workload>_kernel_stats.csv and <out>/<workload>_summary.json
-(bench.py's roofline reads the newest round's summary of its workload).
-Usage: python tools/profile_summary.py <workload> <out_dir> [prof_dir]
+(bench.py's roofline reads the newest round's summary of its workload), stamped
+with the sha256 of the libptgpu.so the passes ran (bench.py reports pmc_stale
+when it loads a different one).  The PMC passes run with PT_PIPELINE=0.
+Usage: python tools/profile_summary.py <workload> <out_dir> [prof_dir] [lib]
 """
 import collections
 import csv
+import hashlib
 import json
 import os
 import shutil
@@ -37,12 +43,19 @@ def main():
     workload, out = sys.argv[1], sys.argv[2]
     KERNEL = KERNELS.get(workload, KERNEL)
     prof = sys.argv[3] if len(sys.argv) > 3 else "gpurun_out/prof"
+    lib = sys.argv[4] if len(sys.argv) > 4 else os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "dsgpuraytracing_amd", "libptgpu.so")
     os.makedirs(out, exist_ok=True)
     ks = os.path.join(prof, "kt", "kt_kernel_stats.csv")
     shutil.copy(ks, os.path.join(out, f"{workload}_kernel_stats.csv"))
     stats = {r["Name"]: r for r in csv.DictReader(open(ks))}
     render = next(v for k, v in stats.items() if KERNEL in k)
     resolve = next((v for k, v in stats.items() if "resolve_kernel" in k), None)
+    iso = None
+    ksi = os.path.join(prof, "kt_iso", "kt_iso_kernel_stats.csv")
+    if os.path.exists(ksi):
+        shutil.copy(ksi, os.path.join(out, f"{workload}_kernel_stats_isolated.csv"))
+        iso = next(v for k, v in {r["Name"]: r for r in csv.DictReader(open(ksi))}.items() if KERNEL in k)
     fetch = _pmc(os.path.join(prof, "fetch", "fetch_counter_collection.csv"))
     write = _pmc(os.path.join(prof, "write", "write_counter_collection.csv"))
     sq = _pmc(os.path.join(prof, "sq", "sq_counter_collection.csv"))
@@ -59,10 +72,14 @@ def main():
     s = {
         "workload": workload,
         "kernel": KERNEL,
+        "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
         "calls": int(render["Calls"]),
         "avg_ms": avg_ns / 1e6,
+        "isolated_avg_ms": float(iso["AverageNs"]) / 1e6 if iso else None,
         "resolve_avg_ms": float(resolve["AverageNs"]) / 1e6 if resolve else None,
     }
+    if iso:  # utilisation over the kernel's own duration, not an overlapped span
+        avg_ns = float(iso["AverageNs"])
     if "FETCH_SIZE" in fetch and "WRITE_SIZE" in write:
         s["fetch_size_kb"] = fetch["FETCH_SIZE"]
         s["write_size_kb"] = write["WRITE_SIZE"]
