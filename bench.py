@@ -564,7 +564,15 @@ def companions(dev0, local, stream, frames):
       * c5_single_gpu: BASELINE C5 (glass/mirror proxy + environment light)
         on this one GPU;
       * c3_lbvh: the headline workload over the GPU-built LBVH
-        (pt_upload_scene_lbvh) instead of the host SAH tree."""
+        (pt_upload_scene_lbvh) instead of the host SAH tree;
+      * c3_per_tile / c3_per_tile_sync: the headline frame driven through the
+        reference's literal seam -- 8 worker threads calling raytrace_tile
+        once per 32x32 tile (1,024 calls, pathtracer.cpp:585-621) through one
+        context, as INTEGRATION.md's adapter does -- asynchronously
+        (pt_tile_submit: tiles batched into launches, completed into the
+        host sampleBuffer + toColor'd frameBuffer on stream callbacks) and with
+        one synchronous pt_render_tiles launch per tile.  Host output
+        included (PCIe), so these are never `value`."""
     import torch
 
     from dsgpuraytracing_amd.pathtracer import Device, Scene, tile_fifo
@@ -602,7 +610,33 @@ def companions(dev0, local, stream, frames):
             "bvh": "gpu-lbvh" if lbvh else "own binned SAH (host)"}
         dev.close()
         del fr
+    res.update(per_tile_companions(local))
     return res
+
+
+def per_tile_companions(local, threads=8):
+    from dsgpuraytracing_amd.pathtracer import PathTracer, Scene
+    wl = WORKLOADS["c3"]
+    dae, envmap, cam = workload_scene(wl)
+    sc = Scene.from_dae(dae, wl["w"], wl["h"], cam_info=cam, envmap=envmap)
+    out = {}
+    for name, asynchronous, frames in (("c3_per_tile", True, 3), ("c3_per_tile_sync", False, 1)):
+        pt = PathTracer(ns_aa=wl["spp"], max_ray_depth=DEPTH, ns_area_light=NSL, seed=SEED, device=local)
+        pt.set_frame_size(wl["w"], wl["h"])
+        pt.set_camera(sc.camera)
+        pt.set_scene(sc)
+        pt.render_tile_workers(num_threads=threads, asynchronous=asynchronous)  # warm-up frame
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            pt.render_tile_workers(num_threads=threads, asynchronous=asynchronous)
+        el = (time.perf_counter() - t0) / frames
+        out[name] = {"workload": wl["desc"] + f", {threads} worker threads x 1,024 raytrace_tile calls "
+                                              f"({'pt_tile_submit, batched' if asynchronous else 'pt_render_tiles, one launch each'})",
+                     "value": round(wl["w"] * wl["h"] * wl["spp"] / el / 1e6, 1), "unit": "Mrays/s",
+                     "ms_per_frame": round(el * 1e3, 3), "frames": frames, "threads": threads,
+                     "host_output": "sampleBuffer + toColor frameBuffer (PCIe-inclusive)"}
+        pt._device().close()
+    return out
 
 
 if __name__ == "__main__":

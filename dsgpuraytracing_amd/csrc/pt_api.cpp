@@ -177,10 +177,31 @@ struct pt_ctx {
   DevBuf<int4> blocks[kSlots];           // footprint-clipped 8x8 pixel blocks of the tiles
   std::vector<int4> blocks_host[kSlots];
   DevBuf<float> partial[kSlots];   // per-slot sample-group sums
+  DevBuf<unsigned long long> accum[kSlots];  // PT_FIXED_ACC: per-slot exact pixel sums (kept zeroed)
   DevBuf<int> spill[kSlots];       // traversal stack entries beyond PT_STACK
   DevBuf<uint32_t> counter[kSlots];
   int64_t culled_px = 0;         // pixels of the last launch outside the footprint
   DevBuf<float> frame;  // device framebuffer for host-output renders
+  // Asynchronous one-tile seam (pt_tile_submit / pt_tile_finish): submitted
+  // tiles wait in `tq` until a batch of `tile_batch` is full, then render as
+  // ONE launch into `frame`, are copied to the pinned `stage` and completed
+  // (copied into the caller's sampleBuffer, toColor'd into its frameBuffer)
+  // by a host function on the context stream.
+  struct TileJob {
+    int4 t;
+    float* hdr;
+    uint32_t* rgba;
+  };
+  struct TileBatch {
+    std::vector<TileJob> jobs;
+    const float* stage;
+    int W, H;
+  };
+  std::vector<TileJob> tq;
+  std::vector<TileBatch*> tile_inflight;
+  int tile_batch = 64;
+  float* stage = nullptr;
+  size_t stage_n = 0;
   DevBuf<int> q_spill;  // ray-query stack spill
   DevBuf<unsigned long long> stats;
   DevBuf<float> q_f;    // ray-query scratch
@@ -233,6 +254,10 @@ int pt_create(int device, pt_ctx** out) {
   for (int v = 0; v < 4; ++v) HIPCHK(ptk_render_occupancy(&c->bpc_variant[v], false, (v & 2) != 0, (v & 1) != 0));
   c->grid_plain = std::max(8, c->bpc_plain) * c->n_cu;
   c->grid_stats = std::max(8, c->bpc_stats) * c->n_cu;
+  if (const char* tb = std::getenv("PT_TILE_BATCH")) {  // tuning knob: tiles per asynchronous launch
+    int v = std::atoi(tb);
+    if (v >= 1) c->tile_batch = v;
+  }
   // counters + one trace record per wave of the largest stats grid
   HIPCHK(c->stats.reserve(PT_STATS_SLOTS + (size_t)PT_WAVE_TRACE * std::max(c->grid_stats, 64 * c->n_cu)));
   *out = c;
@@ -261,10 +286,13 @@ int pt_destroy(pt_ctx* c) {
     c->blocks[k].release();
     c->spill[k].release();
     c->partial[k].release();
+    c->accum[k].release();
     c->counter[k].release();
     if (c->ev_free[k]) (void)hipEventDestroy(c->ev_free[k]);
     if (c->rstream[k]) (void)hipStreamDestroy(c->rstream[k]);
   }
+  for (auto* b : c->tile_inflight) delete b;
+  if (c->stage) (void)hipHostFree(c->stage);
   c->q_spill.release();
   c->frame.release();
   c->stats.release();
@@ -566,8 +594,11 @@ static int build_gpu_bvh(pt_ctx* c, const pt_scene* s) {
   return PT_OK;
 }
 
+static int tile_launch(pt_ctx* c);
+
 static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
   if (!c || !s) return fail(PT_E_INVALID, "pt_upload_scene: NULL argument");
+  if (int rc = tile_launch(c)) return rc;  // queued tiles render with the state they were submitted under
   if (s->n_prims <= 0 || !s->prim_type || !s->prim_bsdf || !s->prim_geom || !s->prim_norm ||
       (!gpu_bvh && (s->n_nodes <= 0 || !s->nodes)))
     return fail(PT_E_INVALID, "pt_upload_scene: empty scene");
@@ -767,12 +798,14 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
   return PT_OK;
 }
 
+
 int pt_upload_scene(pt_ctx* c, const pt_scene* s) { return upload_impl(c, s, false); }
 
 int pt_upload_scene_lbvh(pt_ctx* c, const pt_scene* s) { return upload_impl(c, s, true); }
 
 int pt_set_camera(pt_ctx* c, const pt_camera* cam) {
   if (!c || !cam) return fail(PT_E_INVALID, "pt_set_camera: NULL argument");
+  if (int rc = tile_launch(c)) return rc;
   if (!(cam->screen_dist > 0) || !(cam->screen_w > 0) || !(cam->screen_h > 0))
     return fail(PT_E_INVALID, "pt_set_camera: non-positive screen size/distance");
   c->cam = *cam;
@@ -782,6 +815,7 @@ int pt_set_camera(pt_ctx* c, const pt_camera* cam) {
 
 int pt_set_params(pt_ctx* c, const pt_params* p) {
   if (!c || !p) return fail(PT_E_INVALID, "pt_set_params: NULL argument");
+  if (int rc = tile_launch(c)) return rc;
   if (p->width <= 0 || p->height <= 0 || p->spp <= 0 || p->max_depth < 0 || p->ns_area_light <= 0)
     return fail(PT_E_INVALID, "pt_set_params: width/height/spp/ns_area_light must be positive, max_depth >= 0");
   if (p->max_depth > 254 || p->ns_area_light > 255)  // packed in 8 bits each in the kernel's path state
@@ -1021,9 +1055,18 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   const int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
   if (slots + want * PT_CHUNK_MAX >= (int64_t)UINT32_MAX || npx * P.n_groups >= (int64_t)UINT32_MAX)
     return fail(PT_E_INVALID, "frame too large for one launch");
+#if PT_FIXED_ACC
+  if (c->accum[slot].n < (size_t)npx * 3) {  // zeroed once; every resolve leaves its pixels zeroed
+    HIPCHK(c->accum[slot].reserve((size_t)npx * 3));
+    HIPCHK(hipMemsetAsync(c->accum[slot].p, 0, (size_t)npx * 3 * sizeof(unsigned long long), rs));
+  }
+  P.accum = c->accum[slot].p;
+  c->last.partial_bytes = (int64_t)npx * 24;
+#else
   HIPCHK(c->partial[slot].reserve((size_t)(npx * P.n_groups) * 3));
   P.partial = c->partial[slot].p;
   c->last.partial_bytes = (int64_t)npx * P.n_groups * 12;
+#endif
   auto log2_exact = [](int v) {  // log2(v) for a power of two, else -1
     int k = 0;
     while ((1 << k) < v && k < 30) ++k;
@@ -1142,6 +1185,7 @@ static bool tiles_disjoint(const std::vector<int4>& tl, size_t W, size_t H) {
 int pt_render_tiles(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, float* hdr_out_host, uint32_t flags) {
   int rc = check_ready(c);
   if (rc) return rc;
+  if ((rc = tile_launch(c))) return rc;  // earlier asynchronous tiles first (call order)
   if (n_tiles < 0 || (n_tiles > 0 && (!tiles || !hdr_out_host))) return fail(PT_E_INVALID, "pt_render_tiles: bad args");
   if (flags & PT_FLAG_PACKED) return fail(PT_E_INVALID, "pt_render_tiles: PT_FLAG_PACKED is for pt_render_tiles_device");
   HIPCHK(hipSetDevice(c->device));
@@ -1171,6 +1215,7 @@ int pt_render_tiles_device(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, flo
                            uint32_t flags) {
   int rc = check_ready(c);
   if (rc) return rc;
+  if ((rc = tile_launch(c))) return rc;
   if (n_tiles < 0 || (n_tiles > 0 && (!tiles || !hdr_out_dev)))
     return fail(PT_E_INVALID, "pt_render_tiles_device: bad args");
   HIPCHK(hipSetDevice(c->device));
@@ -1187,6 +1232,73 @@ int pt_render_tiles_device(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, flo
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   if ((rc = launch(c, tl, hdr_out_dev, s, flags))) return rc;
   return finish_stats(c, s, flags, false);
+}
+
+// ---- asynchronous one-tile seam
+// Completion of one batch, on the context stream after its copy to `stage`
+// (a HIP host function: no HIP calls in here).  The tile's pixels go into
+// the caller's sampleBuffer and, as PathTracer::raytrace_tile does at its end
+// (pathtracer.cpp:610), through toColor into its frameBuffer.
+static void tile_done(void* arg) {
+  auto* b = static_cast<pt_ctx::TileBatch*>(arg);
+  for (const pt_ctx::TileJob& j : b->jobs) {
+    for (int y = j.t.y; y < j.t.y + j.t.w; ++y) {
+      const size_t off = ((size_t)y * (size_t)b->W + (size_t)j.t.x) * 3;
+      std::memcpy(j.hdr + off, b->stage + off, (size_t)j.t.z * 3 * sizeof(float));
+    }
+    if (j.rgba) (void)pt_to_color(j.hdr, b->W, b->H, j.t.x, j.t.y, j.t.x + j.t.z, j.t.y + j.t.w, j.rgba);
+  }
+}
+
+// Renders the queued tiles as one launch (nothing queued: nothing to do).
+static int tile_launch(pt_ctx* c) {
+  if (!c || c->tq.empty()) return PT_OK;
+  std::vector<pt_ctx::TileJob> jobs;
+  jobs.swap(c->tq);
+  HIPCHK(hipSetDevice(c->device));
+  const size_t W = (size_t)c->params.width, H = (size_t)c->params.height;
+  std::vector<int4> tl;
+  for (const auto& j : jobs) tl.push_back(j.t);
+  HIPCHK(c->frame.reserve(W * H * 3));
+  if (c->stage_n < W * H * 3) {
+    HIPCHK(hipStreamSynchronize(c->stream));  // earlier batches still copy into the old stage
+    if (c->stage) HIPCHK(hipHostFree(c->stage));
+    c->stage = nullptr;
+    c->stage_n = 0;
+    HIPCHK(hipHostMalloc((void**)&c->stage, W * H * 3 * sizeof(float), hipHostMallocDefault));
+    c->stage_n = W * H * 3;
+  }
+  if (int rc = launch(c, tl, c->frame.p, c->stream, 0)) return rc;
+  for (const int4& t : tl) {
+    const size_t off = ((size_t)t.y * W + (size_t)t.x) * 3;
+    HIPCHK(hipMemcpy2DAsync(c->stage + off, W * 3 * sizeof(float), c->frame.p + off, W * 3 * sizeof(float),
+                            (size_t)t.z * 3 * sizeof(float), (size_t)t.w, hipMemcpyDeviceToHost, c->stream));
+  }
+  auto* b = new pt_ctx::TileBatch{std::move(jobs), c->stage, (int)W, (int)H};
+  c->tile_inflight.push_back(b);
+  HIPCHK(hipLaunchHostFunc(c->stream, tile_done, b));
+  return finish_stats(c, c->stream, 0, false);
+}
+
+int pt_tile_submit(pt_ctx* c, const pt_tile* tile, float* hdr_out_host, uint32_t* rgba_out_host) {
+  int rc = check_ready(c);
+  if (rc) return rc;
+  if (!tile || !hdr_out_host) return fail(PT_E_INVALID, "pt_tile_submit: NULL tile or output");
+  std::vector<int4> tl;
+  if ((rc = build_tiles(c, tile, 1, tl))) return rc;  // clamped to the frame, <= 32 x 32 pieces
+  for (const int4& t : tl) c->tq.push_back(pt_ctx::TileJob{t, hdr_out_host, rgba_out_host});
+  if ((int)c->tq.size() >= c->tile_batch) return tile_launch(c);
+  return PT_OK;
+}
+
+int pt_tile_finish(pt_ctx* c) {
+  if (!c) return fail(PT_E_INVALID, "NULL context");
+  if (int rc = tile_launch(c)) return rc;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));  // every batch copied and completed
+  for (auto* b : c->tile_inflight) delete b;
+  c->tile_inflight.clear();
+  return PT_OK;
 }
 
 int pt_intersect(pt_ctx* c, int64_t n, const double* o, const double* d, const double* max_t, int32_t* hit, float* t,

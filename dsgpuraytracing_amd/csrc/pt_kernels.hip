@@ -560,6 +560,25 @@ __device__ __forceinline__ void env_sample(const KParams& P, float r1, float r2,
   wi = f3(-st * sp, ct, st * cp);
 }
 
+// Exact pixel sums (PT_FIXED_ACC): a finished sample group's float sum g is
+// added to its pixel's accumulator as floor(g * 2^32) in unsigned 32.32 fixed
+// point (g in [0, 2^31); NaN and negatives -> 0; exact: g - trunc(g) and the
+// scaling by 2^32 round nothing).  Integer addition is associative, so the
+// pixel's value is independent of the order in which groups finish -- no float
+// atomics (the reference GPU path atomicAdds floats, kernel.cu:341-343) and no
+// per-group sums in memory.  No-return atomics at agent scope.
+__device__ __forceinline__ unsigned long long to_fixed32(float v) {
+  v = fminf(fmaxf(v, 0.0f), 2147483520.0f);
+  const uint32_t hi = (uint32_t)v;
+  const uint32_t lo = (uint32_t)((v - (float)hi) * 4294967296.0f);
+  return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ void accum_add(unsigned long long* a, float3 g) {
+  __hip_atomic_fetch_add(a, to_fixed32(g.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(a + 1, to_fixed32(g.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(a + 2, to_fixed32(g.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Lane modes of the persistent kernel.
 enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 
@@ -912,7 +931,11 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if (sample < P.spp && !group_starts(sample)) {
           mode = M_CAMERA;
         } else {
+#if PT_FIXED_ACC
+          accum_add(P.accum + 3 * (size_t)pix_index(pix), acc);
+#else
           store3(P.partial + 3 * slot_of(pix, sample), acc);
+#endif
           PT_SLOT_DONE();
           mode = M_FETCH;
         }
@@ -1017,7 +1040,11 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if (ENV) acc = acc + env_dir(P, d);
         ++sample;
         if (sample >= P.spp || group_starts(sample)) {
+#if PT_FIXED_ACC
+          accum_add(P.accum + 3 * (size_t)pix_index(pix), acc);
+#else
           store3(P.partial + 3 * slot_of(pix, sample), acc);
+#endif
           PT_SLOT_DONE();
           mode = M_FETCH;
         }
@@ -1163,6 +1190,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
 // Lanes that resolve one pixel: the pixel's groups are read as one coalesced
 // run (the per-pixel partials are n_groups * 12 B contiguous).
 __host__ __device__ __forceinline__ int resolve_team(int n_groups) {
+  if (PT_FIXED_ACC) return 1;  // one exact sum per pixel
   int k = 1;
   while (k < n_groups && k < 64) k <<= 1;
   return k;
@@ -1185,6 +1213,18 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
   const int4 tile = live ? P.tiles[tq >> 10] : make_int4(0, 0, 0, 0);
   int2 xy = live ? tile_pixel(tile, tq & 1023u) : make_int2(-1, -1);
   float3 acc = f3(0, 0, 0);
+#if PT_FIXED_ACC
+  if (xy.x >= 0 && !culled(P, xy.x, xy.y)) {
+    // the pixel's exact sum -> its mean; the accumulator is left zeroed for
+    // the slot's next launch
+    unsigned long long* a = P.accum + 3 * ((size_t)xy.x + (size_t)xy.y * (size_t)P.W);
+    const double kScale = 2.3283064365386963e-10 / (double)P.spp;  // 2^-32 / spp
+    acc = f3((float)((double)a[0] * kScale), (float)((double)a[1] * kScale), (float)((double)a[2] * kScale));
+    a[0] = a[1] = a[2] = 0ull;
+  }
+  if (xy.x < 0) return;
+  const float inv_spp = 1.0f;
+#else
   if (xy.x >= 0 && !culled(P, xy.x, xy.y)) {
     const float* p = P.partial + 3 * ((size_t)xy.x + (size_t)xy.y * (size_t)P.W) * (size_t)P.n_groups;
     for (int g = j; g < P.n_groups; g += k) acc = acc + ld3(p + 3 * g);
@@ -1194,6 +1234,7 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
     acc = acc + f3(__shfl_xor(acc.x, off), __shfl_xor(acc.y, off), __shfl_xor(acc.z, off));
   if (xy.x < 0 || j != 0) return;
   const float inv_spp = (float)(1.0 / (double)P.spp);
+#endif
   const size_t o = P.packed ? (size_t)(tq & ~1023u) + (size_t)((xy.y - tile.y) * 32 + (xy.x - tile.x))
                             : (size_t)xy.x + (size_t)xy.y * (size_t)P.W;
   store3(P.out + 3 * o, acc * inv_spp);

@@ -105,6 +105,8 @@ _SIGS = {
     "pt_set_params": (c_int32, [c_void_p, POINTER(pt_params)]),
     "pt_render_tiles": (c_int32, [c_void_p, POINTER(pt_tile), c_int32, c_void_p, c_uint32]),
     "pt_render_tiles_device": (c_int32, [c_void_p, POINTER(pt_tile), c_int32, c_void_p, c_void_p, c_uint32]),
+    "pt_tile_submit": (c_int32, [c_void_p, POINTER(pt_tile), c_void_p, c_void_p]),
+    "pt_tile_finish": (c_int32, [c_void_p]),
     "pt_intersect": (c_int32, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
     "pt_get_stats": (c_int32, [c_void_p, POINTER(pt_stats)]),

@@ -103,6 +103,21 @@ class Device:
         check(self._lib.pt_render_tiles_device(self.handle, arr, len(keep), ctypes.c_void_p(out_ptr),
                                                ctypes.c_void_p(stream or None), flags))
 
+    def submit_tile(self, tile, hdr: np.ndarray, rgba: Optional[np.ndarray] = None):
+        """pt_tile_submit: queue one tile; its pixels land in `hdr` ((H, W, 3)
+        float32) and, toColor'd, in `rgba` ((H, W, 4) uint8) when its batch
+        completes.  Both arrays must stay alive until finish_tiles()."""
+        assert hdr.dtype == np.float32 and hdr.flags.c_contiguous
+        if rgba is not None:
+            assert rgba.dtype == np.uint8 and rgba.flags.c_contiguous and rgba.shape[-1] == 4
+        t = native.pt_tile(*[int(v) for v in tile])
+        check(self._lib.pt_tile_submit(self.handle, ctypes.byref(t), hdr.ctypes.data,
+                                       None if rgba is None else rgba.ctypes.data))
+
+    def finish_tiles(self):
+        """pt_tile_finish: render what is queued, wait for every submitted tile."""
+        check(self._lib.pt_tile_finish(self.handle))
+
     def intersect(self, o, d, max_t):
         o = np.ascontiguousarray(o, np.float64)
         d = np.ascontiguousarray(d, np.float64)
@@ -292,6 +307,57 @@ class PathTracer:
         for (x, y, tw, th) in tiles:
             x1, y1 = min(x + tw, w), min(y + th, h)
             self.frameBuffer[y:y1, x:x1] = to_color(self.sampleBuffer[y:y1, x:x1])
+
+    def render_tile_workers(self, num_threads: Optional[int] = None, asynchronous: bool = True,
+                            tiles: Optional[Sequence[Tuple[int, int, int, int]]] = None):
+        """The reference's tile workers (start_raytracing + worker_thread,
+        pathtracer.cpp:192-221, 613-637): `num_threads` threads pop tiles from
+        the 32x32 FIFO and call raytrace_tile on each, through ONE context
+        (calls serialised by a lock, as INTEGRATION.md's adapter does).
+        asynchronous=True: raytrace_tile is pt_tile_submit (tiles batched into
+        launches, each completed into sampleBuffer/frameBuffer on a stream
+        callback; the last worker's pt_tile_finish waits for all);
+        asynchronous=False: one synchronous pt_render_tiles launch per tile."""
+        import queue
+        import threading
+        if not self.has_valid_configuration():
+            raise RuntimeError("PathTracer is not configured (scene, camera, frame size)")
+        h, w = self.sampleBuffer.shape[:2]
+        self._params()
+        dev = self._device()
+        work = queue.Queue()
+        for t in (tile_fifo(w, h) if tiles is None else tiles):
+            work.put(t)
+        lock = threading.Lock()
+        errors = []
+
+        def worker():
+            try:
+                while True:
+                    try:
+                        t = work.get_nowait()
+                    except queue.Empty:
+                        return
+                    if asynchronous:
+                        with lock:
+                            dev.submit_tile(t, self.sampleBuffer, self.frameBuffer)
+                    else:
+                        with lock:
+                            dev.render_tiles([t], self.sampleBuffer)
+                        x1, y1 = min(t[0] + t[2], w), min(t[1] + t[3], h)
+                        self.frameBuffer[t[1]:y1, t[0]:x1] = to_color(self.sampleBuffer[t[1]:y1, t[0]:x1])
+            except Exception as e:  # pragma: no cover - surfaced below
+                errors.append(e)
+
+        ths = [threading.Thread(target=worker) for _ in range(num_threads or self.numWorkerThreads)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        if asynchronous:
+            dev.finish_tiles()
+        if errors:
+            raise errors[0]
 
     def raytrace_pixel(self, x: int, y: int) -> np.ndarray:
         self.raytrace_tile(x, y, 1, 1)

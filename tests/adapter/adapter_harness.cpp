@@ -42,6 +42,7 @@ int main(int argc, char** argv) {
       for (int i; (i = next++) < nt;) gpu.raytrace_tile((i % ntx) * 32, (i / ntx) * 32, 32, 32);
     });
   for (auto& t : th) t.join();
+  gpu.finish_tiles();  // the last worker's call site (worker_thread, workerDoneCount == numWorkerThreads)
   // frame 2 (seed 99) cancelled before its tiles: nothing may be launched
   gpu.begin_frame(99u);
   pt->continueRaytracing = false;

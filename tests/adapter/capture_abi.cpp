@@ -5,7 +5,8 @@
 // the PTDUMP file named by $PT_CAPTURE_OUT under the record names
 // oracle/_ref/ref_driver --mode dump uses; pt_set_params and pt_render_tiles
 // calls are logged ("params": 7 ints per call, "tiles": 4 ints + the seed in
-// force, per call) and leave the output buffer untouched.
+// force, per call; pt_tile_submit calls the same) and leave the output buffer
+// untouched; "finishes" logs the tiles submitted at each pt_tile_finish.
 #include <cstdlib>
 #include <vector>
 
@@ -14,7 +15,7 @@
 
 struct pt_ctx {
   std::vector<double> cam;
-  std::vector<int32_t> ptype, pbsdf, btype, ltype, params, tiles;
+  std::vector<int32_t> ptype, pbsdf, btype, ltype, params, tiles, finishes;
   std::vector<double> pgeom, pnorm, nbb, lgeom;
   std::vector<int64_t> ninfo, env_shape;
   std::vector<float> bpar, lrad, larea, env;
@@ -45,6 +46,7 @@ static void flush(pt_ctx* c) {
   w.i8("node_info", c->ninfo);
   w.i4("params", c->params);
   w.i4("tiles", c->tiles);
+  w.i4("finishes", c->finishes);
 }
 
 extern "C" {
@@ -114,6 +116,17 @@ int pt_render_tiles(pt_ctx* c, const pt_tile* tiles, int32_t n, float*, uint32_t
   if (!c->have_params) return PT_E_NOSCENE;
   for (int32_t i = 0; i < n; ++i)
     c->tiles.insert(c->tiles.end(), {tiles[i].x, tiles[i].y, tiles[i].w, tiles[i].h, (int32_t)c->cur.seed});
+  return PT_OK;
+}
+
+int pt_tile_submit(pt_ctx* c, const pt_tile* t, float* hdr, uint32_t*) {
+  if (!c->have_params || !hdr) return PT_E_NOSCENE;
+  c->tiles.insert(c->tiles.end(), {t->x, t->y, t->w, t->h, (int32_t)c->cur.seed});
+  return PT_OK;
+}
+
+int pt_tile_finish(pt_ctx* c) {
+  c->finishes.push_back((int32_t)(c->tiles.size() / 5));  // tiles submitted when the frame was finished
   return PT_OK;
 }
 

@@ -156,7 +156,8 @@ def test_fullsize_sampled_tiles_match_oracle(tmp_path, restate, name, k, k_mixed
               f"{int(black.sum())} black reference pixels")
         assert close >= min_close, (kind, closes)
         assert rel_mean <= 1e-3, (kind, rel_mean)
-        assert (gflat[black] == 0).mean() >= min_close, kind
+        if black.any():
+            assert (gflat[black] == 0).mean() >= min_close, kind
 
 
 @pytest.mark.parametrize("name,spp", [("c3", 64), ("c4", 16)])

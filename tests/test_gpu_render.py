@@ -656,3 +656,69 @@ def test_hip_pipelined_device_renders_match_synchronous():
         dev.render_tiles(tiles, ref)
         assert np.array_equal(g, ref), seed
     assert np.array_equal(got[0], got[3]) and not np.array_equal(got[0], got[1])
+
+
+@pytest.mark.parametrize("batch,threads,asynchronous", [(None, 8, True), ("3", 4, True), ("1", 2, True),
+                                                         (None, 8, False)])
+def test_hip_tile_workers_seam_bit_identical(monkeypatch, batch, threads, asynchronous):
+    """The reference's literal seam -- worker threads calling raytrace_tile
+    once per 32x32 tile (pathtracer.cpp:585-621) -- through one context, in a
+    shuffled tile order, asynchronously (pt_tile_submit: batched launches
+    completed on stream callbacks) or one synchronous launch per tile: the
+    sampleBuffer equals the whole-frame render bit for bit and the frameBuffer
+    is its toColor."""
+    from dsgpuraytracing_amd.pathtracer import to_color
+    if batch is None:
+        monkeypatch.delenv("PT_TILE_BATCH", raising=False)
+    else:
+        monkeypatch.setenv("PT_TILE_BATCH", batch)
+    sc = Scene.from_dump(golden("c1_default_128x128.scene.ptd"))
+    w, h = 136, 100  # ragged edge tiles
+
+    def tracer():
+        pt = PathTracer(ns_aa=8, max_ray_depth=4, ns_area_light=1, seed=21)
+        pt.set_frame_size(w, h)
+        pt.set_camera(sc.camera)
+        pt.set_scene(sc)
+        return pt
+
+    whole = tracer()
+    whole.start_raytracing()
+    pt = tracer()
+    tiles = tile_fifo(w, h)
+    rng = np.random.default_rng(3)
+    order = [tiles[i] for i in rng.permutation(len(tiles))]
+    pt.render_tile_workers(num_threads=threads, asynchronous=asynchronous, tiles=order)
+    assert whole.sampleBuffer.mean() > 0
+    assert np.array_equal(pt.sampleBuffer, whole.sampleBuffer)
+    assert np.array_equal(pt.frameBuffer, to_color(whole.sampleBuffer))
+    # a second frame through the same context (buffers reused, queue empty again)
+    pt.sampleBuffer[...] = 0
+    pt.frameBuffer[...] = 0
+    pt.render_tile_workers(num_threads=threads, asynchronous=asynchronous, tiles=tiles[::-1])
+    assert np.array_equal(pt.sampleBuffer, whole.sampleBuffer)
+
+
+def test_hip_tile_submit_flushes_before_state_changes():
+    """Queued tiles render with the parameters they were submitted under: a
+    setter launches what is queued first."""
+    from dsgpuraytracing_amd.pathtracer import Device
+    sc = Scene.from_dump(golden("c1_default_64x64.scene.ptd"))
+    dev = Device(0)
+    dev.upload_scene(sc)
+    dev.set_camera(sc.camera)
+    dev.set_params(64, 64, 4, 4, 1, 5)
+    a = np.zeros((64, 64, 3), np.float32)
+    dev.submit_tile((0, 0, 32, 32), a)
+    dev.set_params(64, 64, 4, 4, 1, 6)   # seed changes after the submit
+    dev.submit_tile((32, 0, 32, 32), a)
+    dev.finish_tiles()
+    ref5 = np.zeros_like(a)
+    dev.set_params(64, 64, 4, 4, 1, 5)
+    dev.render_tiles([(0, 0, 64, 64)], ref5)
+    ref6 = np.zeros_like(a)
+    dev.set_params(64, 64, 4, 4, 1, 6)
+    dev.render_tiles([(0, 0, 64, 64)], ref6)
+    assert np.array_equal(a[:32, :32], ref5[:32, :32])
+    assert np.array_equal(a[:32, 32:], ref6[:32, 32:])
+    assert not np.array_equal(ref5[:32, 32:], ref6[:32, 32:])

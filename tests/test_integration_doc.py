@@ -102,3 +102,5 @@ def test_integration_adapter_links_and_hands_over_the_reference_payload(tmp_path
         assert len(tiles) == nt and (tiles[:, 4] == 1234).all(), name
         ntx = (w + 31) // 32
         assert sorted((int(y) // 32) * ntx + int(x) // 32 for x, y in tiles[:, :2]) == list(range(nt)), name
+        # the frame is finished once, after every tile was submitted
+        assert got["finishes"].tolist() == [nt], name
