@@ -23,6 +23,9 @@
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "pt_device.h"
 
 namespace lbvh {
@@ -68,13 +71,28 @@ struct Params {
   float smin[3], sext[3];
   uint32_t* keys;       // sorted Morton codes
   int* ids;             // sorted primitive ids
-  int* child;           // 2 per internal node: >= 0 internal index, < 0: ~leaf index
+  int* child;           // 2 per internal node: >= 0 internal index, < 0: ~leaf (sorted primitive) index
   int* parent;          // parent of internal node i (n-1 entries), then of leaf j (n entries)
-  int* start;           // first sorted primitive of internal node i
-  int* range;           // primitive count of internal node i
+  int* start;           // first primitive (final order) of internal node i (written by the emission)
+  int* range;           // primitives below internal node i
   float* box;           // 6 per internal node (lo xyz, hi xyz)
-  int* flag;            // arrivals per internal node
+  float* cost;          // SAH cost of the subtree of internal node i (unnormalised)
+  int* collapsed;       // 1: internal node i becomes one leaf of its <= kMaxLeaf primitives
+  int* flag;            // arrivals per internal node (bottom-up passes)
+  int* pos;             // final position of sorted primitive j (depth-first leaf order)
 };
+
+// Relaxed agent-scope accesses for tree data shared between the climbing
+// threads of one bottom-up pass (ordered by the acq_rel arrival counters; the
+// XCD L2s are not coherent for plain accesses).
+template <class T>
+__device__ __forceinline__ T ald(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void ast(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __global__ void k_morton(Params P) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -135,6 +153,7 @@ __global__ void k_internal(Params P) {
   P.parent[b >= 0 ? b : (P.n - 1) + ~b] = i;
   P.start[i] = first;
   P.range[i] = last - first + 1;
+  P.collapsed[i] = 0;
   P.flag[i] = 0;
   if (i == 0) P.parent[0] = -1;
 }
@@ -144,82 +163,239 @@ __device__ __forceinline__ void child_box(const Params& P, int c, float lo[3], f
     prim_box(P.prims[P.ids[~c]], lo, hi);
   } else {
     for (int k = 0; k < 3; ++k) {
-      lo[k] = __hip_atomic_load(&P.box[6 * c + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      hi[k] = __hip_atomic_load(&P.box[6 * c + 3 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lo[k] = ald(&P.box[6 * c + k]);
+      hi[k] = ald(&P.box[6 * c + 3 + k]);
     }
   }
 }
 
-// Bottom-up boxes (propogateBBox, helper.cu:437-458): one thread per leaf
-// climbs until it is the first to reach a node.
-__global__ void k_boxes(Params P) {
+// SAH over the binary tree, as the host render tree (render_tree.cpp): one
+// unit per traversal step, one per primitive test, leaves of <= 4 primitives.
+constexpr float kCt = 1.0f, kCi = 1.0f;
+constexpr int kMaxLeaf = 4;
+constexpr int kTreelet = 7;  // treelet leaves (Karras & Aila: 7)
+constexpr int kDpBlock = 64;  // threads per block of the restructuring pass (LDS tables per thread)
+
+__device__ __forceinline__ float half_area(const float lo[3], const float hi[3]) {
+  const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+  return dx * dy + dy * dz + dz * dx;
+}
+__device__ __forceinline__ int node_count(const Params& P, int c) { return c < 0 ? 1 : ald(&P.range[c]); }
+__device__ __forceinline__ float node_cost(const Params& P, int c, const float lo[3], const float hi[3]) {
+  return c < 0 ? kCi * half_area(lo, hi) : ald(&P.cost[c]);
+}
+
+// Bottom-up pass (propogateBBox, helper.cu:437-458, extended): one thread per
+// primitive climbs until it is the first to reach a node; the second arrival
+// owns the node, whose children are final.  It sets the node's box, count,
+// SAH cost and leaf-collapse choice -- and with `optimize`, for nodes with
+// >= kTreelet primitives, first rebuilds the node's treelet SAH-optimally.
+__global__ __launch_bounds__(kDpBlock) void k_treelet(Params P, int optimize) {
+  // per-thread DP tables (lane-strided: conflict-free)
+  __shared__ float s_cost[128 * kDpBlock];
+  __shared__ uint8_t s_pick[128 * kDpBlock];
+  const int tid = threadIdx.x;
+  auto cost_at = [&](int S) -> float& { return s_cost[S * kDpBlock + tid]; };
+  auto pick_at = [&](int S) -> uint8_t& { return s_pick[S * kDpBlock + tid]; };
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= P.n || P.n < 2) return;
-  int node = P.parent[(P.n - 1) + j];
+  int node = ald(&P.parent[(P.n - 1) + j]);
   while (node >= 0) {
     if (__hip_atomic_fetch_add(&P.flag[node], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
-    float la[3], ha[3], lb[3], hb[3];
-    child_box(P, P.child[2 * node], la, ha);
-    child_box(P, P.child[2 * node + 1], lb, hb);
-    for (int k = 0; k < 3; ++k) {
-      __hip_atomic_store(&P.box[6 * node + k], fminf(la[k], lb[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&P.box[6 * node + 3 + k], fmaxf(ha[k], hb[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int c0 = ald(&P.child[2 * node]), c1 = ald(&P.child[2 * node + 1]);
+    const int cnt = node_count(P, c0) + node_count(P, c1);
+    if (optimize && cnt >= kTreelet) {
+      // ---- the treelet: expand the largest-area internal treelet leaf
+      int leaf[kTreelet], inner[kTreelet - 1];
+      float lo[kTreelet][3], hi[kTreelet][3];
+      int nl = 2, ni = 1;
+      leaf[0] = c0;
+      leaf[1] = c1;
+      inner[0] = node;
+      child_box(P, c0, lo[0], hi[0]);
+      child_box(P, c1, lo[1], hi[1]);
+      while (nl < kTreelet) {
+        int best = -1;
+        float ba = -1.0f;
+        for (int i = 0; i < nl; ++i)
+          if (leaf[i] >= 0) {
+            const float a = half_area(lo[i], hi[i]);
+            if (a > ba) {
+              ba = a;
+              best = i;
+            }
+          }
+        if (best < 0) break;
+        const int x = leaf[best];
+        inner[ni++] = x;
+        leaf[best] = ald(&P.child[2 * x]);
+        leaf[nl] = ald(&P.child[2 * x + 1]);
+        child_box(P, leaf[best], lo[best], hi[best]);
+        child_box(P, leaf[nl], lo[nl], hi[nl]);
+        ++nl;
+      }
+      float lcost[kTreelet];
+      int lcnt[kTreelet];
+      for (int i = 0; i < nl; ++i) {
+        lcost[i] = node_cost(P, leaf[i], lo[i], hi[i]);
+        lcnt[i] = node_count(P, leaf[i]);
+      }
+      // ---- DP over the leaf subsets in increasing order (a proper subset
+      // of S is numerically smaller than S)
+      const int full = (1 << nl) - 1;
+      unsigned long long coll_lo = 0ull, coll_hi = 0ull;  // subsets better as one leaf
+      for (int S = 1; S <= full; ++S) {
+        const int low = S & -S;
+        if (S == low) {
+          cost_at(S) = lcost[__ffs(S) - 1];
+          continue;
+        }
+        float blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        int n = 0;
+        for (int i = 0; i < nl; ++i)
+          if (S & (1 << i)) {
+            n += lcnt[i];
+            for (int k = 0; k < 3; ++k) {
+              blo[k] = fminf(blo[k], lo[i][k]);
+              bhi[k] = fmaxf(bhi[k], hi[i][k]);
+            }
+          }
+        const float a = half_area(blo, bhi);
+        // partitions (P, S \ P) with P holding S's lowest leaf: each once
+        const int rest = S ^ low;
+        float best = INFINITY;
+        int bp = low;
+        for (int sub = (rest - 1) & rest;; sub = (sub - 1) & rest) {
+          const int Pm = low | sub;
+          const float c = cost_at(Pm) + cost_at(S ^ Pm);
+          if (c < best) {
+            best = c;
+            bp = Pm;
+          }
+          if (sub == 0) break;
+        }
+        const float csplit = kCt * a + best;
+        const float cleaf = n <= kMaxLeaf ? kCi * a * (float)n : INFINITY;
+        pick_at(S) = (uint8_t)bp;
+        if (cleaf <= csplit) {
+          cost_at(S) = cleaf;
+          if (S < 64) coll_lo |= 1ull << S;
+          else coll_hi |= 1ull << (S - 64);
+        } else {
+          cost_at(S) = csplit;
+        }
+      }
+      // ---- rebuild the treelet top-down from the DP choices, reusing its
+      // internal nodes (the treelet root keeps its index and its parent)
+      int stk_s[kTreelet], stk_x[kTreelet], sp = 0, next = 1;
+      stk_s[sp] = full;
+      stk_x[sp++] = node;
+      while (sp > 0) {
+        --sp;
+        const int S = stk_s[sp], x = stk_x[sp];
+        const int parts[2] = {pick_at(S), S ^ pick_at(S)};
+        for (int side = 0; side < 2; ++side) {
+          const int sub = parts[side];
+          int c;
+          if ((sub & (sub - 1)) == 0) {
+            c = leaf[__ffs(sub) - 1];
+          } else {
+            c = inner[next++];
+            stk_s[sp] = sub;
+            stk_x[sp++] = c;
+          }
+          ast(&P.child[2 * x + side], c);
+          ast(&P.parent[c >= 0 ? c : (P.n - 1) + ~c], x);
+        }
+        float blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        int n = 0;
+        for (int i = 0; i < nl; ++i)
+          if (S & (1 << i)) {
+            n += lcnt[i];
+            for (int k = 0; k < 3; ++k) {
+              blo[k] = fminf(blo[k], lo[i][k]);
+              bhi[k] = fmaxf(bhi[k], hi[i][k]);
+            }
+          }
+        for (int k = 0; k < 3; ++k) {
+          ast(&P.box[6 * x + k], blo[k]);
+          ast(&P.box[6 * x + 3 + k], bhi[k]);
+        }
+        ast(&P.range[x], n);
+        ast(&P.cost[x], cost_at(S));
+        const bool cl = S < 64 ? ((coll_lo >> S) & 1ull) : ((coll_hi >> (S - 64)) & 1ull);
+        ast(&P.collapsed[x], cl ? 1 : 0);
+      }
+    } else {
+      float la[3], ha[3], lb[3], hb[3], blo[3], bhi[3];
+      child_box(P, c0, la, ha);
+      child_box(P, c1, lb, hb);
+      for (int k = 0; k < 3; ++k) {
+        blo[k] = fminf(la[k], lb[k]);
+        bhi[k] = fmaxf(ha[k], hb[k]);
+        ast(&P.box[6 * node + k], blo[k]);
+        ast(&P.box[6 * node + 3 + k], bhi[k]);
+      }
+      const float a = half_area(blo, bhi);
+      const float csplit = kCt * a + node_cost(P, c0, la, ha) + node_cost(P, c1, lb, hb);
+      const float cleaf = cnt <= kMaxLeaf ? kCi * a * (float)cnt : INFINITY;
+      ast(&P.range[node], cnt);
+      ast(&P.cost[node], fminf(csplit, cleaf));
+      ast(&P.collapsed[node], cleaf <= csplit ? 1 : 0);
     }
-    __atomic_thread_fence(__ATOMIC_RELEASE);
-    node = P.parent[node];
+    node = ald(&P.parent[node]);
   }
-}
-
-// Children of binary node c as the renderer sees them: a collapsed subtree
-// (range <= LEAF_NUMBER, treeCollapse kernel.cu:475-485) or a real leaf is a
-// leaf cursor, otherwise the internal index.
-__device__ __forceinline__ int as_ref(const Params& P, int c) {
-  if (c < 0) return ~((~c) << 3);  // one primitive: count 1
-  if (P.range[c] <= kLeafNumber) return ~((P.start[c] << 3) | (P.range[c] - 1));
-  return c;
-}
-
-__device__ __forceinline__ void ref_box(const Params& P, int c, float lo[3], float hi[3]) { child_box(P, c, lo, hi); }
-
-// Binary nodes for the reference-count launch (node index = Karras index).
-__global__ void k_emit_bin(Params P, DNode2* out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P.n - 1) return;
-  float l0[3], h0[3], l1[3], h1[3];
-  const int c0 = P.child[2 * i], c1 = P.child[2 * i + 1];
-  ref_box(P, c0, l0, h0);
-  ref_box(P, c1, l1, h1);
-  DNode2 d;
-  d.a = make_float4(l0[0], h0[0], l0[1], h0[1]);
-  d.b = make_float4(l1[0], h1[0], l1[1], h1[1]);
-  d.c = make_float4(l0[2], h0[2], l1[2], h1[2]);
-  d.e = make_int4(as_ref(P, c0), as_ref(P, c1), 0, 0);
-  out[i] = d;
 }
 
 struct Item {
   int bin;    // internal binary node (not collapsed)
   int idx;    // its BVH4 node index
   int stack;  // worst-case stack entries on entering it
+  int start;  // its first primitive in the final (depth-first leaf) order
 };
 
-// One breadth-first level: each BVH4 node takes up to four children by opening
-// both (non-collapsed internal) children of its binary node.
+__device__ __forceinline__ int cursor(int first, int count) { return ~((first << 3) | (count - 1)); }
+
+// One BVH4 node per item, top-down: open the largest-area internal child
+// (not collapsed) until four children; every child gets its first primitive
+// in depth-first leaf order, collapsed subtrees and primitives become leaf
+// cursors (their primitives numbered here), internal children are queued
+// with a freshly allocated (forward) index.
 __global__ void k_bfs(Params P, const Item* __restrict__ in, int n_in, Item* out, int* n_out, int* n_nodes,
                       int* max_stack, DNode* nodes) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_in) return;
   const Item it = in[t];
-  int kids[4];
-  int nk = 0;
-  for (int s = 0; s < 2; ++s) {
-    const int c = P.child[2 * it.bin + s];
-    if (c >= 0 && P.range[c] > kLeafNumber) {
-      kids[nk++] = P.child[2 * c];
-      kids[nk++] = P.child[2 * c + 1];
-    } else {
-      kids[nk++] = c;
-    }
+  P.start[it.bin] = it.start;
+  int kids[4], ks[4];
+  float klo[4][3], khi[4][3];
+  int nk = 2;
+  kids[0] = P.child[2 * it.bin];
+  kids[1] = P.child[2 * it.bin + 1];
+  ks[0] = it.start;
+  ks[1] = it.start + node_count(P, kids[0]);
+  child_box(P, kids[0], klo[0], khi[0]);
+  child_box(P, kids[1], klo[1], khi[1]);
+  while (nk < 4) {
+    int best = -1;
+    float ba = -1.0f;
+    for (int k = 0; k < nk; ++k)
+      if (kids[k] >= 0 && !P.collapsed[kids[k]]) {
+        const float a = half_area(klo[k], khi[k]);
+        if (a > ba) {
+          ba = a;
+          best = k;
+        }
+      }
+    if (best < 0) break;
+    const int x = kids[best];
+    P.start[x] = ks[best];
+    kids[best] = P.child[2 * x];
+    kids[nk] = P.child[2 * x + 1];
+    ks[nk] = ks[best] + node_count(P, kids[best]);
+    child_box(P, kids[best], klo[best], khi[best]);
+    child_box(P, kids[nk], klo[nk], khi[nk]);
+    ++nk;
   }
   const int below = it.stack + nk - 1;
   atomicMax(max_stack, below);
@@ -227,22 +403,38 @@ __global__ void k_bfs(Params P, const Item* __restrict__ in, int n_in, Item* out
   int ref[4];
   for (int k = 0; k < 4; ++k) {
     if (k < nk) {
-      float l[3], h[3];
-      ref_box(P, kids[k], l, h);
       for (int a = 0; a < 3; ++a) {
-        lo[a][k] = l[a];
-        hi[a][k] = h[a];
+        lo[a][k] = klo[k][a];
+        hi[a][k] = khi[k][a];
       }
-      int r = as_ref(P, kids[k]);
-      if (r >= 0) {  // internal: allocate its BVH4 node (after this one: forward reference)
+      const int c = kids[k];
+      int r;
+      if (c < 0) {  // one primitive
+        P.pos[~c] = ks[k];
+        r = cursor(ks[k], 1);
+      } else if (P.collapsed[c]) {  // a leaf of its <= kMaxLeaf primitives, numbered depth-first
+        P.start[c] = ks[k];
+        int st[kMaxLeaf + 1], sp = 0, m = ks[k];  // depth-first, left child first
+        st[sp++] = c;
+        while (sp > 0) {
+          const int x = st[--sp];
+          if (x < 0) {
+            P.pos[~x] = m++;
+          } else {
+            st[sp++] = P.child[2 * x + 1];
+            st[sp++] = P.child[2 * x];
+          }
+        }
+        r = cursor(ks[k], P.range[c]);
+      } else {
         const int idx = atomicAdd(n_nodes, 1);
-        out[atomicAdd(n_out, 1)] = Item{kids[k], idx, below};
+        out[atomicAdd(n_out, 1)] = Item{c, idx, below, ks[k]};
         r = idx;
       }
       ref[k] = r;
-    } else {  // empty slot: box at +inf
+    } else {  // empty slot: box at +inf, a leaf cursor (never entered)
       for (int a = 0; a < 3; ++a) lo[a][k] = hi[a][k] = __int_as_float(0x7f800000);
-      ref[k] = 0;
+      ref[k] = cursor(0, 1);
     }
   }
   DNode d;
@@ -257,12 +449,43 @@ __global__ void k_bfs(Params P, const Item* __restrict__ in, int n_in, Item* out
   nodes[it.idx] = d;
 }
 
-// Primitives, vertex normals and the sorted -> input id map in sorted order.
+// Binary nodes for the reference-count launch (node index = Karras index),
+// children as the renderer sees them: primitives and collapsed subtrees are
+// leaf cursors over the final order, other internal nodes their index.
+__device__ __forceinline__ int as_ref(const Params& P, int c) {
+  if (c < 0) return cursor(P.pos[~c], 1);
+  if (P.collapsed[c]) return cursor(P.start[c], P.range[c]);
+  return c;
+}
+
+__global__ void k_emit_bin(Params P, DNode2* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.n - 1) return;
+  float l0[3], h0[3], l1[3], h1[3];
+  const int c0 = P.child[2 * i], c1 = P.child[2 * i + 1];
+  child_box(P, c0, l0, h0);
+  child_box(P, c1, l1, h1);
+  DNode2 d;
+  d.a = make_float4(l0[0], h0[0], l0[1], h0[1]);
+  d.b = make_float4(l1[0], h1[0], l1[1], h1[1]);
+  d.c = make_float4(l0[2], h0[2], l1[2], h1[2]);
+  d.e = make_int4(as_ref(P, c0), as_ref(P, c1), 0, 0);
+  out[i] = d;
+}
+
+__global__ void k_identity(Params P) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < P.n) P.pos[j] = j;
+}
+
+// Primitives, vertex normals and the final -> input id map in the final
+// (depth-first leaf) order.
 __global__ void k_gather(Params P, const float* __restrict__ norms_in, DPrim* prims_out, float* norms_out,
                          int* prim_map) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P.n) return;
-  const int s = P.ids[i];
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= P.n) return;
+  const int s = P.ids[j];
+  const int i = P.pos[j];
   prims_out[i] = P.prims[s];
   for (int k = 0; k < 9; ++k) norms_out[9 * (size_t)i + k] = norms_in[9 * (size_t)s + k];
   prim_map[i] = s;
@@ -287,10 +510,12 @@ extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t
     P.smin[k] = in->scene_min[k];
     P.sext[k] = in->scene_extent[k];
   }
+  int passes = 2;  // treelet-restructuring passes (0: the reference's Karras tree, SAH leaf collapse)
+  if (const char* e = std::getenv("PT_LBVH_PASSES")) passes = std::max(0, std::min(8, std::atoi(e)));
   // scratch
   uint32_t *keys_a = nullptr, *keys_b = nullptr;
   int *ids_a = nullptr, *ids_b = nullptr, *ints = nullptr;
-  float* box = nullptr;
+  float *box = nullptr, *cost = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   const size_t ni = (size_t)(n > 1 ? n - 1 : 1);
@@ -298,8 +523,10 @@ extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t
   LB_CHK(hipMalloc(&keys_b, (size_t)n * 4));
   LB_CHK(hipMalloc(&ids_a, (size_t)n * 4));
   LB_CHK(hipMalloc(&ids_b, (size_t)n * 4));
-  LB_CHK(hipMalloc(&ints, (ni * 2 + ni + n + ni + ni + ni + 4) * 4));
+  // child 2ni, parent ni+n, start ni, range ni, collapsed ni, flag ni, pos n, counters 4
+  LB_CHK(hipMalloc(&ints, (ni * 2 + (ni + n) + ni * 4 + n + 4) * 4));
   LB_CHK(hipMalloc(&box, ni * 6 * 4));
+  LB_CHK(hipMalloc(&cost, ni * 4));
   const int B = 256;
   const int gn = (n + B - 1) / B, gi = (int)((ni + B - 1) / B);
   P.keys = keys_a;
@@ -315,9 +542,12 @@ extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t
   P.parent = P.child + 2 * ni;
   P.start = P.parent + ni + n;
   P.range = P.start + ni;
-  P.flag = P.range + ni;
-  int* counters = P.flag + ni;  // n_nodes, n_out, max_stack, spare
+  P.collapsed = P.range + ni;
+  P.flag = P.collapsed + ni;
+  P.pos = P.flag + ni;
+  int* counters = P.pos + n;  // n_nodes, n_out, max_stack, spare
   P.box = box;
+  P.cost = cost;
   LB_CHK(hipMemsetAsync(counters, 0, 16, s));
   // outputs
   LB_CHK(hipMalloc(&out->prims, (size_t)n * sizeof(DPrim)));
@@ -325,9 +555,11 @@ extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t
   LB_CHK(hipMalloc(&out->prim_map, (size_t)n * 4));
   LB_CHK(hipMalloc(&out->nodes4, (size_t)(ni + 1) * sizeof(DNode)));
   LB_CHK(hipMalloc(&out->nodes2, ni * sizeof(DNode2)));
-  hipLaunchKernelGGL(k_gather, dim3(gn), dim3(B), 0, s, P, in->norms, out->prims, out->norms, out->prim_map);
-  LB_CHK(hipGetLastError());
   if (n <= kLeafNumber) {  // a single leaf: one BVH4 node, one child, as the host path
+    hipLaunchKernelGGL(k_identity, dim3(gn), dim3(B), 0, s, P);  // final order = sorted order
+    LB_CHK(hipGetLastError());
+    hipLaunchKernelGGL(k_gather, dim3(gn), dim3(B), 0, s, P, in->norms, out->prims, out->norms, out->prim_map);
+    LB_CHK(hipGetLastError());
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int k = 0; k < 3; ++k) {
       lo[k] = in->scene_min[k];
@@ -341,13 +573,13 @@ extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t
     d.hiy = make_float4(hi[1], inf, inf, inf);
     d.loz = make_float4(lo[2], inf, inf, inf);
     d.hiz = make_float4(hi[2], inf, inf, inf);
-    d.ref = make_int4(~((0 << 3) | (n - 1)), 0, 0, 0);
+    d.ref = make_int4(~((0 << 3) | (n - 1)), ~0, ~0, ~0);
     LB_CHK(hipMemcpyAsync(out->nodes4, &d, sizeof(d), hipMemcpyHostToDevice, s));
     DNode2 b{};
     b.a = make_float4(lo[0], hi[0], lo[1], hi[1]);
     b.b = make_float4(inf, inf, inf, inf);
     b.c = make_float4(lo[2], hi[2], inf, inf);
-    b.e = make_int4(~((0 << 3) | (n - 1)), 0, 0, 0);
+    b.e = make_int4(~((0 << 3) | (n - 1)), ~0, 0, 0);
     LB_CHK(hipMemcpyAsync(out->nodes2, &b, sizeof(b), hipMemcpyHostToDevice, s));
     LB_CHK(hipStreamSynchronize(s));
     out->n4 = 1;
@@ -360,20 +592,26 @@ extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t
   } else {
     hipLaunchKernelGGL(k_internal, dim3(gi), dim3(B), 0, s, P);
     LB_CHK(hipGetLastError());
-    hipLaunchKernelGGL(k_boxes, dim3(gn), dim3(B), 0, s, P);
+    // bottom-up: boxes, counts, SAH costs, leaf collapse; then the treelet passes
+    const int gt = (n + kDpBlock - 1) / kDpBlock;
+    hipLaunchKernelGGL(k_treelet, dim3(gt), dim3(kDpBlock), 0, s, P, 0);
     LB_CHK(hipGetLastError());
-    hipLaunchKernelGGL(k_emit_bin, dim3(gi), dim3(B), 0, s, P, out->nodes2);
-    LB_CHK(hipGetLastError());
-    // breadth-first BVH4 emission from the root (binary node 0 -> BVH4 node 0)
+    for (int p = 0; p < passes; ++p) {
+      LB_CHK(hipMemsetAsync(P.flag, 0, ni * 4, s));
+      hipLaunchKernelGGL(k_treelet, dim3(gt), dim3(kDpBlock), 0, s, P, 1);
+      LB_CHK(hipGetLastError());
+    }
+    // top-down BVH4 emission (breadth first, binary node 0 -> BVH4 node 0),
+    // numbering the primitives in depth-first leaf order on the way
     Item *fa = nullptr, *fb = nullptr;
     LB_CHK(hipMalloc(&fa, (ni + 1) * sizeof(Item)));
     LB_CHK(hipMalloc(&fb, (ni + 1) * sizeof(Item)));
-    Item root{0, 0, 0};
+    Item root{0, 0, 0, 0};
     int one = 1;
     LB_CHK(hipMemcpyAsync(fa, &root, sizeof(root), hipMemcpyHostToDevice, s));
     LB_CHK(hipMemcpyAsync(counters, &one, 4, hipMemcpyHostToDevice, s));  // n_nodes = 1 (the root)
     int n_in = 1;
-    while (n_in > 0) {  // one launch per two binary levels
+    while (n_in > 0) {  // one launch per BVH4 level
       LB_CHK(hipMemsetAsync(counters + 1, 0, 4, s));
       hipLaunchKernelGGL(k_bfs, dim3((n_in + B - 1) / B), dim3(B), 0, s, P, fa, n_in, fb, counters + 1, counters,
                          counters + 2, out->nodes4);
@@ -384,6 +622,10 @@ extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t
       fa = fb;
       fb = t;
     }
+    hipLaunchKernelGGL(k_emit_bin, dim3(gi), dim3(B), 0, s, P, out->nodes2);
+    LB_CHK(hipGetLastError());
+    hipLaunchKernelGGL(k_gather, dim3(gn), dim3(B), 0, s, P, in->norms, out->prims, out->norms, out->prim_map);
+    LB_CHK(hipGetLastError());
     int cnt[3] = {0, 0, 0};
     LB_CHK(hipMemcpyAsync(cnt, counters, 12, hipMemcpyDeviceToHost, s));
     float rb[6];
@@ -405,6 +647,7 @@ extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t
   (void)hipFree(ids_b);
   (void)hipFree(ints);
   (void)hipFree(box);
+  (void)hipFree(cost);
   (void)hipFree(tmp);
   return hipSuccess;
 }

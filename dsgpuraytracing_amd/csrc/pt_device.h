@@ -41,6 +41,9 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #ifndef PT_STACK
 #define PT_STACK 24  // traversal stack entries per lane in LDS (lane-contiguous)
 #endif
+#ifndef PT_SCALAR_BLOCKS
+#define PT_SCALAR_BLOCKS 0  // 1: refill block records through the scalar cache (A/B)
+#endif
 #ifndef PT_FIXED_ACC
 #define PT_FIXED_ACC 0  // 1: exact fixed-point pixel sums by no-return atomics (A/B)
 #endif

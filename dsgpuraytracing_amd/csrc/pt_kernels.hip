@@ -646,7 +646,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   if (STATS && lane <= S_N) s_clk[lane] = lane == S_N ? clock64() : 0ull;
   __syncthreads();
 #define PT_STAMP(k)                                                  \
-  if (STATS) {                                                       \
+  if constexpr (STATS) {                                             \
     const unsigned long long t_ = clock64();                         \
     if (lane == __builtin_amdgcn_readfirstlane(lane)) {              \
       s_clk[k] += t_ - s_clk[S_N];                                   \
@@ -978,6 +978,30 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             if (STATS) n_atomics += lane == 0;
           }
         }
+#if PT_SCALAR_BLOCKS
+        // A chunk of 128 slots (128-aligned) lies inside one 8x8 block when a
+        // block holds a multiple of 128 slots (n_groups a power of two >= 2),
+        // and the lanes are served from at most two chunks -- the rest of the
+        // old one and the new one: both block records are read through the
+        // scalar cache (wave-uniform addresses) instead of one vector-memory
+        // load per lane, which every refill round would wait on.
+        const bool sblocks = P.ngroup_shift >= 1;
+        int4 b_old = make_int4(0, 0, 0, 0), b_new = make_int4(0, 0, 0, 0);
+        if (sblocks) {
+          typedef __attribute__((address_space(4))) const pt_v4i cst_v4i;
+          const cst_v4i* cb = (const cst_v4i*)P.blocks;
+          const uint32_t sh = (uint32_t)P.ngroup_shift + 6u;  // slot -> block index
+          const uint32_t last = total_slots > 0u ? (total_slots - 1u) >> sh : 0u;
+          if (avail > 0u) {
+            const pt_v4i v = cb[min(chunk_next >> sh, last)];
+            b_old = make_int4(v.x, v.y, v.z, v.w);
+          }
+          if (cnt > avail) {
+            const pt_v4i v = cb[min(nbase >> sh, last)];
+            b_new = make_int4(v.x, v.y, v.z, v.w);
+          }
+        }
+#endif
         if (need) {
           uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
           uint32_t slot = rank < avail ? chunk_next + rank : nbase + (rank - avail);
@@ -992,7 +1016,13 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             // resolve_kernel: every ray through them misses the root box).
             uint32_t bq = pixel_of_slot(slot);
             uint32_t g = slot - bq * n_groups;
+#if PT_SCALAR_BLOCKS
+            int4 b;
+            if (sblocks) b = rank < avail ? b_old : b_new;
+            else b = P.blocks[bq >> 6];
+#else
             int4 b = P.blocks[bq >> 6];
+#endif
             int qx = (int)(bq & 7u), qy = (int)((bq >> 3) & 7u);
             if (qx < b.z && qy < b.w) {
               pix = (b.x + qx) | ((b.y + qy) << 16);

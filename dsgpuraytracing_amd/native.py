@@ -114,6 +114,7 @@ _SIGS = {
     "pt_get_wave_trace": (c_int32, [c_void_p, c_void_p, c_int64, POINTER(c_int64)]),
     "pt_last_error": (c_char_p, []),
     "pt_to_color": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p]),
+    "pt_to_color_check": (c_int64, [c_uint32, c_uint32]),
     # include/ptgpu_scene.h (bound with full types in scene_loader.py)
     "pt_host_scene_load": (c_int32, [c_char_p, c_int32, c_int32, c_char_p, POINTER(c_void_p)]),
     "pt_host_scene_view": (c_int32, [c_void_p, c_void_p, c_void_p]),

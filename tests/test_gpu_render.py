@@ -50,6 +50,7 @@ def near_exact_report(a, b):
     ("CBspheres_lambertian_ambientlight_64x64", 64, 64, 4, 4, 2, 3), # hemisphere light, 2 samples
     ("c1_default_64x64", 64, 64, 4, 0, 1, 1),                        # max_ray_depth 0: direct only
     ("c1_default_64x64", 64, 64, 4, 1, 4, 1),                        # AppConfig defaults: -m 1 -l 4
+    ("c1_default_64x64", 64, 64, 4, 4, 3, 2),                        # -l 3: light-sample weight 1/3 (not a power of two)
     ("c1env_64x64", 64, 64, 4, 4, 1, 3),                             # + environment light (-e)
     ("c1env_64x64", 64, 64, 4, 4, 2, 4),
     ("CBspheresenv_64x64", 64, 64, 4, 4, 1, 3),                      # env seen through mirror / glass

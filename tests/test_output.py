@@ -74,3 +74,29 @@ def test_save_image_rows_match_reference(tmp_path):
     assert np.array_equal(_pack(png).reshape(-1), ref["png_rows"])
     write_png(str(tmp_path / "direct.png"), to_color(hdr)[::-1])
     assert open(path, "rb").read() == open(str(tmp_path / "direct.png"), "rb").read()
+
+
+def test_to_color_table_exact_on_every_float():
+    """pt_to_color reads each channel's 8-bit code from a table of the code's
+    255 steps (image_out.cpp); it must equal the direct evaluation
+    code8(powf(s * exposure, 1/2.2)) -- the reference arithmetic -- on EVERY
+    non-negative float up to +inf (2^31 - 2^23 + 1 bit patterns; negatives and
+    NaN take the direct path).  8 threads, about 10 s."""
+    import threading
+
+    from dsgpuraytracing_amd import native
+    L = native.lib()
+    end = 0x7f800001
+    n = 8
+    cuts = [end * k // n for k in range(n + 1)]
+    bad = [None] * n
+
+    def run(k):
+        bad[k] = L.pt_to_color_check(cuts[k], cuts[k + 1])
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert bad == [0] * n, bad
