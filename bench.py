@@ -296,6 +296,8 @@ def main():
                     help="N > 1: strong = one frame's tiles split across the GPUs + one RCCL gather (default); "
                          "weak = one pass of the whole frame per GPU over disjoint sample ranges + one RCCL reduce")
     args = ap.parse_args()
+    if os.environ.get("PT_BENCH_LBVH") == "1":  # A/B arms (tools/ab.sh): the GPU-built tree
+        args.lbvh = True
 
     import torch
     import torch.distributed as dist
@@ -501,7 +503,7 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
                        "parallelism": (f"samples{world}" if weak else f"tiles{world}") if world > 1 else "single",
                        "render_time_s": round(elapsed / frames, 4), "scene_load_s": round(t_load, 3),
                        "single_frame_ms": None if single_ms is None else round(single_ms, 3),
-                       "bvh": "gpu-lbvh" if args.lbvh else ("reference-sah (host)" if os.environ.get("PT_BVH_BUILD") == "ref" else "own binned SAH, 128 bins, C_isect 1 (host)"),
+                       "bvh": bvh_desc(args.lbvh),
                        "upload_s": round(t_up, 4),
                        "host_output_ms_per_frame": None if host_ms is None else round(host_ms, 3)},
             "roofline": roofline(workload, elapsed / frames * 1e3, algorithmic_bytes(st_counts), isolated_ms=iso_ms,
@@ -550,6 +552,19 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
         print(json.dumps(out), flush=True)
 
 
+def bvh_desc(lbvh=False):
+    """The render tree a run traces (pt_api.cpp upload_impl)."""
+    b = os.environ.get("PT_BVH_BUILD")
+    if lbvh:
+        return "gpu-lbvh via pt_upload_scene_lbvh (Karras + treelet restructuring, device-built)"
+    if b == "ref":
+        return "the caller's reference tree (BVHAccel, host)"
+    if b == "sah":
+        return "own binned SAH, 128 bins, C_isect 1 (host)"
+    return ("own GPU-built tree: Karras LBVH + %s treelet-restructuring passes (device)"
+            % os.environ.get("PT_LBVH_PASSES", "3"))
+
+
 def s_get(dev, key):
     return dev.stats().get(key)
 
@@ -563,8 +578,8 @@ def companions(dev0, local, stream, frames):
         multi-GPU (C4, strong) scaling curve;
       * c5_single_gpu: BASELINE C5 (glass/mirror proxy + environment light)
         on this one GPU;
-      * c3_lbvh: the headline workload over the GPU-built LBVH
-        (pt_upload_scene_lbvh) instead of the host SAH tree;
+      * c3_host_sah: the headline workload over the host binned-SAH tree
+        (PT_BVH_BUILD=sah) instead of the default GPU-built tree;
       * c3_per_tile / c3_per_tile_sync: the headline frame driven through the
         reference's literal seam -- 8 worker threads calling raytrace_tile
         once per 32x32 tile (1,024 calls, pathtracer.cpp:585-621) through one
@@ -577,16 +592,25 @@ def companions(dev0, local, stream, frames):
 
     from dsgpuraytracing_amd.pathtracer import Device, Scene, tile_fifo
     res = {}
-    names = {"c3f": "c3_framed", "c4": "c4_single_gpu", "c5": "c5_single_gpu", "c3": "c3_lbvh"}
+    names = {"c3f": "c3_framed", "c4": "c4_single_gpu", "c5": "c5_single_gpu", "c3": "c3_host_sah"}
     for name in ("c3f", "c4", "c5", "c3"):
         wl = WORKLOADS[name]
-        lbvh = name == "c3"
+        host_sah = name == "c3"
         dae, envmap, cam = workload_scene(wl)
         sc = Scene.from_dae(dae, wl["w"], wl["h"], cam_info=cam, envmap=envmap)
         dev = Device(local)
+        old = os.environ.get("PT_BVH_BUILD")
+        if host_sah:
+            os.environ["PT_BVH_BUILD"] = "sah"
         t_up = time.perf_counter()
-        dev.upload_scene(sc, gpu_bvh=lbvh)
+        dev.upload_scene(sc)
         t_up = time.perf_counter() - t_up
+        bvh = bvh_desc()
+        if host_sah:
+            if old is None:
+                del os.environ["PT_BVH_BUILD"]
+            else:
+                os.environ["PT_BVH_BUILD"] = old
         dev.set_camera(sc.camera)
         dev.set_params(wl["w"], wl["h"], wl["spp"], DEPTH, NSL, SEED)
         tl = np.asarray(tile_fifo(wl["w"], wl["h"]), np.int32)
@@ -607,7 +631,7 @@ def companions(dev0, local, stream, frames):
             "unit": "Mrays/s", "ms_per_step": round(el / frames * 1e3, 3), "kernel_ms": round(float(np.mean(k)), 3),
             "frames": frames, "culled_samples": st["culled_samples"],
             "ray_casts_per_s_M": round(rays * frames / el / 1e6, 1), "upload_s": round(t_up, 4),
-            "bvh": "gpu-lbvh" if lbvh else "own binned SAH (host)"}
+            "bvh": bvh}
         dev.close()
         del fr
     res.update(per_tile_companions(local))

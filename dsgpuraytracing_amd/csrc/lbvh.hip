@@ -80,6 +80,8 @@ struct Params {
   int* collapsed;       // 1: internal node i becomes one leaf of its <= kMaxLeaf primitives
   int* flag;            // arrivals per internal node (bottom-up passes)
   int* pos;             // final position of sorted primitive j (depth-first leaf order)
+  float ci;             // SAH cost of a primitive test (a traversal step costs 1)
+  int max_leaf;         // most primitives in one leaf (<= kMaxLeaf)
 };
 
 // Relaxed agent-scope accesses for tree data shared between the climbing
@@ -171,8 +173,8 @@ __device__ __forceinline__ void child_box(const Params& P, int c, float lo[3], f
 
 // SAH over the binary tree, as the host render tree (render_tree.cpp): one
 // unit per traversal step, one per primitive test, leaves of <= 4 primitives.
-constexpr float kCt = 1.0f, kCi = 1.0f;
-constexpr int kMaxLeaf = 4;
+constexpr float kCt = 1.0f;
+constexpr int kMaxLeaf = 8;  // leaf cursors hold <= 8 primitives; P.max_leaf (default 4) is the SAH's limit
 constexpr int kTreelet = 7;  // treelet leaves (Karras & Aila: 7)
 constexpr int kDpBlock = 64;  // threads per block of the restructuring pass (LDS tables per thread)
 
@@ -182,7 +184,7 @@ __device__ __forceinline__ float half_area(const float lo[3], const float hi[3])
 }
 __device__ __forceinline__ int node_count(const Params& P, int c) { return c < 0 ? 1 : ald(&P.range[c]); }
 __device__ __forceinline__ float node_cost(const Params& P, int c, const float lo[3], const float hi[3]) {
-  return c < 0 ? kCi * half_area(lo, hi) : ald(&P.cost[c]);
+  return c < 0 ? P.ci * half_area(lo, hi) : ald(&P.cost[c]);
 }
 
 // Bottom-up pass (propogateBBox, helper.cu:437-458, extended): one thread per
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(kDpBlock) void k_treelet(Params P, int optimize) {
           if (sub == 0) break;
         }
         const float csplit = kCt * a + best;
-        const float cleaf = n <= kMaxLeaf ? kCi * a * (float)n : INFINITY;
+        const float cleaf = n <= P.max_leaf ? P.ci * a * (float)n : INFINITY;
         pick_at(S) = (uint8_t)bp;
         if (cleaf <= csplit) {
           cost_at(S) = cleaf;
@@ -338,7 +340,7 @@ __global__ __launch_bounds__(kDpBlock) void k_treelet(Params P, int optimize) {
       }
       const float a = half_area(blo, bhi);
       const float csplit = kCt * a + node_cost(P, c0, la, ha) + node_cost(P, c1, lb, hb);
-      const float cleaf = cnt <= kMaxLeaf ? kCi * a * (float)cnt : INFINITY;
+      const float cleaf = cnt <= P.max_leaf ? P.ci * a * (float)cnt : INFINITY;
       ast(&P.range[node], cnt);
       ast(&P.cost[node], fminf(csplit, cleaf));
       ast(&P.collapsed[node], cleaf <= csplit ? 1 : 0);
@@ -510,8 +512,12 @@ extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t
     P.smin[k] = in->scene_min[k];
     P.sext[k] = in->scene_extent[k];
   }
-  int passes = 2;  // treelet-restructuring passes (0: the reference's Karras tree, SAH leaf collapse)
+  int passes = 3;  // treelet-restructuring passes (0: the reference's Karras tree, SAH leaf collapse)
   if (const char* e = std::getenv("PT_LBVH_PASSES")) passes = std::max(0, std::min(8, std::atoi(e)));
+  P.ci = 1.0f;      // the host SAH tree's costs (render_tree.cpp)
+  P.max_leaf = 4;
+  if (const char* e = std::getenv("PT_LBVH_CI")) P.ci = std::max(0.05f, std::min(8.0f, (float)std::atof(e)));  // tuning knobs
+  if (const char* e = std::getenv("PT_LBVH_MAXLEAF")) P.max_leaf = std::max(1, std::min(kMaxLeaf, std::atoi(e)));
   // scratch
   uint32_t *keys_a = nullptr, *keys_b = nullptr;
   int *ids_a = nullptr, *ids_b = nullptr, *ints = nullptr;

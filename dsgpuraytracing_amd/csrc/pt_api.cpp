@@ -618,8 +618,17 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
   pt_scene ps;
   const pt_scene* const s0 = s;  // the caller's scene (reference BVH order)
   int rc0 = 0;
-  const char* bb = std::getenv("PT_BVH_BUILD");  // "ref": render over the reference's own tree
-  if (!gpu_bvh && !(bb && std::strcmp(bb, "ref") == 0)) {
+  // The render tree: by default this library's GPU-built
+  // tree (Karras LBVH + treelet restructuring, lbvh.hip) over the caller's
+  // primitives; PT_BVH_BUILD=sah: the host binned-SAH tree; =ref: the
+  // caller's own (reference) tree.  pt_upload_scene_lbvh always builds on
+  // the GPU.  The reference-count launch walks the caller's tree in every case
+  // but pt_upload_scene_lbvh's.
+  const char* bb = std::getenv("PT_BVH_BUILD");
+  const bool host_sah = bb && std::strcmp(bb, "sah") == 0;
+  const bool ref_tree = bb && std::strcmp(bb, "ref") == 0;
+  const bool gpu_tree = !gpu_bvh && !host_sah && !ref_tree;
+  if (!gpu_bvh && host_sah) {
     sah_nodes.resize((size_t)std::max<int64_t>(1, 2 * s->n_prims - 1));
     perm.resize((size_t)s->n_prims);
     int64_t nn = 0;
@@ -738,7 +747,25 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
     HIPCHK(hipMemcpy(c->prims_ref.p, prims0.data(), prims0.size() * sizeof(DPrim), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->norms_ref.p, norms0.data(), norms0.size() * sizeof(float), hipMemcpyHostToDevice));
   }
-  if (!gpu_bvh) {
+  if (gpu_tree) {
+    // the caller's tree: validated, kept as the binary nodes of the
+    // reference-count launch over a caller-order copy of the primitives
+    std::vector<DNode> dn0;
+    std::vector<DNode2> d2;
+    int ms0 = 0;
+    if (int rc = build_host_bvh(s0, dn0, d2, ms0)) return rc;
+    HIPCHK(c->prims_ref.reserve(prims.size()));
+    HIPCHK(c->norms_ref.reserve(norms.size()));
+    HIPCHK(hipMemcpy(c->prims_ref.p, prims.data(), prims.size() * sizeof(DPrim), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->norms_ref.p, norms.data(), norms.size() * sizeof(float), hipMemcpyHostToDevice));
+    if (int rc = build_gpu_bvh(c, s0)) return rc;  // adopts prims/norms/prim_map/nodes in its own order
+    HIPCHK(c->nodes2.reserve(d2.size()));
+    HIPCHK(hipMemcpy(c->nodes2.p, d2.data(), d2.size() * sizeof(DNode2), hipMemcpyHostToDevice));
+    c->bvh_stack = std::max(c->bvh_stack, ms0);
+    if (c->bvh_stack > PT_STACK_MAX)
+      return fail(PT_E_INVALID, "pt_upload_scene: BVH needs a deeper traversal stack (" +
+                                    std::to_string(c->bvh_stack) + " > " + std::to_string(PT_STACK_MAX) + ")");
+  } else if (!gpu_bvh) {
     std::vector<DNode> dn;
     std::vector<DNode2> d2;
     int max_stack = 0;
