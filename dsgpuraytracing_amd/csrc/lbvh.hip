@@ -176,7 +176,6 @@ __device__ __forceinline__ void child_box(const Params& P, int c, float lo[3], f
 constexpr float kCt = 1.0f;
 constexpr int kMaxLeaf = 8;  // leaf cursors hold <= 8 primitives; P.max_leaf (default 4) is the SAH's limit
 constexpr int kTreelet = 7;  // treelet leaves (Karras & Aila: 7)
-constexpr int kDpBlock = 64;  // threads per block of the restructuring pass (LDS tables per thread)
 
 __device__ __forceinline__ float half_area(const float lo[3], const float hi[3]) {
   const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
@@ -187,165 +186,185 @@ __device__ __forceinline__ float node_cost(const Params& P, int c, const float l
   return c < 0 ? P.ci * half_area(lo, hi) : ald(&P.cost[c]);
 }
 
-// Bottom-up pass (propogateBBox, helper.cu:437-458, extended): one thread per
-// primitive climbs until it is the first to reach a node; the second arrival
-// owns the node, whose children are final.  It sets the node's box, count,
-// SAH cost and leaf-collapse choice -- and with `optimize`, for nodes with
-// >= kTreelet primitives, first rebuilds the node's treelet SAH-optimally.
-__global__ __launch_bounds__(kDpBlock) void k_treelet(Params P, int optimize) {
-  // per-thread DP tables (lane-strided: conflict-free)
-  __shared__ float s_cost[128 * kDpBlock];
-  __shared__ uint8_t s_pick[128 * kDpBlock];
-  const int tid = threadIdx.x;
-  auto cost_at = [&](int S) -> float& { return s_cost[S * kDpBlock + tid]; };
-  auto pick_at = [&](int S) -> uint8_t& { return s_pick[S * kDpBlock + tid]; };
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= P.n || P.n < 2) return;
-  int node = ald(&P.parent[(P.n - 1) + j]);
-  while (node >= 0) {
-    if (__hip_atomic_fetch_add(&P.flag[node], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
-    const int c0 = ald(&P.child[2 * node]), c1 = ald(&P.child[2 * node + 1]);
-    const int cnt = node_count(P, c0) + node_count(P, c1);
-    if (optimize && cnt >= kTreelet) {
-      // ---- the treelet: expand the largest-area internal treelet leaf
-      int leaf[kTreelet], inner[kTreelet - 1];
-      float lo[kTreelet][3], hi[kTreelet][3];
-      int nl = 2, ni = 1;
-      leaf[0] = c0;
-      leaf[1] = c1;
-      inner[0] = node;
-      child_box(P, c0, lo[0], hi[0]);
-      child_box(P, c1, lo[1], hi[1]);
-      while (nl < kTreelet) {
-        int best = -1;
-        float ba = -1.0f;
-        for (int i = 0; i < nl; ++i)
-          if (leaf[i] >= 0) {
-            const float a = half_area(lo[i], hi[i]);
-            if (a > ba) {
-              ba = a;
-              best = i;
-            }
-          }
-        if (best < 0) break;
-        const int x = leaf[best];
-        inner[ni++] = x;
-        leaf[best] = ald(&P.child[2 * x]);
-        leaf[nl] = ald(&P.child[2 * x + 1]);
-        child_box(P, leaf[best], lo[best], hi[best]);
-        child_box(P, leaf[nl], lo[nl], hi[nl]);
-        ++nl;
-      }
-      float lcost[kTreelet];
-      int lcnt[kTreelet];
-      for (int i = 0; i < nl; ++i) {
-        lcost[i] = node_cost(P, leaf[i], lo[i], hi[i]);
-        lcnt[i] = node_count(P, leaf[i]);
-      }
-      // ---- DP over the leaf subsets in increasing order (a proper subset
-      // of S is numerically smaller than S)
-      const int full = (1 << nl) - 1;
-      unsigned long long coll_lo = 0ull, coll_hi = 0ull;  // subsets better as one leaf
-      for (int S = 1; S <= full; ++S) {
-        const int low = S & -S;
-        if (S == low) {
-          cost_at(S) = lcost[__ffs(S) - 1];
-          continue;
-        }
-        float blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
-        int n = 0;
-        for (int i = 0; i < nl; ++i)
-          if (S & (1 << i)) {
-            n += lcnt[i];
-            for (int k = 0; k < 3; ++k) {
-              blo[k] = fminf(blo[k], lo[i][k]);
-              bhi[k] = fmaxf(bhi[k], hi[i][k]);
-            }
-          }
-        const float a = half_area(blo, bhi);
-        // partitions (P, S \ P) with P holding S's lowest leaf: each once
-        const int rest = S ^ low;
-        float best = INFINITY;
-        int bp = low;
-        for (int sub = (rest - 1) & rest;; sub = (sub - 1) & rest) {
-          const int Pm = low | sub;
-          const float c = cost_at(Pm) + cost_at(S ^ Pm);
-          if (c < best) {
-            best = c;
-            bp = Pm;
-          }
-          if (sub == 0) break;
-        }
-        const float csplit = kCt * a + best;
-        const float cleaf = n <= P.max_leaf ? P.ci * a * (float)n : INFINITY;
-        pick_at(S) = (uint8_t)bp;
-        if (cleaf <= csplit) {
-          cost_at(S) = cleaf;
-          if (S < 64) coll_lo |= 1ull << S;
-          else coll_hi |= 1ull << (S - 64);
-        } else {
-          cost_at(S) = csplit;
+// Box, count, SAH cost and leaf-collapse choice of internal node `node` from
+// its (final) children.
+__device__ void node_update(const Params& P, int node, int c0, int c1, int cnt) {
+  float la[3], ha[3], lb[3], hb[3], blo[3], bhi[3];
+  child_box(P, c0, la, ha);
+  child_box(P, c1, lb, hb);
+  for (int k = 0; k < 3; ++k) {
+    blo[k] = fminf(la[k], lb[k]);
+    bhi[k] = fmaxf(ha[k], hb[k]);
+    ast(&P.box[6 * node + k], blo[k]);
+    ast(&P.box[6 * node + 3 + k], bhi[k]);
+  }
+  const float a = half_area(blo, bhi);
+  const float csplit = kCt * a + node_cost(P, c0, la, ha) + node_cost(P, c1, lb, hb);
+  const float cleaf = cnt <= P.max_leaf ? P.ci * a * (float)cnt : INFINITY;
+  ast(&P.range[node], cnt);
+  ast(&P.cost[node], fminf(csplit, cleaf));
+  ast(&P.collapsed[node], cleaf <= csplit ? 1 : 0);
+}
+
+// SAH-optimal rebuild of the treelet rooted at R (wave-uniform), by the whole
+// wave: the treelet is R's kTreelet largest-area descendants (leaves); the DP
+// over the leaf subsets runs one subset size at a time, the subsets of one
+// size on parallel lanes, each lane scanning its subset's partitions; lane 0
+// then rewrites the treelet's internal nodes from the DP choices.
+__device__ void treelet_wave(const Params& P, int R, int lane, float* s_cost, uint8_t* s_pick, uint8_t* s_coll) {
+  int leaf[kTreelet], inner[kTreelet - 1];
+  float lo[kTreelet][3], hi[kTreelet][3];
+  int nl = 2, ni = 1;
+  leaf[0] = ald(&P.child[2 * R]);
+  leaf[1] = ald(&P.child[2 * R + 1]);
+  inner[0] = R;
+  child_box(P, leaf[0], lo[0], hi[0]);
+  child_box(P, leaf[1], lo[1], hi[1]);
+  while (nl < kTreelet) {
+    int best = -1;
+    float ba = -1.0f;
+    for (int i = 0; i < nl; ++i)
+      if (leaf[i] >= 0) {
+        const float a = half_area(lo[i], hi[i]);
+        if (a > ba) {
+          ba = a;
+          best = i;
         }
       }
-      // ---- rebuild the treelet top-down from the DP choices, reusing its
-      // internal nodes (the treelet root keeps its index and its parent)
-      int stk_s[kTreelet], stk_x[kTreelet], sp = 0, next = 1;
-      stk_s[sp] = full;
-      stk_x[sp++] = node;
-      while (sp > 0) {
-        --sp;
-        const int S = stk_s[sp], x = stk_x[sp];
-        const int parts[2] = {pick_at(S), S ^ pick_at(S)};
-        for (int side = 0; side < 2; ++side) {
-          const int sub = parts[side];
-          int c;
-          if ((sub & (sub - 1)) == 0) {
-            c = leaf[__ffs(sub) - 1];
-          } else {
-            c = inner[next++];
-            stk_s[sp] = sub;
-            stk_x[sp++] = c;
+    if (best < 0) break;
+    const int x = leaf[best];
+    inner[ni++] = x;
+    leaf[best] = ald(&P.child[2 * x]);
+    leaf[nl] = ald(&P.child[2 * x + 1]);
+    child_box(P, leaf[best], lo[best], hi[best]);
+    child_box(P, leaf[nl], lo[nl], hi[nl]);
+    ++nl;
+  }
+  float lcost[kTreelet];
+  int lcnt[kTreelet];
+  for (int i = 0; i < nl; ++i) {
+    lcost[i] = node_cost(P, leaf[i], lo[i], hi[i]);
+    lcnt[i] = node_count(P, leaf[i]);
+  }
+  const int full = (1 << nl) - 1;
+  if (lane < nl) s_cost[1 << lane] = lcost[lane];
+  __syncthreads();
+  for (int k = 2; k <= nl; ++k) {
+    for (int S = lane + 1; S <= full; S += 64) {
+      if (__popc(S) != k) continue;
+      float blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+      int n = 0;
+      for (int i = 0; i < nl; ++i)
+        if (S & (1 << i)) {
+          n += lcnt[i];
+          for (int q = 0; q < 3; ++q) {
+            blo[q] = fminf(blo[q], lo[i][q]);
+            bhi[q] = fmaxf(bhi[q], hi[i][q]);
           }
-          ast(&P.child[2 * x + side], c);
-          ast(&P.parent[c >= 0 ? c : (P.n - 1) + ~c], x);
         }
-        float blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
-        int n = 0;
-        for (int i = 0; i < nl; ++i)
-          if (S & (1 << i)) {
-            n += lcnt[i];
-            for (int k = 0; k < 3; ++k) {
-              blo[k] = fminf(blo[k], lo[i][k]);
-              bhi[k] = fmaxf(bhi[k], hi[i][k]);
-            }
-          }
-        for (int k = 0; k < 3; ++k) {
-          ast(&P.box[6 * x + k], blo[k]);
-          ast(&P.box[6 * x + 3 + k], bhi[k]);
-        }
-        ast(&P.range[x], n);
-        ast(&P.cost[x], cost_at(S));
-        const bool cl = S < 64 ? ((coll_lo >> S) & 1ull) : ((coll_hi >> (S - 64)) & 1ull);
-        ast(&P.collapsed[x], cl ? 1 : 0);
-      }
-    } else {
-      float la[3], ha[3], lb[3], hb[3], blo[3], bhi[3];
-      child_box(P, c0, la, ha);
-      child_box(P, c1, lb, hb);
-      for (int k = 0; k < 3; ++k) {
-        blo[k] = fminf(la[k], lb[k]);
-        bhi[k] = fmaxf(ha[k], hb[k]);
-        ast(&P.box[6 * node + k], blo[k]);
-        ast(&P.box[6 * node + 3 + k], bhi[k]);
-      }
       const float a = half_area(blo, bhi);
-      const float csplit = kCt * a + node_cost(P, c0, la, ha) + node_cost(P, c1, lb, hb);
-      const float cleaf = cnt <= P.max_leaf ? P.ci * a * (float)cnt : INFINITY;
-      ast(&P.range[node], cnt);
-      ast(&P.cost[node], fminf(csplit, cleaf));
-      ast(&P.collapsed[node], cleaf <= csplit ? 1 : 0);
+      // partitions (P, S \ P) with P holding S's lowest leaf: each once
+      const int low = S & -S, rest = S ^ low;
+      float best = INFINITY;
+      int bp = low;
+      for (int sub = (rest - 1) & rest;; sub = (sub - 1) & rest) {
+        const int Pm = low | sub;
+        const float c = s_cost[Pm] + s_cost[S ^ Pm];
+        if (c < best) {
+          best = c;
+          bp = Pm;
+        }
+        if (sub == 0) break;
+      }
+      const float csplit = kCt * a + best;
+      const float cleaf = n <= P.max_leaf ? P.ci * a * (float)n : INFINITY;
+      s_pick[S] = (uint8_t)bp;
+      s_coll[S] = cleaf <= csplit ? 1 : 0;
+      s_cost[S] = fminf(csplit, cleaf);
     }
-    node = ald(&P.parent[node]);
+    __syncthreads();
+  }
+  if (lane == 0) {
+    // rebuild top-down, reusing the treelet's internal nodes (the root keeps
+    // its index and its parent)
+    int stk_s[kTreelet], stk_x[kTreelet], sp = 0, next = 1;
+    stk_s[sp] = full;
+    stk_x[sp++] = R;
+    while (sp > 0) {
+      --sp;
+      const int S = stk_s[sp], x = stk_x[sp];
+      const int parts[2] = {s_pick[S], S ^ s_pick[S]};
+      for (int side = 0; side < 2; ++side) {
+        const int sub = parts[side];
+        int c;
+        if ((sub & (sub - 1)) == 0) {
+          c = leaf[__ffs(sub) - 1];
+        } else {
+          c = inner[next++];
+          stk_s[sp] = sub;
+          stk_x[sp++] = c;
+        }
+        ast(&P.child[2 * x + side], c);
+        ast(&P.parent[c >= 0 ? c : (P.n - 1) + ~c], x);
+      }
+      float blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+      int n = 0;
+      for (int i = 0; i < nl; ++i)
+        if (S & (1 << i)) {
+          n += lcnt[i];
+          for (int q = 0; q < 3; ++q) {
+            blo[q] = fminf(blo[q], lo[i][q]);
+            bhi[q] = fmaxf(bhi[q], hi[i][q]);
+          }
+        }
+      for (int q = 0; q < 3; ++q) {
+        ast(&P.box[6 * x + q], blo[q]);
+        ast(&P.box[6 * x + 3 + q], bhi[q]);
+      }
+      ast(&P.range[x], n);
+      ast(&P.cost[x], s_cost[S]);
+      ast(&P.collapsed[x], (int)s_coll[S]);
+    }
+  }
+  __syncthreads();  // the tables are reused by the wave's next treelet
+}
+
+// Bottom-up pass (propogateBBox, helper.cu:437-458, extended): one lane per
+// primitive climbs until it is the first to reach a node; the second arrival
+// owns the node, whose children are final, and sets its box, count, SAH cost
+// and leaf-collapse choice -- with `optimize`, for nodes with >= kTreelet
+// primitives, after the wave has rebuilt the node's treelet.  Lanes stay in
+// the loop (idle) until every lane of the wave has finished climbing, so the
+// whole wave takes part in every treelet's DP.  One wave per workgroup.
+__global__ __launch_bounds__(64) void k_treelet(Params P, int optimize) {
+  __shared__ float s_cost[128];
+  __shared__ uint8_t s_pick[128], s_coll[128];
+  const int lane = threadIdx.x;
+  const int j = blockIdx.x * 64 + lane;
+  bool active = j < P.n && P.n >= 2;
+  int node = active ? ald(&P.parent[(P.n - 1) + j]) : -1;
+  for (;;) {
+    if (active) {
+      if (node < 0) active = false;
+      else if (__hip_atomic_fetch_add(&P.flag[node], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        active = false;  // the first arrival: the sibling subtree is not finished
+    }
+    if (__ballot(active) == 0ull) break;
+    int c0 = 0, c1 = 0, cnt = 0;
+    if (active) {
+      c0 = ald(&P.child[2 * node]);
+      c1 = ald(&P.child[2 * node + 1]);
+      cnt = node_count(P, c0) + node_count(P, c1);
+    }
+    const bool opt = active && optimize && cnt >= kTreelet;
+    unsigned long long m = __ballot(opt);
+    while (m != 0ull) {
+      const int l = __ffsll((long long)m) - 1;
+      m &= m - 1ull;
+      treelet_wave(P, __shfl(node, l), lane, s_cost, s_pick, s_coll);
+    }
+    if (active && !opt) node_update(P, node, c0, c1, cnt);
+    if (active) node = ald(&P.parent[node]);
   }
 }
 
@@ -599,12 +618,11 @@ extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t
     hipLaunchKernelGGL(k_internal, dim3(gi), dim3(B), 0, s, P);
     LB_CHK(hipGetLastError());
     // bottom-up: boxes, counts, SAH costs, leaf collapse; then the treelet passes
-    const int gt = (n + kDpBlock - 1) / kDpBlock;
-    hipLaunchKernelGGL(k_treelet, dim3(gt), dim3(kDpBlock), 0, s, P, 0);
-    LB_CHK(hipGetLastError());
-    for (int p = 0; p < passes; ++p) {
-      LB_CHK(hipMemsetAsync(P.flag, 0, ni * 4, s));
-      hipLaunchKernelGGL(k_treelet, dim3(gt), dim3(kDpBlock), 0, s, P, 1);
+    // (the first pass sets every node's box and cost on its way up too)
+    const int gt = (n + 63) / 64;
+    for (int p = 0; p < std::max(1, passes); ++p) {
+      if (p > 0) LB_CHK(hipMemsetAsync(P.flag, 0, ni * 4, s));
+      hipLaunchKernelGGL(k_treelet, dim3(gt), dim3(64), 0, s, P, passes > 0 ? 1 : 0);
       LB_CHK(hipGetLastError());
     }
     // top-down BVH4 emission (breadth first, binary node 0 -> BVH4 node 0),

@@ -98,6 +98,10 @@ def test_lbvh_treelet_restructuring_keeps_nearest_hits(monkeypatch, passes):
     maxt = rng.uniform(0.1, 3.0, m)
     res = []
     for gpu in (False, True):
+        if gpu:
+            monkeypatch.delenv("PT_BVH_BUILD", raising=False)
+        else:  # the host binned-SAH tree
+            monkeypatch.setenv("PT_BVH_BUILD", "sah")
         dev = Device(0)
         dev.upload_scene(sc, gpu_bvh=gpu)
         res.append(dev.intersect(o, dr, maxt))
@@ -110,7 +114,9 @@ def test_lbvh_treelet_restructuring_keeps_nearest_hits(monkeypatch, passes):
     # shared-edge triangles: which one a tree reports first is the tree's)
     assert ((p0[both] == p1[both]) | (t0[both] == t1[both])).mean() >= 0.9995
     assert np.allclose(t0[both], t1[both], rtol=1e-6, atol=0)
+    monkeypatch.setenv("PT_BVH_BUILD", "sah")
     a, sa = _render(sc, 128, 128, 4, 9, gpu_bvh=False)
+    monkeypatch.delenv("PT_BVH_BUILD", raising=False)
     b, sb = _render(sc, 128, 128, 4, 9, gpu_bvh=True)
     assert _close(b, a) >= 0.999
     print(f"passes {passes}: BVH4 nodes {sb['bvh_nodes']} (host {sa['bvh_nodes']}), node visits {sb['node_visits']} "
