@@ -177,7 +177,6 @@ struct pt_ctx {
   DevBuf<int4> blocks[kSlots];           // footprint-clipped 8x8 pixel blocks of the tiles
   std::vector<int4> blocks_host[kSlots];
   DevBuf<float> partial[kSlots];   // per-slot sample-group sums
-  DevBuf<unsigned long long> accum[kSlots];  // PT_FIXED_ACC: per-slot exact pixel sums (kept zeroed)
   DevBuf<int> spill[kSlots];       // traversal stack entries beyond PT_STACK
   DevBuf<uint32_t> counter[kSlots];
   int64_t culled_px = 0;         // pixels of the last launch outside the footprint
@@ -286,7 +285,6 @@ int pt_destroy(pt_ctx* c) {
     c->blocks[k].release();
     c->spill[k].release();
     c->partial[k].release();
-    c->accum[k].release();
     c->counter[k].release();
     if (c->ev_free[k]) (void)hipEventDestroy(c->ev_free[k]);
     if (c->rstream[k]) (void)hipStreamDestroy(c->rstream[k]);
@@ -1082,18 +1080,9 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   const int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
   if (slots + want * PT_CHUNK_MAX >= (int64_t)UINT32_MAX || npx * P.n_groups >= (int64_t)UINT32_MAX)
     return fail(PT_E_INVALID, "frame too large for one launch");
-#if PT_FIXED_ACC
-  if (c->accum[slot].n < (size_t)npx * 3) {  // zeroed once; every resolve leaves its pixels zeroed
-    HIPCHK(c->accum[slot].reserve((size_t)npx * 3));
-    HIPCHK(hipMemsetAsync(c->accum[slot].p, 0, (size_t)npx * 3 * sizeof(unsigned long long), rs));
-  }
-  P.accum = c->accum[slot].p;
-  c->last.partial_bytes = (int64_t)npx * 24;
-#else
   HIPCHK(c->partial[slot].reserve((size_t)(npx * P.n_groups) * 3));
   P.partial = c->partial[slot].p;
   c->last.partial_bytes = (int64_t)npx * P.n_groups * 12;
-#endif
   auto log2_exact = [](int v) {  // log2(v) for a power of two, else -1
     int k = 0;
     while ((1 << k) < v && k < 30) ++k;

@@ -41,12 +41,6 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #ifndef PT_STACK
 #define PT_STACK 24  // traversal stack entries per lane in LDS (lane-contiguous)
 #endif
-#ifndef PT_SCALAR_BLOCKS
-#define PT_SCALAR_BLOCKS 0  // 1: refill block records through the scalar cache (A/B)
-#endif
-#ifndef PT_FIXED_ACC
-#define PT_FIXED_ACC 0  // 1: exact fixed-point pixel sums by no-return atomics (A/B)
-#endif
 #ifndef PT_STACK_MAX
 #define PT_STACK_MAX 128  // deepest worst-case stack accepted (entries past PT_STACK spill to global memory)
 #endif
@@ -131,7 +125,6 @@ struct KParams {
   float* out;         // W*H*3, or n_tiles*1024*3 when packed
   int packed;         // PT_FLAG_PACKED: tile i's pixel (x, y) -> out[3 * (i*1024 + (y-ty)*32 + (x-tx))]
   float* partial;     // W*H*n_groups*3: each sample group's sum, resolved into `out` in group order
-  unsigned long long* accum;  // PT_FIXED_ACC: W*H*3 exact 32.32 fixed-point pixel sums (zero between launches)
   const int4* blocks;  // (x, y, w<=8, h<=8): footprint-clipped pixel blocks of the tiles
   int n_blocks;
   uint32_t* work_counter;

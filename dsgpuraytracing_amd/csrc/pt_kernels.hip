@@ -560,25 +560,6 @@ __device__ __forceinline__ void env_sample(const KParams& P, float r1, float r2,
   wi = f3(-st * sp, ct, st * cp);
 }
 
-// Exact pixel sums (PT_FIXED_ACC): a finished sample group's float sum g is
-// added to its pixel's accumulator as floor(g * 2^32) in unsigned 32.32 fixed
-// point (g in [0, 2^31); NaN and negatives -> 0; exact: g - trunc(g) and the
-// scaling by 2^32 round nothing).  Integer addition is associative, so the
-// pixel's value is independent of the order in which groups finish -- no float
-// atomics (the reference GPU path atomicAdds floats, kernel.cu:341-343) and no
-// per-group sums in memory.  No-return atomics at agent scope.
-__device__ __forceinline__ unsigned long long to_fixed32(float v) {
-  v = fminf(fmaxf(v, 0.0f), 2147483520.0f);
-  const uint32_t hi = (uint32_t)v;
-  const uint32_t lo = (uint32_t)((v - (float)hi) * 4294967296.0f);
-  return ((unsigned long long)hi << 32) | lo;
-}
-__device__ __forceinline__ void accum_add(unsigned long long* a, float3 g) {
-  __hip_atomic_fetch_add(a, to_fixed32(g.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_fetch_add(a + 1, to_fixed32(g.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_fetch_add(a + 2, to_fixed32(g.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // Lane modes of the persistent kernel.
 enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 
@@ -931,11 +912,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if (sample < P.spp && !group_starts(sample)) {
           mode = M_CAMERA;
         } else {
-#if PT_FIXED_ACC
-          accum_add(P.accum + 3 * (size_t)pix_index(pix), acc);
-#else
           store3(P.partial + 3 * slot_of(pix, sample), acc);
-#endif
           PT_SLOT_DONE();
           mode = M_FETCH;
         }
@@ -978,13 +955,13 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             if (STATS) n_atomics += lane == 0;
           }
         }
-#if PT_SCALAR_BLOCKS
         // A chunk of 128 slots (128-aligned) lies inside one 8x8 block when a
         // block holds a multiple of 128 slots (n_groups a power of two >= 2),
         // and the lanes are served from at most two chunks -- the rest of the
         // old one and the new one: both block records are read through the
         // scalar cache (wave-uniform addresses) instead of one vector-memory
-        // load per lane, which every refill round would wait on.
+        // load per lane, which every refill round would wait on (C5 +1%,
+        // framed C3 +0.3%, C3 neutral: profiles/r3/ab_scalar_blocks.txt).
         const bool sblocks = P.ngroup_shift >= 1;
         int4 b_old = make_int4(0, 0, 0, 0), b_new = make_int4(0, 0, 0, 0);
         if (sblocks) {
@@ -1001,7 +978,6 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             b_new = make_int4(v.x, v.y, v.z, v.w);
           }
         }
-#endif
         if (need) {
           uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
           uint32_t slot = rank < avail ? chunk_next + rank : nbase + (rank - avail);
@@ -1016,13 +992,9 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             // resolve_kernel: every ray through them misses the root box).
             uint32_t bq = pixel_of_slot(slot);
             uint32_t g = slot - bq * n_groups;
-#if PT_SCALAR_BLOCKS
-            int4 b;
+            int4 b;  // (other groupings: one vector-memory load per lane)
             if (sblocks) b = rank < avail ? b_old : b_new;
             else b = P.blocks[bq >> 6];
-#else
-            int4 b = P.blocks[bq >> 6];
-#endif
             int qx = (int)(bq & 7u), qy = (int)((bq >> 3) & 7u);
             if (qx < b.z && qy < b.w) {
               pix = (b.x + qx) | ((b.y + qy) << 16);
@@ -1070,11 +1042,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if (ENV) acc = acc + env_dir(P, d);
         ++sample;
         if (sample >= P.spp || group_starts(sample)) {
-#if PT_FIXED_ACC
-          accum_add(P.accum + 3 * (size_t)pix_index(pix), acc);
-#else
           store3(P.partial + 3 * slot_of(pix, sample), acc);
-#endif
           PT_SLOT_DONE();
           mode = M_FETCH;
         }
@@ -1220,7 +1188,6 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
 // Lanes that resolve one pixel: the pixel's groups are read as one coalesced
 // run (the per-pixel partials are n_groups * 12 B contiguous).
 __host__ __device__ __forceinline__ int resolve_team(int n_groups) {
-  if (PT_FIXED_ACC) return 1;  // one exact sum per pixel
   int k = 1;
   while (k < n_groups && k < 64) k <<= 1;
   return k;
@@ -1243,18 +1210,6 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
   const int4 tile = live ? P.tiles[tq >> 10] : make_int4(0, 0, 0, 0);
   int2 xy = live ? tile_pixel(tile, tq & 1023u) : make_int2(-1, -1);
   float3 acc = f3(0, 0, 0);
-#if PT_FIXED_ACC
-  if (xy.x >= 0 && !culled(P, xy.x, xy.y)) {
-    // the pixel's exact sum -> its mean; the accumulator is left zeroed for
-    // the slot's next launch
-    unsigned long long* a = P.accum + 3 * ((size_t)xy.x + (size_t)xy.y * (size_t)P.W);
-    const double kScale = 2.3283064365386963e-10 / (double)P.spp;  // 2^-32 / spp
-    acc = f3((float)((double)a[0] * kScale), (float)((double)a[1] * kScale), (float)((double)a[2] * kScale));
-    a[0] = a[1] = a[2] = 0ull;
-  }
-  if (xy.x < 0) return;
-  const float inv_spp = 1.0f;
-#else
   if (xy.x >= 0 && !culled(P, xy.x, xy.y)) {
     const float* p = P.partial + 3 * ((size_t)xy.x + (size_t)xy.y * (size_t)P.W) * (size_t)P.n_groups;
     for (int g = j; g < P.n_groups; g += k) acc = acc + ld3(p + 3 * g);
@@ -1264,7 +1219,6 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
     acc = acc + f3(__shfl_xor(acc.x, off), __shfl_xor(acc.y, off), __shfl_xor(acc.z, off));
   if (xy.x < 0 || j != 0) return;
   const float inv_spp = (float)(1.0 / (double)P.spp);
-#endif
   const size_t o = P.packed ? (size_t)(tq & ~1023u) + (size_t)((xy.y - tile.y) * 32 + (xy.x - tile.x))
                             : (size_t)xy.x + (size_t)xy.y * (size_t)P.W;
   store3(P.out + 3 * o, acc * inv_spp);
