@@ -1027,6 +1027,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   }
   c->culled_px = px_all - px_in;
   std::vector<int4>& bh = c->blocks_host[slot];
+  if (!c->blocks[slot].p) HIPCHK(c->blocks[slot].reserve(1));  // never a null block list (a launch may cull every block)
   if (bl.size() != bh.size() || std::memcmp(bl.data(), bh.data(), bl.size() * sizeof(int4)) != 0) {
     bh = bl;
     HIPCHK(c->blocks[slot].reserve(bl.size()));
@@ -1171,6 +1172,7 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags, bool sync) {
     c->last.hitshade_clocks = (int64_t)v[16];
     for (int k = 0; k < 4; ++k) c->last.section_clocks[k] = (int64_t)v[17 + k];
     for (int k = 0; k < 4; ++k) c->last.lane_iters[k] = (int64_t)v[27 + k];
+    c->last.deep_stack_steps = (int64_t)v[31];
     for (int k = 0; k < 3; ++k) c->last.wave_span[k] = (int64_t)(v[22 + k] - v[21]);
     for (int k = 0; k < 2; ++k) c->last.wave_span[3 + k] = v[25 + k] ? (int64_t)(v[25 + k] - v[21]) : -1;
     c->last.counters_valid = 1;
@@ -1285,11 +1287,17 @@ static int tile_launch(pt_ctx* c) {
     c->stage_n = W * H * 3;
   }
   if (int rc = launch(c, tl, c->frame.p, c->stream, 0)) return rc;
+  // one copy of the band of whole rows the batch's tiles span (a batch of the
+  // FIFO is a few tile rows): pixels of the band outside the tiles land in the
+  // stage only, never in the caller's buffers
+  int y0 = (int)H, y1 = 0;
   for (const int4& t : tl) {
-    const size_t off = ((size_t)t.y * W + (size_t)t.x) * 3;
-    HIPCHK(hipMemcpy2DAsync(c->stage + off, W * 3 * sizeof(float), c->frame.p + off, W * 3 * sizeof(float),
-                            (size_t)t.z * 3 * sizeof(float), (size_t)t.w, hipMemcpyDeviceToHost, c->stream));
+    y0 = std::min(y0, t.y);
+    y1 = std::max(y1, t.y + t.w);
   }
+  const size_t off = (size_t)y0 * W * 3;
+  HIPCHK(hipMemcpyAsync(c->stage + off, c->frame.p + off, (size_t)(y1 - y0) * W * 3 * sizeof(float),
+                        hipMemcpyDeviceToHost, c->stream));
   auto* b = new pt_ctx::TileBatch{std::move(jobs), c->stage, (int)W, (int)H};
   c->tile_inflight.push_back(b);
   HIPCHK(hipLaunchHostFunc(c->stream, tile_done, b));

@@ -666,6 +666,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // traversal lane-iterations: at the other step kind, finished and waiting
   // for the shading round, retired, stepping a leaf
   uint32_t l_other = 0, l_ready = 0, l_dead = 0, l_leaf = 0;
+  uint32_t l_deep = 0;  // traversal lane-steps taken with stack entries in the global spill area
   uint32_t n_atomics = 0;              // work-queue atomics (lane 0)
   uint32_t chunk_next = 0, chunk_end = 0;  // the wave's private range of work slots
   uint32_t seen = 0;                       // queue head after this wave's last claim
@@ -962,7 +963,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         // scalar cache (wave-uniform addresses) instead of one vector-memory
         // load per lane, which every refill round would wait on (C5 +1%,
         // framed C3 +0.3%, C3 neutral: profiles/r3/ab_scalar_blocks.txt).
-        const bool sblocks = P.ngroup_shift >= 1;
+        const bool sblocks = P.ngroup_shift >= 1 && total_slots > 0u;  // (no blocks: nothing to read)
         int4 b_old = make_int4(0, 0, 0, 0), b_new = make_int4(0, 0, 0, 0);
         if (sblocks) {
           typedef __attribute__((address_space(4))) const pt_v4i cst_v4i;
@@ -1093,6 +1094,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         l_ready += mode == M_SHADE;
         l_dead += mode == M_DONE;
         l_leaf += at_leaf && leaf_iter;
+        l_deep += trav && tr.sp > PT_STACK;
       }
       if (leaf_iter) {
         if (at_leaf) done = leaf_step<STATS>(P.prims, stk, tr, ct);
@@ -1124,8 +1126,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
       if (lane == 0) atomicAdd(P.stats + k, s);
     }
-    const uint32_t li[4] = {l_other, l_ready, l_dead, l_leaf};
-    for (int k = 0; k < 4; ++k) {
+    const uint32_t li[5] = {l_other, l_ready, l_dead, l_leaf, l_deep};
+    for (int k = 0; k < 5; ++k) {
       unsigned long long s = li[k];
       for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
       if (lane == 0) atomicAdd(P.stats + 27 + k, s);

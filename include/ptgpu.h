@@ -209,7 +209,8 @@ typedef struct pt_stats {
   int64_t lane_iters[4];   /* traversal lane-iterations (64 per wave iteration) spent at the other
                               step kind, finished and waiting for the shading round, retired
                               (queue drained), stepping a leaf; node steps = node_visits */
-  int64_t reserved0;       /* 0 (was uniform_node_steps of a removed experimental build) */
+  int64_t deep_stack_steps; /* traversal lane-steps taken while the ray's stack held entries beyond the
+                              PT_STACK (24) kept in LDS, i.e. in the global spill area */
   int64_t partial_bytes;   /* device bytes of the sample-group sums one render slot holds for the last
                               launch's frame (W*H*ceil(spp/group_spp)*12; two slots pipeline renders) */
 } pt_stats;

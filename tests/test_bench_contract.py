@@ -65,7 +65,7 @@ def test_pmc_summary_agrees_with_committed_kernel_trace():
 
 
 def test_committed_bench_lines_keep_the_contract():
-    path = os.path.join(ROOT, "profiles", "r2", "bench_c3_default.jsonl")
+    path = os.path.join(ROOT, "profiles", "r3", "bench_c3_default.jsonl")
     with open(path) as f:
         d = json.loads(f.read().strip().splitlines()[-1])
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
@@ -75,5 +75,11 @@ def test_committed_bench_lines_keep_the_contract():
     assert d["value"] == pytest.approx(1024 * 1024 * 64 / (d["config"]["render_time_s"] * 1e6), rel=0.02)
     assert 0.0 < d["roofline"]["frac"] <= 1.0
     assert d["cpu_baseline"]["kind"] in ("reference", "port") and d["cpu_baseline"]["cores"] >= 1
-    for name in ("c3_framed", "c4_single_gpu", "c5_single_gpu", "c3_lbvh"):
+    for name in ("c3_framed", "c4_single_gpu", "c5_single_gpu", "c3_host_sah", "c3_per_tile", "c3_per_tile_sync"):
         assert d["companions"][name]["value"] > 0, name
+    # the roofline's durations: per frame, none above ms_per_step; the isolated
+    # kernel time beside it; the PMC summary of the library the line ran
+    r = d["roofline"]
+    assert r["duration_ms"] == pytest.approx(d["ms_per_step"], rel=1e-3)
+    assert r["isolated_kernel_ms"] > 0 and r["frac_isolated"] > 0
+    assert d["dist"]["world_size"] == 1
