@@ -501,7 +501,7 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
                        "width": W, "height": H, "spp": SPP, "max_ray_depth": DEPTH, "ns_area_light": NSL,
                        "spp_total": SPP * world if weak else SPP,
                        "parallelism": (f"samples{world}" if weak else f"tiles{world}") if world > 1 else "single",
-                       "render_time_s": round(elapsed / frames, 4), "scene_load_s": round(t_load, 3),
+                       "render_time_s": round(elapsed / frames, 7), "scene_load_s": round(t_load, 3),
                        "single_frame_ms": None if single_ms is None else round(single_ms, 3),
                        "bvh": bvh_desc(args.lbvh),
                        "upload_s": round(t_up, 4),
