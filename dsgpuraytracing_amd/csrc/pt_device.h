@@ -34,7 +34,7 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #define PT_LEAF_WEIGHT 16  // leaf steps when leaf lanes >= node lanes * 16 / PT_LEAF_WEIGHT
 #endif
 #ifndef PT_ENV_GUIDE
-#define PT_ENV_GUIDE 64  // buckets of the environment-CDF guide tables
+#define PT_ENV_GUIDE 1024  // buckets of the environment-CDF guide tables (with the window compare: C5 +10% over 64, profiles/r3/ab_env_window_search.txt)
 #endif
 #define PT_STATS_SLOTS 32  // launch counters; per-wave trace records (PT_WAVE_TRACE u64 each) follow
 #define PT_WAVE_TRACE 9

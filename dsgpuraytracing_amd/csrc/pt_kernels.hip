@@ -516,14 +516,18 @@ __device__ __forceinline__ float3 env_dir(const KParams& P, float3 d) {
 // lower_bound of v = r * a[n-1] accelerated by a guide table g[0..G] with
 // g[k] = lower_bound(a, k/G * a[n-1]) (built on the host): the answer lies in
 // [g[k-1], g[k+2]] for k = floor(r*G), one bucket of slack either side for
-// rounding; the result is exactly std::lower_bound's.
+// rounding; the result is exactly std::lower_bound's.  With PT_ENV_GUIDE
+// buckets the window is a few entries where the CDF carries mass (where
+// samples land): it is halved down to <= 4 entries, then compared in ONE
+// memory round trip (lower_bound = lo + #{entries < v}, the array is sorted)
+// instead of a chain of dependent loads.
 __device__ __forceinline__ int guided_lower_bound(const float* __restrict__ a, float v, float r,
                                                   const int* __restrict__ g, int G) {
   const int k = min(G - 1, max(0, (int)(r * (float)G)));
   int lo = g[max(k - 1, 0)];
   const int hi = g[min(k + 2, G)];
   int n = hi - lo;  // candidates [lo, hi); hi itself satisfies a[hi] >= v
-  while (n > 0) {
+  while (n > 4) {
     const int half = n >> 1;
     if (a[lo + half] < v) {
       lo += half + 1;
@@ -532,7 +536,10 @@ __device__ __forceinline__ int guided_lower_bound(const float* __restrict__ a, f
       n = half;
     }
   }
-  return lo;
+  const float kBig = 3.0e38f;
+  const float w0 = n > 0 ? a[lo] : kBig, w1 = n > 1 ? a[lo + 1] : kBig;
+  const float w2 = n > 2 ? a[lo + 2] : kBig, w3 = n > 3 ? a[lo + 3] : kBig;
+  return lo + (int)(w0 < v) + (int)(w1 < v) + (int)(w2 < v) + (int)(w3 < v);
 }
 
 // importanceSampling (69-115): inverse CDF over rows (pTheta), then within the
