@@ -660,7 +660,30 @@ def per_tile_companions(local, threads=8):
                      "ms_per_frame": round(el * 1e3, 3), "frames": frames, "threads": threads,
                      "host_output": "sampleBuffer + toColor frameBuffer (PCIe-inclusive)"}
         pt._device().close()
+    out["c3_per_tile_native"] = seam_native(wl, dae, cam, threads)
     return out
+
+
+def seam_native(wl, dae, cam, threads, frames=3):
+    """The same per-tile seam driven from C++ (tools/seam_bench.cpp: 8
+    std::thread workers, one context, a mutex around raytrace_tile), so the
+    seam is timed without the Python adapter; also the whole frame as one
+    pt_render_tiles call + pt_to_color with host output, and a bit-for-bit
+    check of both seams against it.  A child process: this process's own
+    contexts are closed first."""
+    import subprocess
+    exe = os.path.join(ROOT, "dsgpuraytracing_amd", "seam_bench")
+    if cam is not None or not os.path.exists(exe):
+        return {"skipped": "no seam_bench binary" if cam is None else "camera file not supported"}
+    r = subprocess.run([exe, dae, str(wl["w"]), str(wl["h"]), str(wl["spp"]), str(threads), str(frames)],
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
+    if r.returncode not in (0, 3):
+        raise RuntimeError(f"seam_bench failed ({r.returncode}): {r.stderr.decode(errors='replace')[-400:]}")
+    res = json.loads(r.stdout.decode().strip().splitlines()[-1])
+    res["workload"] = wl["desc"] + f", C++ driver, {threads} std::thread workers"
+    res["unit"] = "Mrays/s"
+    res["frames"] = frames
+    return res
 
 
 if __name__ == "__main__":

@@ -36,6 +36,8 @@ def up_to_date() -> bool:
     if not os.path.exists(LIB):
         return False
     t = os.path.getmtime(LIB)
+    if not os.path.exists(SEAM_BENCH):
+        return False
     return all(os.path.getmtime(p) <= t for p in _sources() + _headers() + [__file__])
 
 
@@ -84,7 +86,23 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(link)}\n{r.stdout.decode(errors='replace')}")
     os.replace(tmp, LIB)
+    build_seam_bench()
     return LIB
+
+
+SEAM_BENCH = os.path.join(PKG, "seam_bench")
+
+
+def build_seam_bench() -> str:
+    """tools/seam_bench.cpp: the C++ driver of the per-tile seam (bench.py's
+    c3_per_tile companions), linked against the in-tree libptgpu.so."""
+    src = os.path.join(ROOT, "tools", "seam_bench.cpp")
+    cmd = ["g++", "-O2", "-std=c++17", "-pthread", f"-I{os.path.join(ROOT, 'include')}", src, "-o", SEAM_BENCH,
+           f"-L{PKG}", "-lptgpu", "-Wl,-rpath,$ORIGIN"]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    if r.returncode != 0:
+        raise RuntimeError(f"seam_bench build failed: {' '.join(cmd)}\n{r.stdout.decode(errors='replace')}")
+    return SEAM_BENCH
 
 
 if __name__ == "__main__":

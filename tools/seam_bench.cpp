@@ -1,0 +1,108 @@
+// seam_bench.cpp — the reference's literal raytrace_tile seam, driven from C++
+// the way INTEGRATION.md's adapter drives it: N std::thread workers pop 32x32
+// tiles from one FIFO (PathTracer::worker_thread, src/pathtracer.cpp:613-637)
+// and call raytrace_tile through ONE pt_ctx (calls serialised by a mutex).
+//   async: pt_tile_submit (tiles batched into launches, each completed into
+//          the sampleBuffer + toColor'd frameBuffer on a stream callback), the
+//          last worker's pt_tile_finish;
+//   sync:  one pt_render_tiles launch per tile + pt_to_color of the tile.
+// Also the whole frame as ONE pt_render_tiles call + pt_to_color (host output
+// included), and a bit-for-bit check of both seams against it.  Prints one
+// JSON line.  Built by dsgpuraytracing_amd/build.py; run by bench.py.
+// usage: seam_bench scene.dae W H spp threads frames
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "ptgpu.h"
+#include "ptgpu_scene.h"
+
+static void check(int rc, const char* what) {
+  if (rc != PT_OK) {
+    std::fprintf(stderr, "seam_bench: %s: %s\n", what, pt_last_error());
+    std::exit(1);
+  }
+}
+
+int main(int argc, char** argv) {
+  if (argc < 7) return 2;
+  const int W = std::atoi(argv[2]), H = std::atoi(argv[3]), spp = std::atoi(argv[4]);
+  const int threads = std::atoi(argv[5]), frames = std::atoi(argv[6]);
+  pt_host_scene* hs = nullptr;
+  check(pt_host_scene_load(argv[1], W, H, nullptr, &hs), "pt_host_scene_load");
+  pt_scene scene;
+  pt_camera cam;
+  check(pt_host_scene_view(hs, &scene, &cam), "pt_host_scene_view");
+  pt_ctx* ctx = nullptr;
+  check(pt_create(0, &ctx), "pt_create");
+  check(pt_upload_scene(ctx, &scene), "pt_upload_scene");
+  check(pt_set_camera(ctx, &cam), "pt_set_camera");
+  const pt_params p = {W, H, spp, 4, 1, 1u, 0u};
+  check(pt_set_params(ctx, &p), "pt_set_params");
+  std::vector<pt_tile> fifo;
+  for (int y = 0; y < H; y += 32)
+    for (int x = 0; x < W; x += 32) fifo.push_back({x, y, 32, 32});
+  const size_t npx = (size_t)W * H;
+  std::vector<float> whole(npx * 3), hdr(npx * 3);
+  std::vector<uint32_t> whole_rgba(npx), rgba(npx);
+  using clk = std::chrono::steady_clock;
+  auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+
+  auto frame_whole = [&]() {
+    check(pt_render_tiles(ctx, fifo.data(), (int)fifo.size(), whole.data(), 0), "pt_render_tiles");
+    check(pt_to_color(whole.data(), W, H, 0, 0, W, H, whole_rgba.data()), "pt_to_color");
+  };
+  auto frame_tiles = [&](bool async) {
+    std::atomic<int> next(0);
+    std::mutex m;
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+      th.emplace_back([&] {
+        for (int i; (i = next++) < (int)fifo.size();) {
+          const pt_tile& tile = fifo[(size_t)i];
+          if (async) {
+            std::lock_guard<std::mutex> lock(m);
+            check(pt_tile_submit(ctx, &tile, hdr.data(), rgba.data()), "pt_tile_submit");
+          } else {
+            {
+              std::lock_guard<std::mutex> lock(m);
+              check(pt_render_tiles(ctx, &tile, 1, hdr.data(), 0), "pt_render_tiles");
+            }
+            check(pt_to_color(hdr.data(), W, H, tile.x, tile.y, tile.x + tile.w, tile.y + tile.h, rgba.data()),
+                  "pt_to_color");
+          }
+        }
+      });
+    for (auto& t : th) t.join();
+    if (async) check(pt_tile_finish(ctx), "pt_tile_finish");
+  };
+  auto timed = [&](auto fn, int n) {
+    fn();  // warm-up
+    const auto t0 = clk::now();
+    for (int i = 0; i < n; ++i) fn();
+    return ms(t0, clk::now()) / n;
+  };
+  const double t_whole = timed(frame_whole, frames);
+  const double t_async = timed([&] { frame_tiles(true); }, frames);
+  const bool same_async = std::memcmp(hdr.data(), whole.data(), npx * 12) == 0 &&
+                          std::memcmp(rgba.data(), whole_rgba.data(), npx * 4) == 0;
+  std::fill(hdr.begin(), hdr.end(), 0.f);
+  const double t_sync = timed([&] { frame_tiles(false); }, std::max(1, frames / 3));
+  const bool same_sync = std::memcmp(hdr.data(), whole.data(), npx * 12) == 0 &&
+                         std::memcmp(rgba.data(), whole_rgba.data(), npx * 4) == 0;
+  const double samples = (double)npx * spp;
+  std::printf(
+      "{\"threads\": %d, \"tiles\": %zu, \"frame_host_ms\": %.3f, \"per_tile_async_ms\": %.3f, "
+      "\"per_tile_sync_ms\": %.3f, \"frame_host_Mrays\": %.1f, \"per_tile_async_Mrays\": %.1f, "
+      "\"per_tile_sync_Mrays\": %.1f, \"async_bit_identical\": %s, \"sync_bit_identical\": %s}\n",
+      threads, fifo.size(), t_whole, t_async, t_sync, samples / t_whole / 1e3, samples / t_async / 1e3,
+      samples / t_sync / 1e3, same_async ? "true" : "false", same_sync ? "true" : "false");
+  pt_destroy(ctx);
+  pt_host_scene_free(hs);
+  return same_async && same_sync ? 0 : 3;
+}
