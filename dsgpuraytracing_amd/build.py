@@ -31,7 +31,7 @@ def _headers():
 
 
 def up_to_date() -> bool:
-    if os.environ.get("PT_HIPCC_FLAGS"):
+    if os.environ.get("PT_HIPCC_FLAGS") or os.environ.get("PT_KERNEL_SCHED"):
         return False
     if not os.path.exists(LIB):
         return False
@@ -66,7 +66,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
             # cost more VALU slots and VGPRs than the pairing saves here
             # (render_kernel 103 -> 99 VGPRs; C3 +3.5%)
             cmd.insert(1, "-fno-slp-vectorize")
-        if base == "pt_kernels.hip" or (base == "pt_kernels_env.hip" and os.environ.get("PT_ENV_SCHED") == "ilp"):
+        sched = os.environ.get("PT_KERNEL_SCHED", "ilp")  # experiments: "default" drops the ILP scheduler
+        if (base == "pt_kernels.hip" and sched == "ilp") or (base == "pt_kernels_env.hip" and os.environ.get("PT_ENV_SCHED") == "ilp"):
             # iterative-ILP machine scheduling: C3 +1.7%, framed C3 +1.8% (the
             # ENV kernels, -2.9% with it, live in pt_kernels_env.hip without it)
             cmd[1:1] = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]

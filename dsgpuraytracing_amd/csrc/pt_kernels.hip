@@ -241,13 +241,22 @@ typedef __attribute__((address_space(3))) int lds_int;
 
 struct Stack {
   lds_int* lds;   // s_stack + lane, stride PT_BLOCK
-  int* spill;     // P.stack_spill + global lane id, stride sstride (may be null)
+  int* spill;     // the spill area (wave-uniform base, may be null): column = global lane id, stride sstride
   uint32_t sstride;
+  // Entry i >= PT_STACK of this lane.  The global lane id is re-derived at
+  // each (rare) spill access from the workgroup id and the lane's mbcnt, in a
+  // volatile asm the compiler cannot hoist: a per-lane 64-bit spill pointer
+  // would hold two VGPRs in every wave for the whole kernel.
+  __device__ __forceinline__ int* spill_at(int i) const {
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return spill + ((size_t)(i - PT_STACK) * sstride + (size_t)blockIdx.x * PT_BLOCK + l);
+  }
   __device__ __forceinline__ void put(int i, int v) const {
     if (i < PT_STACK) {
       lds[i * PT_BLOCK] = v;
     } else {
-      spill[(size_t)(i - PT_STACK) * sstride] = v;
+      *spill_at(i) = v;
     }
   }
   __device__ __forceinline__ int get(int i) const {
@@ -255,7 +264,7 @@ struct Stack {
     if (i < PT_STACK) {
       v = lds[i * PT_BLOCK];
     } else {
-      v = spill[(size_t)(i - PT_STACK) * sstride];
+      v = *spill_at(i);
     }
     return v;
   }
@@ -596,8 +605,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   const int lane = threadIdx.x;
   const uint32_t wave_id = blockIdx.x;  // the persistent wave (one per workgroup)
   const uint32_t n_waves = gridDim.x;
-  const uint32_t gid = wave_id * PT_BLOCK + lane;
-  const Stack stk{(lds_int*)(s_stack + lane), P.stack_spill ? P.stack_spill + gid : nullptr, n_waves * PT_BLOCK};
+  const Stack stk{(lds_int*)(s_stack + lane), P.stack_spill, n_waves * PT_BLOCK};
   // The BVH4 root, which every ray visits first: one LDS copy per wave, so
   // the root step of a fresh ray costs no vector-memory traffic (C3 +2%).
   __shared__ DNode s_root;
@@ -1241,7 +1249,7 @@ __global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __rest
                                                            int32_t* anyhit, int* spill, const int* prim_map) {
   __shared__ int s_stack[PT_STACK * PT_BLOCK];
   int64_t i = (int64_t)blockIdx.x * PT_BLOCK + threadIdx.x;
-  const Stack stk{(lds_int*)(s_stack + threadIdx.x), spill ? spill + i : nullptr, gridDim.x * PT_BLOCK};
+  const Stack stk{(lds_int*)(s_stack + threadIdx.x), spill, gridDim.x * PT_BLOCK};
   if (i >= n) return;
   float3 O = f3(o[3 * i], o[3 * i + 1], o[3 * i + 2]);
   float3 D = f3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
