@@ -13,12 +13,19 @@
 //   4. bottom-up boxes, the second child to arrive completing its parent
 //      (agent-scope acquire/release: the per-XCD L2s are not coherent);
 //   5. subtrees of <= LEAF_NUMBER = 4 primitives collapse into leaves.
+// Beyond the reference (this is the renderer's default tree since round 3):
+//   6. treelet restructuring (Karras & Aila 2013): further bottom-up passes
+//      (PT_LBVH_PASSES, default 3) rebuild every node's 7-leaf treelet to its
+//      SAH optimum by a wave-cooperative dynamic program over the leaf subsets;
+//   7. leaves chosen by SAH (a subtree of <= 4 primitives becomes a leaf only
+//      where the SAH says a split no longer pays), as the host SAH tree.
 // Then, MI355X-specific: the binary tree is emitted both as the 64-B binary
-// nodes of the reference-count launch and, breadth-first two levels at a time,
-// as the 128-B BVH4 nodes the renderer traverses (children allocated after
-// their parent, so references only point forward); primitives and normals are
-// gathered into sorted order; the worst-case traversal stack is computed on the
-// way down.
+// nodes of the reference-count launch and, breadth-first, as the 128-B BVH4
+// nodes the renderer traverses (the largest-area internal child opened until
+// four children; children allocated after their parent, so references only
+// point forward; primitives numbered in depth-first leaf order); primitives and
+// normals are gathered into that order; the worst-case traversal stack is
+// computed on the way down.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>

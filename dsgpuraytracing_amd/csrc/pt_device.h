@@ -21,8 +21,16 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #ifndef PT_GROUP_SPP
 #define PT_GROUP_SPP 4  // default samples per work slot (C3 +3.3% over 2; 8 or more: C3 -4%, C5 -10%)
 #endif
+// Leave traversal when this many lanes finished their ray (shade them
+// together).  Scenes with an environment light shade longer per round (map
+// lookups on every miss, inverse-CDF light samples) and want larger rounds:
+// same-session sweep (profiles/r3/ab_shade_batch.txt) C3 / framed C3 / C4
+// +1.5 / +3.4 / +5.6% at 32 vs 48, C5 -4% at 36 and best at 48.
 #ifndef PT_SHADE_BATCH
-#define PT_SHADE_BATCH 48  // default: leave traversal when this many lanes finished their ray
+#define PT_SHADE_BATCH 32
+#endif
+#ifndef PT_SHADE_BATCH_ENV
+#define PT_SHADE_BATCH_ENV 48
 #endif
 #ifndef PT_LDS_BSDFS
 #define PT_LDS_BSDFS 16  // material tables up to this size are staged in LDS
