@@ -14,14 +14,19 @@ the scene.
 
   * N = 1 (default): C3 = CBdragon proxy CBbunny_sub1 (114,316 triangles;
     CBdragon.dae is absent), 1024x1024, 64 spp.
-  * N > 1 (torchrun, one process per GPU), default: BASELINE C4 = the same
-    scene at 1920x1080, 256 spp, ONE frame's 32x32 tiles dealt diagonally
-    over the GPUs, each rank rendering its tiles into a packed buffer, then
-    ONE RCCL gather of the packed tiles onto rank 0 (SURVEY.md §8(e));
-    value = W*H*256 / max-rank time ("scaling": "strong"), the image is
-    bit-identical to the 1-GPU image.  --scaling weak (opt-in) renders one
-    64-spp pass of the whole frame per GPU over disjoint sample ranges plus
-    one RCCL sum-reduce.
+  * N > 1 (torchrun, one process per GPU), default: the SAME C3 workload per
+    GPU ("scaling": "weak"): rank r renders one 64-spp pass of the whole
+    frame over sample indices 64r .. 64r+63 (the counter RNG is keyed by the
+    sample index, so the passes are disjoint slices of one 64N-spp render),
+    then ONE RCCL sum-reduce assembles the 64N-spp image on rank 0; value =
+    N*W*H*64 / max-rank time.  Per-GPU work is the N = 1 line's, so the
+    driver's per-N values form a scaling curve of one workload.
+  * --workload c4 --scaling strong: BASELINE C4 = the same scene at
+    1920x1080, 256 spp, ONE frame's 32x32 tiles dealt diagonally over the
+    GPUs, each rank rendering its tiles into a packed buffer, then ONE RCCL
+    gather of the packed tiles onto rank 0; value =
+    W*H*256 / max-rank time ("scaling": "strong"), the image bit-identical
+    to the 1-GPU image.
 The exchange is inside the timed region.  Device renders are queued back to
 back and consecutive frames overlap on the GPU (pt_api.cpp's two-slot render
 pipeline: the next frame's waves fill the CUs the previous frame's drain
@@ -286,15 +291,16 @@ def main():
     ap.add_argument("--no-extras", action="store_true",
                     help="N = 1: skip the companion measurements (framed C3, single-GPU C4 and C5, C3 over the GPU LBVH)")
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
-                    help="default: c3 on one GPU, c4 (the BASELINE multi-GPU config) on N > 1")
+                    help="default: c3 (the headline config) at every N")
     ap.add_argument("--lbvh", action="store_true", help="build the BVH on the GPU (pt_upload_scene_lbvh)")
     ap.add_argument("--spp", type=int, default=0, help="diagnostic: override the workload's spp (not a BASELINE config)")
     ap.add_argument("--emulate-shard", type=int, default=0,
                     help="diagnostic: render only one rank's share of an N-GPU split on this one GPU")
     ap.add_argument("--emulate-rank", type=int, default=0, help="the rank --emulate-shard renders")
-    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
-                    help="N > 1: strong = one frame's tiles split across the GPUs + one RCCL gather (default); "
-                         "weak = one pass of the whole frame per GPU over disjoint sample ranges + one RCCL reduce")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N > 1: weak = one pass of the whole frame per GPU over disjoint sample ranges + one RCCL "
+                         "reduce (default); strong = one frame's tiles split across the GPUs + one RCCL gather "
+                         "(BASELINE C4: --workload c4 --scaling strong)")
     args = ap.parse_args()
     if os.environ.get("PT_BENCH_LBVH") == "1":  # A/B arms (tools/ab.sh): the GPU-built tree
         args.lbvh = True
@@ -335,7 +341,7 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
     import torch.distributed as dist
 
     global W, H, SPP
-    workload = args.workload or ("c3" if world == 1 else "c4")
+    workload = args.workload or "c3"
     wl = WORKLOADS[workload]
     W, H, SPP = wl["w"], wl["h"], args.spp or wl["spp"]
 

@@ -153,7 +153,8 @@ def render_sharded(render_packed: Callable[[List[Tile], object], None], frame, t
 # the sample grouping fixes each pixel's float summation order, the render
 # tree decides ties between equidistant primitives.  Ranks that disagree on
 # them would assemble a frame that is not the 1-GPU frame bit for bit.
-VALUE_KNOBS = ("PT_SAMPLE_GROUP", "PT_WAVES_PER_CU", "PT_BVH_BUILD", "PT_COLLAPSE", "PT_LIB")
+VALUE_KNOBS = ("PT_SAMPLE_GROUP", "PT_WAVES_PER_CU", "PT_BVH_BUILD", "PT_COLLAPSE", "PT_LBVH_PASSES", "PT_LBVH_CI",
+               "PT_LBVH_MAXLEAF", "PT_LIB")
 DEFAULT_TIMEOUT_S = 120
 
 
