@@ -994,7 +994,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   }
   screen_footprint(c, P);
   P.shade_batch = c->env_w > 0 ? PT_SHADE_BATCH_ENV : PT_SHADE_BATCH;
-  P.leaf_weight = PT_LEAF_WEIGHT;
+  P.leaf_weight = c->env_w > 0 ? PT_LEAF_WEIGHT_ENV : PT_LEAF_WEIGHT;
   if (const char* lw = std::getenv("PT_LEAF_WEIGHT")) {  // tuning knob
     int v = std::atoi(lw);
     if (v >= 1) P.leaf_weight = v;

@@ -38,8 +38,15 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #ifndef PT_LDS_LIGHTS
 #define PT_LDS_LIGHTS 8
 #endif
+// leaf steps when leaf lanes >= node lanes * 16 / leaf weight; with 32-lane
+// shading rounds 10 beats 16 (C3 +1.9%, framed C3 +1.8%, C4 +1.4%); C5 (the
+// environment-light build) is flat between 10 and 16 and keeps 16
+// (profiles/r3/ab_leaf_weight.txt)
 #ifndef PT_LEAF_WEIGHT
-#define PT_LEAF_WEIGHT 16  // leaf steps when leaf lanes >= node lanes * 16 / PT_LEAF_WEIGHT
+#define PT_LEAF_WEIGHT 10
+#endif
+#ifndef PT_LEAF_WEIGHT_ENV
+#define PT_LEAF_WEIGHT_ENV 16
 #endif
 #ifndef PT_ENV_GUIDE
 #define PT_ENV_GUIDE 1024  // buckets of the environment-CDF guide tables (with the window compare: C5 +10% over 64, profiles/r3/ab_env_window_search.txt)
