@@ -379,16 +379,19 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
     if ex is not None:
         mine_arr = np.asarray(ex.mine, dtype=np.int32).reshape(-1, 4)
 
+    band = [frame]  # weak: the rows the reduce carries (set from the launch's screen footprint below)
+
     def reduce_passes():  # weak: sum the N passes onto rank 0, mean over SPP*N samples
+        rows = band[0]
         if backend == "gloo":  # host staging (one-GPU rehearsals)
-            h = frame.cpu()
+            h = rows.cpu()
             dist.reduce(h, dst=0)
             if rank == 0:
-                frame.copy_(h)
+                rows.copy_(h)
         else:
-            dist.reduce(frame, dst=0)
+            dist.reduce(rows, dst=0)
         if rank == 0:
-            frame.mul_(1.0 / world)
+            rows.mul_(1.0 / world)
 
     xev = []  # (start, end) events around each timed step's exchange
     # A rank whose render fails keeps joining the exchanges; guard.check() (a
@@ -423,6 +426,15 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
     st_counts = step(stats="ref")
     st_perf = step(stats=True)
     guard.check()
+    if weak:
+        # Rows outside the scene's screen footprint are 0 in every pass (their
+        # camera rays miss the scene box: pt_stats.footprint), so the reduce
+        # carries only the footprint's rows -- the same image, fewer bytes
+        # (C3: 53% of the frame's rows).  Every rank computes the same rows.
+        y0, y1 = st_perf["footprint"][1], st_perf["footprint"][3]
+        band[0] = frame[y0:y1 + 1]
+        frame[:y0].zero_()
+        frame[y1 + 1:].zero_()
     # the ranks must group each pixel's samples alike (bit-identical frame)
     knobs = check_value_knobs({"group_spp": st_perf["group_spp"]})
     for _ in range(args.warmup):
@@ -507,6 +519,8 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
                        "width": W, "height": H, "spp": SPP, "max_ray_depth": DEPTH, "ns_area_light": NSL,
                        "spp_total": SPP * world if weak else SPP,
                        "parallelism": (f"samples{world}" if weak else f"tiles{world}") if world > 1 else "single",
+                       "exchange_bytes_per_rank": (int(band[0].numel() * 4) if weak else
+                                                   (int(ex.packed.numel() * 4) if ex is not None else 0)),
                        "render_time_s": round(elapsed / frames, 7), "scene_load_s": round(t_load, 3),
                        "single_frame_ms": None if single_ms is None else round(single_ms, 3),
                        "bvh": bvh_desc(args.lbvh),

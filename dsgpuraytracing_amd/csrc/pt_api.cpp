@@ -993,6 +993,10 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     P.root_hi[k] = c->root_hi[k];
   }
   screen_footprint(c, P);
+  c->last.footprint[0] = std::max(0, P.cull_x0);
+  c->last.footprint[1] = std::max(0, P.cull_y0);
+  c->last.footprint[2] = std::min(P.W - 1, P.cull_x1);
+  c->last.footprint[3] = std::min(P.H - 1, P.cull_y1);
   P.shade_batch = c->env_w > 0 ? PT_SHADE_BATCH_ENV : PT_SHADE_BATCH;
   P.leaf_weight = c->env_w > 0 ? PT_LEAF_WEIGHT_ENV : PT_LEAF_WEIGHT;
   if (const char* lw = std::getenv("PT_LEAF_WEIGHT")) {  // tuning knob

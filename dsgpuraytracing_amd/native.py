@@ -92,7 +92,8 @@ class pt_stats(ctypes.Structure):
                 ("leaf_steps", c_int64), ("hitshade_clocks", c_int64), ("resolve_ms", c_double),
                 ("bvh_stack", c_int32), ("bvh_nodes", c_int64), ("section_clocks", c_int64 * 4),
                 ("wave_span", c_int64 * 5), ("group_spp", c_int32), ("lane_iters", c_int64 * 4),
-                ("deep_stack_steps", c_int64), ("partial_bytes", c_int64)]
+                ("deep_stack_steps", c_int64), ("partial_bytes", c_int64),
+                ("footprint", c_int32 * 4)]
 
 
 # Every symbol include/ptgpu.h and include/ptgpu_scene.h declare, with ctypes signatures.

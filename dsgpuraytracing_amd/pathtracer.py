@@ -138,6 +138,7 @@ class Device:
         out["section_clocks"] = list(s.section_clocks)
         out["wave_span"] = list(s.wave_span)
         out["lane_iters"] = list(s.lane_iters)
+        out["footprint"] = list(s.footprint)
         return out
 
     def launch_times(self, n: int = 256):

@@ -213,6 +213,10 @@ typedef struct pt_stats {
                               PT_STACK (24) kept in LDS, i.e. in the global spill area */
   int64_t partial_bytes;   /* device bytes of the sample-group sums one render slot holds for the last
                               launch's frame (W*H*ceil(spp/group_spp)*12; two slots pipeline renders) */
+  int32_t footprint[4];    /* the scene's screen footprint of the last launch, x0, y0, x1, y1 inclusive and
+                              clamped to the frame: every pixel outside it has radiance 0 for every sample
+                              (its camera ray misses the scene box; not traced).  The whole frame when
+                              culling is off (environment light, camera not in front of the box). */
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */

@@ -192,6 +192,16 @@ def test_footprint_cull_exact_at_full_size(monkeypatch, name, spp):
     assert np.array_equal(plain, plain_traced)
     assert np.array_equal(plain, culled)
     assert culled.mean() > 0
+    # the reported footprint (pt_stats.footprint; bench.py's weak-scaling
+    # reduce carries only its rows): everything outside it is exactly 0 in the
+    # TRACED frame, and the rectangle is not the whole frame here
+    x0, y0, x1, y1 = st["footprint"]
+    assert 0 <= x0 <= x1 < w and 0 <= y0 <= y1 < h
+    assert (x1 - x0 + 1) * (y1 - y0 + 1) < w * h
+    outside = np.ones((h, w), bool)
+    outside[y0:y1 + 1, x0:x1 + 1] = False
+    assert not traced[outside].any()
+    assert st2["footprint"] == [0, 0, w - 1, h - 1]
 
 
 def test_c3_fullsize_deterministic_and_split():
