@@ -97,11 +97,22 @@ def algorithmic_bytes(st: dict) -> float:
             + 36.0 * st["ext_hits"] + 12.0 * st["pixels"])
 
 
+def lib_path() -> str:
+    from dsgpuraytracing_amd import native
+    return os.path.abspath(os.environ["PT_LIB"]) if os.environ.get("PT_LIB") else native.LIB_PATH
+
+
+def kernel_sha256(path=None) -> str:
+    """sha256 of the device code (.hip_fatbin) of the libptgpu.so this process
+    loads: what a PMC summary's counts belong to (dsgpuraytracing_amd/elfsha.py)."""
+    from dsgpuraytracing_amd import elfsha
+    return elfsha.kernel_sha256(path or lib_path())
+
+
 def lib_sha256(path=None) -> str:
     """sha256 of the libptgpu.so this process loads (PT_LIB or the in-tree one)."""
     import hashlib
-    from dsgpuraytracing_amd import native
-    path = path or (os.path.abspath(os.environ["PT_LIB"]) if os.environ.get("PT_LIB") else native.LIB_PATH)
+    path = path or lib_path()
     h = hashlib.sha256()
     with open(path, "rb") as f:
         for blk in iter(lambda: f.read(1 << 20), b""):
@@ -126,12 +137,13 @@ def profile_summary(workload: str):
 
 
 def roofline(workload: str, frame_ms: float, alg_bytes: float, isolated_ms: float = 0.0,
-             pipelined_ms: float = 0.0, lib_sha: str | None = None) -> dict:
+             pipelined_ms: float = 0.0, lib_sha: str | None = None, kernel_sha: str | None = None) -> dict:
     """Roofline of the dominant kernel (render_kernel).  Per-launch counts come
     from the committed PMC summary of the same workload and library (they are a
     property of the workload and the build, not of the clock; `pmc_stale` is
     true when the summary was collected on a different libptgpu.so than the one
-    this run loaded).  Views:
+    this run loaded: the device-code sha256, `kernel_sha256`, when the summary
+    carries one, else the whole library's).  Views:
       hbm   -- (2 x FETCH_SIZE + WRITE_SIZE) bytes (gfx950 correction,
                MI355X_MICROARCH.md §HBM) vs 8 TB/s;
       l2    -- (TCC_HIT + TCC_MISS) requests x 128 B vs 34.5 TB/s (an upper
@@ -185,8 +197,14 @@ def roofline(workload: str, frame_ms: float, alg_bytes: float, isolated_ms: floa
     if pm:
         out["pmc"] = {k: (round(pm[k], 4) if isinstance(pm.get(k), float) else pm.get(k))
                       for k in ("avg_ms", "isolated_avg_ms", "sq_wait_any_frac", "sq_wait_inst_any_frac",
-                                "sq_active_inst_any_frac", "valu_issue_util", "l2_hit_rate", "source", "lib_sha256")}
-        out["pmc_stale"] = bool(lib_sha) and pm.get("lib_sha256") != lib_sha
+                                "sq_active_inst_any_frac", "valu_issue_util", "l2_hit_rate", "source", "lib_sha256",
+                                "kernel_sha256")}
+        # stale = the counts were collected on different device code than this
+        # run's (summaries without a kernel stamp compare the whole library)
+        if pm.get("kernel_sha256") and kernel_sha:
+            out["pmc_stale"] = pm["kernel_sha256"] != kernel_sha
+        else:
+            out["pmc_stale"] = bool(lib_sha) and pm.get("lib_sha256") != lib_sha
     return out
 
 
@@ -527,7 +545,7 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
                        "upload_s": round(t_up, 4),
                        "host_output_ms_per_frame": None if host_ms is None else round(host_ms, 3)},
             "roofline": roofline(workload, elapsed / frames * 1e3, algorithmic_bytes(st_counts), isolated_ms=iso_ms,
-                                 pipelined_ms=avg_ms, lib_sha=lib_sha256()),
+                                 pipelined_ms=avg_ms, lib_sha=lib_sha256(), kernel_sha=kernel_sha256()),
             "resolve_ms": round(float(np.mean(resolve_ms)), 4),
             "counters": {k: st_counts[k] for k in ("camera_rays", "bounce_rays", "shadow_rays", "node_visits",
                                                    "tri_tests", "sphere_tests", "ext_hits", "culled_samples")},

@@ -46,6 +46,10 @@ def test_roofline_views_are_fractions_and_bound_is_the_largest_measured():
     assert r["traffic"] == pm["hbm_bytes_per_launch"]
     assert r["pmc_stale"] is False
     assert bench.roofline("c3", frame_ms, alg, lib_sha="0" * 64)["pmc_stale"] is True
+    # with a device-code stamp the kernel sha decides (host-only library changes keep the counts)
+    if pm.get("kernel_sha256"):
+        assert bench.roofline("c3", frame_ms, alg, lib_sha="0" * 64, kernel_sha=pm["kernel_sha256"])["pmc_stale"] is False
+        assert bench.roofline("c3", frame_ms, alg, lib_sha=pm["lib_sha256"], kernel_sha="0" * 64)["pmc_stale"] is True
     # HBM bytes from the PMC passes: 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction), in KB
     assert pm["hbm_bytes_per_launch"] == pytest.approx((2 * pm["fetch_size_kb"] + pm["write_size_kb"]) * 1024,
                                                        rel=1e-6)
@@ -83,3 +87,14 @@ def test_committed_bench_lines_keep_the_contract():
     assert r["duration_ms"] == pytest.approx(d["ms_per_step"], rel=1e-3)
     assert r["isolated_kernel_ms"] > 0 and r["frac_isolated"] > 0
     assert d["dist"]["world_size"] == 1
+
+
+def test_kernel_sha_reads_the_device_code_section():
+    from dsgpuraytracing_amd import elfsha, native
+    lib = native.LIB_PATH
+    code = elfsha.section_bytes(lib, ".hip_fatbin")
+    assert len(code) > 100_000  # the gfx950 code objects of every kernel
+    assert elfsha.kernel_sha256(lib) == __import__("hashlib").sha256(code).hexdigest()
+    assert elfsha.kernel_sha256(lib) != elfsha.file_sha256(lib)
+    with pytest.raises(KeyError):
+        elfsha.section_bytes(lib, ".no_such_section")

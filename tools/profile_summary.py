@@ -23,6 +23,9 @@ import os
 import shutil
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dsgpuraytracing_amd.elfsha import kernel_sha256  # noqa: E402
+
 # render_kernel<STATS, DBG, BIN, ENV, GTAB>: the timed launch of each workload
 KERNELS = {"c5": "render_kernel<false, false, false, true, false>"}
 KERNEL = "render_kernel<false, false, false, false, false>"
@@ -73,6 +76,7 @@ def main():
         "workload": workload,
         "kernel": KERNEL,
         "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
+        "kernel_sha256": kernel_sha256(lib),
         "calls": int(render["Calls"]),
         "avg_ms": avg_ns / 1e6,
         "isolated_avg_ms": float(iso["AverageNs"]) / 1e6 if iso else None,
