@@ -623,7 +623,7 @@ def companions(dev0, local, stream, frames):
         once per 32x32 tile (1,024 calls, pathtracer.cpp:585-621) through one
         context, as INTEGRATION.md's adapter does -- asynchronously
         (pt_tile_submit: tiles batched into launches, completed into the
-        host sampleBuffer + toColor'd frameBuffer on stream callbacks) and with
+        host sampleBuffer + toColor'd frameBuffer by a completion thread) and with
         one synchronous pt_render_tiles launch per tile.  Host output
         included (PCIe), so these are never `value`."""
     import torch

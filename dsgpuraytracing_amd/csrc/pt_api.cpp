@@ -11,6 +11,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -183,9 +186,12 @@ struct pt_ctx {
   DevBuf<float> frame;  // device framebuffer for host-output renders
   // Asynchronous one-tile seam (pt_tile_submit / pt_tile_finish): submitted
   // tiles wait in `tq` until a batch of `tile_batch` is full, then render as
-  // ONE launch into `frame`, are copied to the pinned `stage` and completed
-  // (copied into the caller's sampleBuffer, toColor'd into its frameBuffer)
-  // by a host function on the context stream.
+  // ONE launch into `frame`; the rows the batch spans are copied to the
+  // batch's own pinned stage and an event is recorded behind the copy.  A
+  // completion thread (`tworker`) waits on that event and completes the
+  // batch -- copies its tiles into the caller's sampleBuffer and toColors them
+  // into its frameBuffer -- OFF the stream, so the next batch's render never
+  // waits for host work (a stream host function would serialise them).
   struct TileJob {
     int4 t;
     float* hdr;
@@ -193,14 +199,22 @@ struct pt_ctx {
   };
   struct TileBatch {
     std::vector<TileJob> jobs;
-    const float* stage;
-    int W, H;
+    float* stage = nullptr;  // pinned: rows y0 .. y0 + rows - 1 of the frame
+    size_t cap = 0;          // floats the stage holds
+    int y0 = 0, W = 0, H = 0;
+    hipEvent_t ev = nullptr;
   };
   std::vector<TileJob> tq;
-  std::vector<TileBatch*> tile_inflight;
-  int tile_batch = 64;
-  float* stage = nullptr;
-  size_t stage_n = 0;
+  int tile_batch = 256;  // tiles per launch (PT_TILE_BATCH): 256 beat 16-128 and 1024 (profiles/r3/seam_native_batch_sweep.txt)
+  std::mutex tmu;
+  std::condition_variable tcv;
+  std::deque<TileBatch*> tpending;  // rendered batches awaiting completion, in launch order
+  std::vector<TileBatch*> tfree;    // completed batches: stages and events for reuse
+  int tinflight = 0;                // batches launched and not yet completed
+  int terr = PT_OK;                 // first completion error (reported by pt_tile_finish)
+  std::string terrmsg;
+  bool tstop = false;
+  std::thread tworker;
   DevBuf<int> q_spill;  // ray-query stack spill
   DevBuf<unsigned long long> stats;
   DevBuf<float> q_f;    // ray-query scratch
@@ -263,6 +277,8 @@ int pt_create(int device, pt_ctx** out) {
   return PT_OK;
 }
 
+static void tile_worker_stop(pt_ctx* c);
+
 int pt_destroy(pt_ctx* c) {
   if (!c) return PT_OK;
   (void)hipSetDevice(c->device);
@@ -289,8 +305,7 @@ int pt_destroy(pt_ctx* c) {
     if (c->ev_free[k]) (void)hipEventDestroy(c->ev_free[k]);
     if (c->rstream[k]) (void)hipStreamDestroy(c->rstream[k]);
   }
-  for (auto* b : c->tile_inflight) delete b;
-  if (c->stage) (void)hipHostFree(c->stage);
+  tile_worker_stop(c);
   c->q_spill.release();
   c->frame.release();
   c->stats.release();
@@ -1257,54 +1272,141 @@ int pt_render_tiles_device(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, flo
 }
 
 // ---- asynchronous one-tile seam
-// Completion of one batch, on the context stream after its copy to `stage`
-// (a HIP host function: no HIP calls in here).  The tile's pixels go into
-// the caller's sampleBuffer and, as PathTracer::raytrace_tile does at its end
-// (pathtracer.cpp:610), through toColor into its frameBuffer.
-static void tile_done(void* arg) {
-  auto* b = static_cast<pt_ctx::TileBatch*>(arg);
+// Completion of one batch (on the completion thread, after the batch's event):
+// the tiles' pixels go from the batch's stage into the caller's sampleBuffer
+// and, as PathTracer::raytrace_tile does at its end (pathtracer.cpp:610),
+// through toColor into its frameBuffer.
+static void tile_complete(const pt_ctx::TileBatch* b) {
   for (const pt_ctx::TileJob& j : b->jobs) {
     for (int y = j.t.y; y < j.t.y + j.t.w; ++y) {
-      const size_t off = ((size_t)y * (size_t)b->W + (size_t)j.t.x) * 3;
-      std::memcpy(j.hdr + off, b->stage + off, (size_t)j.t.z * 3 * sizeof(float));
+      const size_t dst = ((size_t)y * (size_t)b->W + (size_t)j.t.x) * 3;
+      const size_t src = ((size_t)(y - b->y0) * (size_t)b->W + (size_t)j.t.x) * 3;
+      std::memcpy(j.hdr + dst, b->stage + src, (size_t)j.t.z * 3 * sizeof(float));
     }
     if (j.rgba) (void)pt_to_color(j.hdr, b->W, b->H, j.t.x, j.t.y, j.t.x + j.t.z, j.t.y + j.t.w, j.rgba);
   }
 }
 
+// The completion thread: batches in launch order; each waits for its own
+// event only, so completing batch k overlaps the render of batch k+1.
+static void tile_worker(pt_ctx* c) {
+  (void)hipSetDevice(c->device);
+  for (;;) {
+    pt_ctx::TileBatch* b = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(c->tmu);
+      c->tcv.wait(lk, [&] { return c->tstop || !c->tpending.empty(); });
+      if (c->tpending.empty()) return;  // stopping, nothing left to complete
+      b = c->tpending.front();
+      c->tpending.pop_front();
+    }
+    const hipError_t e = hipEventSynchronize(b->ev);
+    if (e == hipSuccess) tile_complete(b);
+    std::lock_guard<std::mutex> lk(c->tmu);
+    if (e != hipSuccess && c->terr == PT_OK) {
+      c->terr = PT_E_HIP;
+      c->terrmsg = std::string("tile completion: ") + hipGetErrorString(e);
+    }
+    b->jobs.clear();
+    c->tfree.push_back(b);
+    --c->tinflight;
+    c->tcv.notify_all();
+  }
+}
+
+static void tile_worker_stop(pt_ctx* c) {
+  if (c->tworker.joinable()) {
+    {
+      std::lock_guard<std::mutex> lk(c->tmu);
+      c->tstop = true;
+    }
+    c->tcv.notify_all();
+    c->tworker.join();  // drains the pending batches first
+  }
+  for (auto* b : c->tfree) {
+    if (b->stage) (void)hipHostFree(b->stage);
+    if (b->ev) (void)hipEventDestroy(b->ev);
+    delete b;
+  }
+  c->tfree.clear();
+}
+
 // Renders the queued tiles as one launch (nothing queued: nothing to do).
 static int tile_launch(pt_ctx* c) {
   if (!c || c->tq.empty()) return PT_OK;
+  constexpr int kMaxBatchesInFlight = 8;  // bounds the pinned staging memory
   std::vector<pt_ctx::TileJob> jobs;
   jobs.swap(c->tq);
   HIPCHK(hipSetDevice(c->device));
   const size_t W = (size_t)c->params.width, H = (size_t)c->params.height;
   std::vector<int4> tl;
   for (const auto& j : jobs) tl.push_back(j.t);
-  HIPCHK(c->frame.reserve(W * H * 3));
-  if (c->stage_n < W * H * 3) {
-    HIPCHK(hipStreamSynchronize(c->stream));  // earlier batches still copy into the old stage
-    if (c->stage) HIPCHK(hipHostFree(c->stage));
-    c->stage = nullptr;
-    c->stage_n = 0;
-    HIPCHK(hipHostMalloc((void**)&c->stage, W * H * 3 * sizeof(float), hipHostMallocDefault));
-    c->stage_n = W * H * 3;
-  }
-  if (int rc = launch(c, tl, c->frame.p, c->stream, 0)) return rc;
-  // one copy of the band of whole rows the batch's tiles span (a batch of the
-  // FIFO is a few tile rows): pixels of the band outside the tiles land in the
-  // stage only, never in the caller's buffers
+  // the band of whole rows the batch's tiles span (a batch of the FIFO is a
+  // few tile rows): one copy; pixels of the band outside the tiles land in
+  // the stage only, never in the caller's buffers
   int y0 = (int)H, y1 = 0;
   for (const int4& t : tl) {
     y0 = std::min(y0, t.y);
     y1 = std::max(y1, t.y + t.w);
   }
-  const size_t off = (size_t)y0 * W * 3;
-  HIPCHK(hipMemcpyAsync(c->stage + off, c->frame.p + off, (size_t)(y1 - y0) * W * 3 * sizeof(float),
-                        hipMemcpyDeviceToHost, c->stream));
-  auto* b = new pt_ctx::TileBatch{std::move(jobs), c->stage, (int)W, (int)H};
-  c->tile_inflight.push_back(b);
-  HIPCHK(hipLaunchHostFunc(c->stream, tile_done, b));
+  const size_t need = (size_t)(y1 - y0) * W * 3;
+  pt_ctx::TileBatch* b = nullptr;
+  {
+    std::unique_lock<std::mutex> lk(c->tmu);
+    if (!c->tworker.joinable()) {
+      c->tstop = false;
+      c->tworker = std::thread(tile_worker, c);
+    }
+    c->tcv.wait(lk, [&] { return !c->tfree.empty() || c->tinflight < kMaxBatchesInFlight; });
+    if (!c->tfree.empty()) {
+      b = c->tfree.back();
+      c->tfree.pop_back();
+    }
+  }
+  if (!b) b = new pt_ctx::TileBatch();
+  auto give_back = [&] {
+    std::lock_guard<std::mutex> lk(c->tmu);
+    c->tfree.push_back(b);
+  };
+  if (b->cap < need) {
+    if (b->stage) (void)hipHostFree(b->stage);
+    b->stage = nullptr;
+    b->cap = 0;
+    if (hipHostMalloc((void**)&b->stage, need * sizeof(float), hipHostMallocDefault) != hipSuccess) {
+      give_back();
+      return fail(PT_E_HIP, "pt_tile_submit: pinned staging allocation failed");
+    }
+    b->cap = need;
+  }
+  if (!b->ev && hipEventCreateWithFlags(&b->ev, hipEventDisableTiming) != hipSuccess) {
+    give_back();
+    return fail(PT_E_HIP, "pt_tile_submit: event creation failed");
+  }
+  if (hipError_t e = c->frame.reserve(W * H * 3); e != hipSuccess) {
+    give_back();
+    return fail(PT_E_HIP, std::string("pt_tile_submit: ") + hipGetErrorString(e));
+  }
+  if (int rc = launch(c, tl, c->frame.p, c->stream, 0)) {
+    give_back();
+    return rc;
+  }
+  hipError_t e = hipMemcpyAsync(b->stage, c->frame.p + (size_t)y0 * W * 3, need * sizeof(float),
+                                hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipEventRecord(b->ev, c->stream);
+  if (e != hipSuccess) {
+    give_back();
+    return fail(PT_E_HIP, std::string("pt_tile_submit: ") + hipGetErrorString(e));
+  }
+  b->jobs = std::move(jobs);
+  b->y0 = y0;
+  b->W = (int)W;
+  b->H = (int)H;
+  {
+    std::lock_guard<std::mutex> lk(c->tmu);
+    c->tpending.push_back(b);
+    ++c->tinflight;
+  }
+  c->tcv.notify_all();
   return finish_stats(c, c->stream, 0, false);
 }
 
@@ -1322,10 +1424,17 @@ int pt_tile_submit(pt_ctx* c, const pt_tile* tile, float* hdr_out_host, uint32_t
 int pt_tile_finish(pt_ctx* c) {
   if (!c) return fail(PT_E_INVALID, "NULL context");
   if (int rc = tile_launch(c)) return rc;
-  HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipStreamSynchronize(c->stream));  // every batch copied and completed
-  for (auto* b : c->tile_inflight) delete b;
-  c->tile_inflight.clear();
+  int err = PT_OK;
+  std::string msg;
+  {
+    std::unique_lock<std::mutex> lk(c->tmu);
+    c->tcv.wait(lk, [&] { return c->tinflight == 0; });  // every batch copied and completed
+    err = c->terr;
+    msg = c->terrmsg;
+    c->terr = PT_OK;
+    c->terrmsg.clear();
+  }
+  if (err != PT_OK) return fail(err, msg);
   return PT_OK;
 }
 

@@ -31,7 +31,7 @@
  *                               + PathTracer::updateBufferFromGPU (setup.cu:147-179,813-843)
  *   pt_tile_submit / pt_tile_finish   raytrace_tile from the reference's worker threads,
  *                               asynchronous: tiles batched into launches, each completed
- *                               (sampleBuffer + toColor) on a stream callback
+ *                               (sampleBuffer + toColor) by a completion thread
  *   pt_render_tiles_device      same, output left in device memory on a caller stream
  *                               (used for the multi-GPU framebuffer reduction)
  *   pt_intersect                BVHAccel::intersect(ray, isect) and BVHAccel::intersect(ray)
@@ -254,16 +254,20 @@ int pt_render_tiles_device(pt_ctx* ctx, const pt_tile* tiles, int32_t n_tiles, f
  * (src/pathtracer.cpp:585-611) as the reference's worker threads call it
  * (worker_thread, pathtracer.cpp:613-621), without one launch and one host
  * synchronisation per tile.  pt_tile_submit queues the tile and returns; queued
- * tiles render as ONE launch once PT_TILE_BATCH (default 64) are queued, or at
+ * tiles render as ONE launch once PT_TILE_BATCH (default 256) are queued, or at
  * pt_tile_finish.  When a tile's launch completes, its pixels are written into
  * hdr_out_host (the width*height*3 sampleBuffer) and, if rgba_out_host is not
- * NULL, toColor'd into it (the width*height frameBuffer, as pt_to_color), on a
- * runtime thread -- exactly what raytrace_tile leaves behind.  The caller keeps
+ * NULL, toColor'd into it (the width*height frameBuffer, as pt_to_color), by the
+ * context's completion thread, which waits on each launch's event off the
+ * render stream (so completing one batch overlaps the next batch's render) --
+ * exactly what raytrace_tile leaves behind.  At most 8 launched batches await
+ * completion; a submit beyond that waits for one.  The caller keeps
  * both buffers alive and does not write the tile's pixels until pt_tile_finish
  * returns.  pt_tile_finish renders what is still queued and waits for every
  * submitted tile.  Tiles render with the scene/camera/params of submission
  * (the setters and the synchronous renders first launch what is queued).  The
- * pixels equal those of a whole-frame pt_render_tiles bit for bit. */
+ * pixels equal those of a whole-frame pt_render_tiles bit for bit.  A failed
+ * completion (HIP error) is reported by the next pt_tile_finish. */
 int pt_tile_submit(pt_ctx* ctx, const pt_tile* tile, float* hdr_out_host, uint32_t* rgba_out_host);
 int pt_tile_finish(pt_ctx* ctx);
 /* Batched BVHAccel::intersect.  Rays: origin o[3n], direction d[3n] (normalised),

@@ -7,12 +7,16 @@ Chain:
       the robust fp32 ray offset flip a discrete decision)
   HIP  ~  reference (independent seeds)           statistical (noise floor)
 """
+import os
+
 import numpy as np
 import pytest
 
 from dsgpuraytracing_amd import native, ptdump
 from dsgpuraytracing_amd.pathtracer import PathTracer, Scene, tile_fifo
 from tests.oracle_helpers import golden
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -675,7 +679,7 @@ def test_hip_tile_workers_seam_bit_identical(monkeypatch, batch, threads, asynch
     """The reference's literal seam -- worker threads calling raytrace_tile
     once per 32x32 tile (pathtracer.cpp:585-621) -- through one context, in a
     shuffled tile order, asynchronously (pt_tile_submit: batched launches
-    completed on stream callbacks) or one synchronous launch per tile: the
+    completed by a completion thread) or one synchronous launch per tile: the
     sampleBuffer equals the whole-frame render bit for bit and the frameBuffer
     is its toColor."""
     from dsgpuraytracing_amd.pathtracer import to_color
@@ -708,6 +712,25 @@ def test_hip_tile_workers_seam_bit_identical(monkeypatch, batch, threads, asynch
     pt.frameBuffer[...] = 0
     pt.render_tile_workers(num_threads=threads, asynchronous=asynchronous, tiles=tiles[::-1])
     assert np.array_equal(pt.sampleBuffer, whole.sampleBuffer)
+
+
+@pytest.mark.parametrize("w,h,threads", [(256, 192, 8), (200, 136, 3)])
+def test_native_seam_bench_bit_identical(w, h, threads):
+    """tools/seam_bench.cpp -- C++ std::thread workers calling the one-tile
+    seam through one context, as INTEGRATION.md's adapter does -- checks both
+    seams (asynchronous pt_tile_submit, synchronous per-tile launches) against
+    the whole-frame render bit for bit (sampleBuffer and toColor frameBuffer)
+    and exits 3 when they differ."""
+    import json
+    import subprocess
+    exe = os.path.join(ROOT, "dsgpuraytracing_amd", "seam_bench")
+    assert os.path.exists(exe), "build() compiles tools/seam_bench.cpp"
+    r = subprocess.run([exe, os.path.join(ROOT, "assets", "CBspheres_lambertian.dae"), str(w), str(h), "4",
+                        str(threads), "2"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
+    assert r.returncode == 0, r.stderr.decode(errors="replace")[-500:]
+    d = json.loads(r.stdout.decode().strip().splitlines()[-1])
+    assert d["async_bit_identical"] and d["sync_bit_identical"]
+    assert d["tiles"] == ((w + 31) // 32) * ((h + 31) // 32)
 
 
 def test_hip_tile_submit_flushes_before_state_changes():

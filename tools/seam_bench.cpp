@@ -3,7 +3,7 @@
 // tiles from one FIFO (PathTracer::worker_thread, src/pathtracer.cpp:613-637)
 // and call raytrace_tile through ONE pt_ctx (calls serialised by a mutex).
 //   async: pt_tile_submit (tiles batched into launches, each completed into
-//          the sampleBuffer + toColor'd frameBuffer on a stream callback), the
+//          the sampleBuffer + toColor'd frameBuffer by the library's completion thread), the
 //          last worker's pt_tile_finish;
 //   sync:  one pt_render_tiles launch per tile + pt_to_color of the tile.
 // Also the whole frame as ONE pt_render_tiles call + pt_to_color (host output
