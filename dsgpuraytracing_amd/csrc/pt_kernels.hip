@@ -1218,27 +1218,48 @@ __host__ __device__ __forceinline__ int resolve_team(int n_groups) {
 // j sums groups j, j+k, j+2k, ... in order, then the team adds its k partial
 // sums by a fixed butterfly.  One lane per pixel read 12-B words n_groups * 12
 // B apart (C5: 3 KB stride, 1.4 TB/s); the team reads contiguous runs.
+// One workgroup per tile: a tile outside the scene's screen footprint is
+// written 0 row by row (no team, no partial-sum reads); otherwise the 256
+// lanes sweep the tile's rows 256/k pixels at a time (consecutive pixels'
+// group sums are contiguous).  One wave per 16 pixels measured 0.27 ms on C3
+// and 2.2 ms on C4/C5, mostly workgroup dispatch for the culled three
+// quarters of the frame.
 __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
-  const int k = resolve_team(P.n_groups);
-  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
-  const uint32_t tq = t / (uint32_t)k;  // pixel slot (k is a power of two: a shift)
-  const int j = (int)(t & (uint32_t)(k - 1));
-  const bool live = tq < (uint32_t)P.n_tiles * 1024u;
-  const int4 tile = live ? P.tiles[tq >> 10] : make_int4(0, 0, 0, 0);
-  int2 xy = live ? tile_pixel(tile, tq & 1023u) : make_int2(-1, -1);
-  float3 acc = f3(0, 0, 0);
-  if (xy.x >= 0 && !culled(P, xy.x, xy.y)) {
-    const float* p = P.partial + 3 * ((size_t)xy.x + (size_t)xy.y * (size_t)P.W) * (size_t)P.n_groups;
-    for (int g = j; g < P.n_groups; g += k) acc = acc + ld3(p + 3 * g);
+  const int ti = (int)blockIdx.x;
+  const int4 tile = P.tiles[ti];
+  const int tid = (int)threadIdx.x;
+  const bool outside = tile.x > P.cull_x1 || tile.x + tile.z - 1 < P.cull_x0 || tile.y > P.cull_y1 ||
+                       tile.y + tile.w - 1 < P.cull_y0;
+  if (outside) {
+    const int rowf = tile.z * 3;  // floats per tile row
+    for (int i = tid; i < rowf * tile.w; i += 256) {
+      const int r = i / rowf, c = i - r * rowf;
+      const size_t o = P.packed ? ((size_t)ti * 1024u + (size_t)r * 32u) * 3u + (size_t)c
+                                : ((size_t)(tile.y + r) * (size_t)P.W + (size_t)tile.x) * 3u + (size_t)c;
+      P.out[o] = 0.0f;
+    }
+    return;
   }
-  // team lanes are consecutive, aligned, and all reach the shuffles
-  for (int off = 1; off < k; off <<= 1)
-    acc = acc + f3(__shfl_xor(acc.x, off), __shfl_xor(acc.y, off), __shfl_xor(acc.z, off));
-  if (xy.x < 0 || j != 0) return;
+  const int k = resolve_team(P.n_groups);
+  const int per = 256 / k;  // pixels per sweep step
+  const int j = tid & (k - 1);
   const float inv_spp = (float)(1.0 / (double)P.spp);
-  const size_t o = P.packed ? (size_t)(tq & ~1023u) + (size_t)((xy.y - tile.y) * 32 + (xy.x - tile.x))
-                            : (size_t)xy.x + (size_t)xy.y * (size_t)P.W;
-  store3(P.out + 3 * o, acc * inv_spp);
+  for (int base = 0; base < 1024; base += per) {  // uniform trip count: every lane reaches the shuffles
+    const int q = base + tid / k;                 // pixel of the tile, row-major 32 x 32
+    const int x = tile.x + (q & 31), y = tile.y + (q >> 5);
+    const bool in_tile = (q & 31) < tile.z && (q >> 5) < tile.w;
+    float3 acc = f3(0, 0, 0);
+    if (in_tile && !culled(P, x, y)) {
+      const float* p = P.partial + 3 * ((size_t)x + (size_t)y * (size_t)P.W) * (size_t)P.n_groups;
+      for (int g = j; g < P.n_groups; g += k) acc = acc + ld3(p + 3 * g);
+    }
+    for (int off = 1; off < k; off <<= 1)
+      acc = acc + f3(__shfl_xor(acc.x, off), __shfl_xor(acc.y, off), __shfl_xor(acc.z, off));
+    if (in_tile && j == 0) {
+      const size_t o = P.packed ? (size_t)ti * 1024u + (size_t)q : (size_t)x + (size_t)y * (size_t)P.W;
+      store3(P.out + 3 * o, acc * inv_spp);
+    }
+  }
 }
 
 // Batched BVHAccel::intersect queries, one lane per ray.
@@ -1318,8 +1339,8 @@ extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, 
 }
 
 extern "C" hipError_t ptk_launch_resolve(const KParams* P, hipStream_t s) {
-  int grid = (int)(((int64_t)P->n_tiles * 1024 * ptk::resolve_team(P->n_groups) + 255) / 256);
-  hipLaunchKernelGGL(ptk::resolve_kernel, dim3(grid), dim3(256), 0, s, *P);
+  if (P->n_tiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(ptk::resolve_kernel, dim3(P->n_tiles), dim3(256), 0, s, *P);
   return hipGetLastError();
 }
 
