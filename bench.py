@@ -307,7 +307,8 @@ def main():
     ap.add_argument("--scene-dump", default=None, help="PTDUMP scene instead of the native .dae loader")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
-                    help="N = 1: skip the companion measurements (framed C3, single-GPU C4 and C5, C3 over the GPU LBVH)")
+                    help="skip the companion measurements (N = 1: framed C3, single-GPU C4 and C5, host-SAH tree, "
+                         "per-tile seams; N > 1: strong scaling of the C3 and C4 frames)")
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
                     help="default: c3 (the headline config) at every N")
     ap.add_argument("--lbvh", action="store_true", help="build the BVH on the GPU (pt_upload_scene_lbvh)")
@@ -484,6 +485,12 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
         dist.all_gather(allr, mine)
         per_rank = [[round(float(v), 4) for v in r.cpu().tolist()] for r in allr]
 
+    strong = None
+    if world > 1 and not args.no_extras and weak:
+        # every rank takes part (collectives inside)
+        strong = strong_companions(local, rank, world, backend, StepGuard, TileExchange,
+                                   frames=max(3, min(args.steps, 10)))
+
     host_ms = None
     single_ms = None
     iso_ms = 0.0
@@ -564,6 +571,8 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
         out["ray_casts_per_s_M"] = round(rays * frames * (world if weak else 1) / elapsed / 1e6, 1)
         if per_rank is not None:
             out["per_rank"] = {"fields": ["kernel_ms", "resolve_ms", "exchange_ms", "pixels"], "ranks": per_rank}
+        if strong is not None:
+            out["companions"] = strong
         elif xev:
             out["exchange_ms"] = round(xchg_ms, 4)
         if world == 1 and not args.no_extras and workload == "c3" and not args.scene_dump:
@@ -588,6 +597,65 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
             except Exception as e:  # reported, never silently replaced
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
+
+
+def strong_companions(local, rank, world, backend, StepGuard, TileExchange, frames=5, warmup=2):
+    """N > 1 companions (never `value`): STRONG scaling of one frame -- its
+    32x32 tiles dealt diagonally over the N GPUs, each rank rendering its
+    tiles into a packed buffer, ONE RCCL gather onto rank 0
+    -- for the headline C3 frame and for BASELINE C4 (1080p, 256 spp, the
+    multi-GPU config).  Same clock as the headline: barrier + synchronise on
+    both sides of `frames` back-to-back frames, max over ranks; value =
+    W*H*spp*frames / that time.  Images are bit-identical to 1 GPU
+    (tests/test_dist.py, test_c4_fullsize_eight_way_split_bit_identical)."""
+    import torch
+    import torch.distributed as dist
+
+    from dsgpuraytracing_amd.pathtracer import Device, Scene, tile_fifo
+    res = {}
+    stream = torch.cuda.current_stream().cuda_stream
+    for name in ("c3", "c4"):
+        wl = WORKLOADS[name]
+        w, h, spp = wl["w"], wl["h"], wl["spp"]
+        dae, envmap, cam = workload_scene(wl)
+        sc = Scene.from_dae(dae, w, h, cam_info=cam, envmap=envmap)
+        dev = Device(local)
+        dev.upload_scene(sc)
+        dev.set_camera(sc.camera)
+        dev.set_params(w, h, spp, DEPTH, NSL, SEED)
+        frame = torch.zeros((h, w, 3), dtype=torch.float32, device=f"cuda:{local}")
+        ex = TileExchange(tile_fifo(w, h), w, h, rank, world, frame.device)
+        mine = np.asarray(ex.mine, dtype=np.int32).reshape(-1, 4)
+        guard = StepGuard()
+
+        def step():
+            guard.run(dev.render_tiles_device, mine, ex.packed.data_ptr(), stream, packed=True)
+            ex.exchange(frame)
+
+        for _ in range(warmup):
+            step()
+        guard.check()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            step()
+        dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        guard.check()
+        t = torch.tensor([el], dtype=torch.float64, device="cpu" if backend == "gloo" else f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        res[f"{name}_strong"] = {
+            "workload": wl["desc"] + f", one frame's tiles over {world} GPUs + one gather (strong)",
+            "value": round(w * h * spp * frames / el / 1e6, 1), "unit": "Mrays/s",
+            "ms_per_frame": round(el / frames * 1e3, 3), "frames": frames, "scaling": "strong",
+            "gather_bytes_per_rank": int(ex.packed.numel() * 4),
+            "image_mean": float(frame.mean().item()) if rank == 0 else None}
+        dev.close()
+        del frame, ex
+    return res
 
 
 def bvh_desc(lbvh=False):
