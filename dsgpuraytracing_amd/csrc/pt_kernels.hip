@@ -578,6 +578,11 @@ __device__ __forceinline__ void env_sample(const KParams& P, float r1, float r2,
 
 // Lane modes of the persistent kernel.
 enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
+// What follows a lane's shadow ray (the `shadow` state; 0 = not a shadow ray).
+enum : int { SH_RESUME = 1, SH_FOLLOW = 2, SH_GROUP_END = 3 };
+#ifndef PT_FOLLOW
+#define PT_FOLLOW 1
+#endif
 
 // Wave-clock sections of the STATS build: every shader clock of a wave's
 // lifetime falls in exactly one (pt_stats.shade_clocks + trav_clocks = the
@@ -652,7 +657,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
 
   // ---- per-lane state
   int mode = M_FETCH;
-  bool shadow = false;  // the ray in flight is a shadow ray
+  // the ray in flight: 0 extension (camera / bounce) ray, else a shadow ray
+  // followed by -- SH_RESUME: the shading round (NEE resumes at the cursor);
+  // SH_FOLLOW: the next extension ray, already sampled (origin in hp,
+  // direction in ns), started inside the traversal loop; SH_GROUP_END: the
+  // shading round that stores the finished group and refills
+  int shadow = 0;
   // the work slot (pixel, sample group) this lane renders: its pixel as packed
   // coordinates (x | y << 16; W, H <= 65535) and its current sample; the
   // group is sample / group_spp
@@ -716,17 +726,42 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   };
   const uint32_t total_slots = (uint32_t)P.n_blocks * 64u * n_groups;
   const int batch = P.shade_batch;
+  // Camera::generate_ray (camera.cpp:113-129) for the lane's pixel and
+  // current sample, at the jittered position of raytrace_pixel
+  // (pathtracer.cpp:571-575); starts the sample's random stream.  Returns
+  // whether the ray enters the scene's root box (a ray that misses it sees
+  // nothing but the environment: pathtracer.cpp:421-426).
+  auto camera_ray = [&](Trav& t) -> bool {
+    const int px = pix & 0xffff, py = (int)((uint32_t)pix >> 16);
+    rbase = ptrng::stream_base(P.seed, (uint32_t)(px + py * P.W), (uint32_t)sample + P.sample_base);
+    rdim = ptrng::kDrawInit;
+    float ry = PT_DRAW();  // UniformGridSampler2D draws y first
+    float rx = PT_DRAW();
+    float fx = ((float)px + rx) * P.inv_w;
+    float fy = ((float)py + ry) * P.inv_h;
+    float3 sp = f3((0.5f - fx) * P.cam_ax, (0.5f - fy) * P.cam_ay, 1.0f);
+    float3 wsp = ld3(P.c2w_col0) * sp.x + ld3(P.c2w_col1) * sp.y + ld3(P.c2w_col2) * sp.z;
+    float3 d = normalize(f3(0, 0, 0) - wsp);
+    trav_init(t, wsp + ld3(P.cam_pos), d, 3.0e38f, false);
+    if (STATS) n_cam++;
+    if (DBG && pix_index(pix) == P.dbg_pix) printf("pixel (%d,%d) sample %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g)\n", px, py, sample, t.o.x, t.o.y, t.o.z, d.x, d.y, d.z);
+    return box_hit(t, P.root_lo, P.root_hi);
+  };
 
   for (;;) {
     // ================= shading phase: lanes whose ray finished =================
     if (mode == M_SHADE) {
       const bool found = tr.found;
       bool finish = false;  // the sample is complete
+      bool group_end = false;  // the group's last sample ended with the shadow ray just finished
+      bool after = false;      // the sample's last shadow ray is emitted: the bounce / camera ray follows it
       int stage;            // 0: NEE (+ bounce), 2: none
       if (shadow) {
         if (!found) acc = acc + pend;  // unoccluded (the light sample was already counted)
         if (DBG && pix_index(pix) == P.dbg_pix) printf("    shadow %s (pend %.6g) prim %d t %.9g\n", found ? "occluded" : "clear", pend.x, tr.prim, tr.tmax);
-        stage = 0;
+        group_end = PT_FOLLOW && shadow == SH_GROUP_END;
+        stage = group_end ? 2 : 0;
+        shadow = 0;
       } else if (!found) {
         // miss: the environment map if there is one and includeLe (pathtracer.cpp:411-427)
         if (ENV && includeLe) acc = acc + mul(T, env_dir(P, tr.d));
@@ -843,13 +878,23 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           if (STATS) n_shadow++;
           break;
         }
+        // the shadow ray just emitted is the vertex's last light sample
+        const bool emit_last = PT_FOLLOW && emitted && li + 1 >= P.n_lights &&
+                               ls >= ((__float_as_int(light_f(li, 0)) | 2) == 2 ? 1 : P.ns_area);
         cur = (cur & 0xffu) | ((uint32_t)ls << 8) | ((uint32_t)li << 16);
         PT_STAMP(S_NEE);
-        if (emitted) {
-          shadow = true;
+        // With more light samples to take, the bounce waits for the shading
+        // round after the last shadow ray.  After the last one it is sampled
+        // now (every light draw precedes the BSDF draws, as in trace_ray) and
+        // the lane goes on with the next extension ray -- the bounce, or the
+        // next sample's camera ray -- where the shadow ray ends, inside the
+        // traversal loop: one shading round per path vertex, not two.
+        if (emitted && !emit_last) {
+          shadow = SH_RESUME;
           mode = M_TRAV;
         } else if ((int)(cur & 0xffu) >= P.max_depth) {
           finish = true;
+          after = emitted;
         } else {
           // ---- indirect bounce (pathtracer.cpp:527-552)
           float3 wi;
@@ -909,13 +954,20 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           if (PT_DRAW() < pterm) {
             if (DBG && pix_index(pix) == P.dbg_pix) printf("    RR terminate (p=%.4g)\n", pterm);
             finish = true;
+            after = emitted;
           } else {
             if (DBG && pix_index(pix) == P.dbg_pix) printf("    bounce wi=(%.6g %.6g %.6g) pdf %.5g p %.4g dim word %08x\n", wi.x, wi.y, wi.z, pdf, pterm, rdim);
             T = mul(T, f * (fabsf(wi.z) * rcp(pdf * (1.0f - pterm))));
             float3 v = normalize(fr.to_world(wi));
             const float3 bo = offset_ray(hp, dot(v, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng);
-            trav_init(tr, bo, v, 3.0e38f, false);
-            shadow = false;
+            if (emitted) {  // (only Diffuse emits shadow rays, so tr.d above was never read)
+              hp = bo;      // the bounce ray waits in (hp, ns) behind the shadow ray in tr
+              ns = v;
+              shadow = SH_FOLLOW;
+            } else {
+              trav_init(tr, bo, v, 3.0e38f, false);
+              shadow = 0;
+            }
             mode = M_TRAV;
             includeLe = btype == 1 || btype == 2 || btype == 3;
             ++cur;  // depth + 1
@@ -926,12 +978,19 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       if (finish) {
         ++sample;
         if (sample < P.spp && !group_starts(sample)) {
-          mode = M_CAMERA;
+          mode = M_CAMERA;  // after a shadow ray: the camera ray goes to (hp, ns), behind it
+          if (after) shadow = SH_FOLLOW;
+        } else if (after) {
+          shadow = SH_GROUP_END;
+          mode = M_TRAV;
         } else {
-          store3(P.partial + 3 * slot_of(pix, sample), acc);
-          PT_SLOT_DONE();
-          mode = M_FETCH;
+          group_end = true;
         }
+      }
+      if (group_end) {
+        store3(P.partial + 3 * slot_of(pix, sample), acc);
+        PT_SLOT_DONE();
+        mode = M_FETCH;
       }
       PT_STAMP(S_BSDF);
     }
@@ -1032,35 +1091,36 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       PT_STAMP(S_FETCH);
       // ---- camera rays: Camera::generate_ray (camera.cpp:113-129) at the
       // jittered pixel position of raytrace_pixel (pathtracer.cpp:571-575)
+      // A lane whose shadow ray is still to be traced (shadow != 0: the
+      // sample ended with its last light sample) keeps that ray in tr and
+      // parks the camera ray in (hp, ns), to start when the shadow ray ends.
       while (mode == M_CAMERA) {
-        const int px = pix & 0xffff, py = (int)((uint32_t)pix >> 16);
-        rbase = ptrng::stream_base(P.seed, (uint32_t)(px + py * P.W), (uint32_t)sample + P.sample_base);
-        rdim = ptrng::kDrawInit;
-        float ry = PT_DRAW();  // UniformGridSampler2D draws y first
-        float rx = PT_DRAW();
-        float fx = ((float)px + rx) * P.inv_w;
-        float fy = ((float)py + ry) * P.inv_h;
-        float3 sp = f3((0.5f - fx) * P.cam_ax, (0.5f - fy) * P.cam_ay, 1.0f);
-        float3 wsp = ld3(P.c2w_col0) * sp.x + ld3(P.c2w_col1) * sp.y + ld3(P.c2w_col2) * sp.z;
-        float3 d = normalize(f3(0, 0, 0) - wsp);
-        trav_init(tr, wsp + ld3(P.cam_pos), d, 3.0e38f, false);
-        if (STATS) n_cam++;
-        if (DBG && pix_index(pix) == P.dbg_pix) printf("pixel (%d,%d) sample %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g)\n", px, py, sample, tr.o.x, tr.o.y, tr.o.z, d.x, d.y, d.z);
-        if (box_hit(tr, P.root_lo, P.root_hi)) {
+        Trav cr;
+        const bool in = camera_ray(cr);
+        if (!shadow) tr = cr;
+        if (in) {
           T = f3(1, 1, 1);
           cur = 0;  // depth 0
           includeLe = true;
-          shadow = false;
+          if (shadow) {
+            hp = cr.o;
+            ns = cr.d;
+          }
           mode = M_TRAV;
           break;
         }
         // miss: the sample sees the environment (includeLe) or nothing
-        if (ENV) acc = acc + env_dir(P, d);
+        if (ENV) acc = acc + env_dir(P, cr.d);
         ++sample;
         if (sample >= P.spp || group_starts(sample)) {
-          store3(P.partial + 3 * slot_of(pix, sample), acc);
-          PT_SLOT_DONE();
-          mode = M_FETCH;
+          if (shadow) {
+            shadow = SH_GROUP_END;
+            mode = M_TRAV;
+          } else {
+            store3(P.partial + 3 * slot_of(pix, sample), acc);
+            PT_SLOT_DONE();
+            mode = M_FETCH;
+          }
         }
       }
       PT_STAMP(S_CAMERA);
@@ -1119,6 +1179,16 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         else done = node_step<STATS>(P.nodes, stk, tr, ct);
       }
       if (done) mode = M_SHADE;
+      // a shadow ray ended with the next extension ray already sampled: add
+      // the light sample and go on with that ray, no shading round
+      if (PT_FOLLOW && __ballot(done && shadow == SH_FOLLOW) != 0ull) {
+        if (done && shadow == SH_FOLLOW) {
+          if (!tr.found) acc = acc + pend;
+          trav_init(tr, hp, ns, 3.0e38f, false);
+          shadow = 0;
+          mode = M_TRAV;
+        }
+      }
       if (STATS && done) {
         ray_steps_max = max(ray_steps_max, r_steps);
         ray_idle_max = max(ray_idle_max, r_idle);
