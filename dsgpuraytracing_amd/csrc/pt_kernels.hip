@@ -123,6 +123,7 @@ __device__ __forceinline__ Frame make_frame(float3 n) {
 // "modifies" them): the loads must be issued before it and cannot be sunk
 // into later branches (node steps, leaf steps and the hit record).
 #define PT_FENCE4(v) asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w))
+#define PT_FENCE3(v) asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z))
 
 struct RayState {
   float3 o, d;
@@ -147,8 +148,17 @@ struct Trav {
   float tmax;
   int node, sp;
   int prim;
+  int pl;  // a postponed leaf cursor (0: none), PT_POSTPONE
   bool any, found;
 };
+
+// Speculative traversal (Aila & Laine 2009): when a node step's nearest hit
+// child is a leaf and the next one a node, the lane postpones the leaf (tr.pl)
+// and takes the node step, so it keeps stepping nodes with the wave; the leaf
+// is tested in the wave's next leaf iteration or when the stack runs empty.
+#ifndef PT_POSTPONE
+#define PT_POSTPONE 0
+#endif
 
 __device__ __forceinline__ void trav_init(Trav& tr, float3 o, float3 d, float tmax, bool any) {
   const float kTiny = 1e-20f;
@@ -163,6 +173,7 @@ __device__ __forceinline__ void trav_init(Trav& tr, float3 o, float3 d, float tm
   tr.any = any;
   tr.found = false;
   tr.prim = -1;
+  tr.pl = 0;
 }
 
 // Moller-Trumbore terms of one triangle (u, v, t; det = 0 means parallel).
@@ -271,7 +282,14 @@ struct Stack {
 };
 
 __device__ __forceinline__ bool trav_pop(const Stack& stk, Trav& tr) {
-  if (tr.sp == 0) return true;
+  if (tr.sp == 0) {
+    if (PT_POSTPONE && tr.pl != 0) {  // the postponed leaf is the last thing left
+      tr.node = tr.pl;
+      tr.pl = 0;
+      return false;
+    }
+    return true;
+  }
   --tr.sp;
   tr.node = stk.get(tr.sp);
   return false;
@@ -301,6 +319,8 @@ __device__ __forceinline__ bool node_order(const Stack& stk, Trav& tr, const flo
   cswap(d1, r1, d3, r3);
   cswap(d1, r1, d2, r2);
   if (d0 == kMiss) return trav_pop(stk, tr);
+  // postpone the nearest child when it is a leaf and the next hit child a node
+  const bool pp = PT_POSTPONE && tr.pl == 0 && r0 < 0 && r1 >= 0 && d1 != kMiss;
   // push the farther hits (farthest first), continue with the nearest.  The
   // hits are a sorted prefix, so with room for three entries every candidate
   // is written and the top only advances past hits (no branches).
@@ -311,14 +331,15 @@ __device__ __forceinline__ bool node_order(const Stack& stk, Trav& tr, const flo
     stk.lds[sp * PT_BLOCK] = r2;
     sp += d2 != kMiss;
     stk.lds[sp * PT_BLOCK] = r1;
-    sp += d1 != kMiss;
+    sp += d1 != kMiss && !pp;
   } else {
     if (d3 != kMiss) stk.put(sp++, r3);
     if (d2 != kMiss) stk.put(sp++, r2);
-    if (d1 != kMiss) stk.put(sp++, r1);
+    if (d1 != kMiss && !pp) stk.put(sp++, r1);
   }
   tr.sp = sp;
-  tr.node = r0;
+  tr.node = pp ? r1 : r0;
+  if (PT_POSTPONE) tr.pl = pp ? r0 : tr.pl;
   return false;
 }
 
@@ -434,8 +455,11 @@ __device__ __forceinline__ int leaf_count(int cur) { return ((~cur) & 7) + 1; }
 template <bool STATS>
 __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const Stack& stk, Trav& tr,
                                           Counters& ct) {
-  const int pa = leaf_first(tr.node);
-  const int n = leaf_count(tr.node);
+  // the lane's current leaf, or (at a node) its postponed one
+  const bool main = !PT_POSTPONE || tr.node < 0;
+  const int lc = main ? tr.node : tr.pl;
+  const int pa = leaf_first(lc);
+  const int n = leaf_count(lc);
   const bool two = n >= 2;
   const int pb = two ? pa + 1 : pa;
   float4 a0 = prims[pa].v0, a1 = prims[pa].e1, a2 = prims[pa].e2;
@@ -450,7 +474,13 @@ __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const
   if (prim_test<STATS>(a0, a1, a2, pa, tr, ct)) return true;
   if (two && prim_test<STATS>(b0, b1, b2, pb, tr, ct)) return true;
   if (n > 2) {
-    tr.node = ~(((pa + 2) << 3) | (n - 3));
+    const int next = ~(((pa + 2) << 3) | (n - 3));
+    if (main) tr.node = next;
+    else tr.pl = next;
+    return false;
+  }
+  if (!main) {
+    tr.pl = 0;
     return false;
   }
   return trav_pop(stk, tr);
@@ -579,9 +609,19 @@ __device__ __forceinline__ void env_sample(const KParams& P, float r1, float r2,
 // Lane modes of the persistent kernel.
 enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 // What follows a lane's shadow ray (the `shadow` state; 0 = not a shadow ray).
-enum : int { SH_RESUME = 1, SH_FOLLOW = 2, SH_GROUP_END = 3 };
+enum : int { SH_RESUME = 1, SH_FOLLOW = 2, SH_GROUP_END = 3, SH_STORE = 4, SH_STORE_FOLLOW = 5 };
 #ifndef PT_FOLLOW
 #define PT_FOLLOW 1
+#endif
+#ifndef PT_EARLY_STORE
+#if PT_ENV_TU
+#ifndef PT_EARLY_STORE_ENV
+#define PT_EARLY_STORE_ENV 1
+#endif
+#define PT_EARLY_STORE PT_EARLY_STORE_ENV
+#else
+#define PT_EARLY_STORE 1
+#endif
 #endif
 
 // Wave-clock sections of the STATS build: every shader clock of a wave's
@@ -661,8 +701,13 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // followed by -- SH_RESUME: the shading round (NEE resumes at the cursor);
   // SH_FOLLOW: the next extension ray, already sampled (origin in hp,
   // direction in ns), started inside the traversal loop; SH_GROUP_END: the
-  // shading round that stores the finished group and refills
+  // shading round that stores the finished group and refills; SH_STORE: the
+  // group already ended -- its total without the light sample is stored, the
+  // total with it waits in pend and is stored over it (at oslot) if the
+  // shadow ray is clear, then the lane retires (the queue is drained) or, with
+  // SH_STORE_FOLLOW, goes on with the next group's camera ray in (hp, ns)
   int shadow = 0;
+  uint32_t oslot = 0;
   // the work slot (pixel, sample group) this lane renders: its pixel as packed
   // coordinates (x | y << 16; W, H <= 65535) and its current sample; the
   // group is sample / group_spp
@@ -746,6 +791,28 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     if (STATS) n_cam++;
     if (DBG && pix_index(pix) == P.dbg_pix) printf("pixel (%d,%d) sample %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g)\n", px, py, sample, t.o.x, t.o.y, t.o.z, d.x, d.y, d.z);
     return box_hit(t, P.root_lo, P.root_hi);
+  };
+
+  // A shadow ray ended (`done`) with what follows it already settled: add the
+  // light sample (or store the group's total with it) and go on with the
+  // next extension ray -- or retire -- without a shading round.
+  auto follow_on = [&](bool done) {
+    if (PT_FOLLOW && __ballot(done && shadow >= SH_FOLLOW && shadow != SH_GROUP_END) != 0ull) {
+      if (done && shadow >= SH_FOLLOW && shadow != SH_GROUP_END) {
+        if (shadow == SH_FOLLOW) {
+          if (!tr.found) acc = acc + pend;
+        } else if (!tr.found) {
+          store3(P.partial + 3 * (size_t)oslot, pend);  // the group's total with the light sample
+        }
+        if (shadow == SH_STORE) {
+          mode = M_DONE;
+        } else {
+          trav_init(tr, hp, ns, 3.0e38f, false);
+          mode = M_TRAV;
+        }
+        shadow = 0;
+      }
+    }
   };
 
   for (;;) {
@@ -981,8 +1048,18 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           mode = M_CAMERA;  // after a shadow ray: the camera ray goes to (hp, ns), behind it
           if (after) shadow = SH_FOLLOW;
         } else if (after) {
-          shadow = SH_GROUP_END;
-          mode = M_TRAV;
+          if (PT_EARLY_STORE) {  // store now, refill in this round (the shadow ray waits)
+            PT_FENCE3(pend);  // (no contraction into pend's last multiply: the sum rounds as at the shadow ray's return)
+            pend = acc + pend;
+            oslot = (uint32_t)slot_of(pix, sample);
+            store3(P.partial + 3 * (size_t)oslot, acc);
+            PT_SLOT_DONE();
+            shadow = SH_STORE;
+            mode = M_FETCH;
+          } else {
+            shadow = SH_GROUP_END;
+            mode = M_TRAV;
+          }
         } else {
           group_end = true;
         }
@@ -1057,7 +1134,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
           uint32_t slot = rank < avail ? chunk_next + rank : nbase + (rank - avail);
           if (slot >= total_slots) {
-            mode = M_DONE;
+            mode = (PT_EARLY_STORE && shadow) ? M_TRAV : M_DONE;  // (a pending shadow ray is traced first)
             if (STATS && w_empty == 0ull) w_empty = wall_clock64();
           } else {
             // slot = (block * 64 + pixel-in-block) * n_groups + group: the
@@ -1105,6 +1182,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           if (shadow) {
             hp = cr.o;
             ns = cr.d;
+            if (shadow == SH_STORE) shadow = SH_STORE_FOLLOW;
           }
           mode = M_TRAV;
           break;
@@ -1113,10 +1191,18 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if (ENV) acc = acc + env_dir(P, cr.d);
         ++sample;
         if (sample >= P.spp || group_starts(sample)) {
-          if (shadow) {
+          if (shadow == SH_FOLLOW && PT_EARLY_STORE) {  // the pending light sample belongs to this group
+            PT_FENCE3(pend);  // (no contraction into pend's last multiply: the sum rounds as at the shadow ray's return)
+            pend = acc + pend;
+            oslot = (uint32_t)slot_of(pix, sample);
+            store3(P.partial + 3 * (size_t)oslot, acc);
+            PT_SLOT_DONE();
+            shadow = SH_STORE;
+            mode = M_FETCH;
+          } else if (shadow == SH_FOLLOW) {
             shadow = SH_GROUP_END;
             mode = M_TRAV;
-          } else {
+          } else {  // (no pending light sample, or one of an earlier group)
             store3(P.partial + 3 * slot_of(pix, sample), acc);
             PT_SLOT_DONE();
             mode = M_FETCH;
@@ -1136,9 +1222,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     // copy: the wave's first traversal iteration no longer waits on a global
     // load for them.
     if constexpr (!BIN) {
+      bool done = false;
       if (mode == M_TRAV && tr.node == 0) {
-        if (node_step<STATS, true>(P.nodes, stk, tr, ct, (lds_cchar*)&s_root)) mode = M_SHADE;
+        done = node_step<STATS, true>(P.nodes, stk, tr, ct, (lds_cchar*)&s_root);
+        if (done) mode = M_SHADE;
       }
+      follow_on(done);  // (a shadow ray leaves the root only if it misses every child box)
     }
     // Once the queue is drained, lanes retire (M_DONE): shade when 3/4 of the
     // lanes still working are ready, not when `batch` of 64 are, or the tail
@@ -1172,23 +1261,15 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         l_deep += trav && tr.sp > PT_STACK;
       }
       if (leaf_iter) {
-        if (at_leaf) done = leaf_step<STATS>(P.prims, stk, tr, ct);
+        // (node lanes holding a postponed leaf test it too)
+        if (at_leaf || (PT_POSTPONE && trav && tr.pl != 0)) done = leaf_step<STATS>(P.prims, stk, tr, ct);
         if (STATS) n_leafit += lane == 0;
       } else if (trav && !at_leaf) {
         if constexpr (BIN) done = node_step2<STATS>(P.nodes2, stk, tr, ct);
         else done = node_step<STATS>(P.nodes, stk, tr, ct);
       }
       if (done) mode = M_SHADE;
-      // a shadow ray ended with the next extension ray already sampled: add
-      // the light sample and go on with that ray, no shading round
-      if (PT_FOLLOW && __ballot(done && shadow == SH_FOLLOW) != 0ull) {
-        if (done && shadow == SH_FOLLOW) {
-          if (!tr.found) acc = acc + pend;
-          trav_init(tr, hp, ns, 3.0e38f, false);
-          shadow = 0;
-          mode = M_TRAV;
-        }
-      }
+      follow_on(done);
       if (STATS && done) {
         ray_steps_max = max(ray_steps_max, r_steps);
         ray_idle_max = max(ray_idle_max, r_idle);

@@ -33,3 +33,6 @@ for name, dae, env, cam, w, h, spp, depth, nsl in CASES:
     dev.render_tiles(tile_fifo(w, h), out)
     dev.close()
     print(name, hashlib.sha256(out.tobytes()).hexdigest()[:16], f"{float(out.mean()):.6f}", flush=True)
+    if os.environ.get("IMG_SAVE"):  # directory for the frames (offline diffs between builds)
+        os.makedirs(os.environ["IMG_SAVE"], exist_ok=True)
+        np.save(os.path.join(os.environ["IMG_SAVE"], name + ".npy"), out)
