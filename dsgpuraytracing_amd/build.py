@@ -31,7 +31,7 @@ def _headers():
 
 
 def up_to_date() -> bool:
-    if os.environ.get("PT_HIPCC_FLAGS") or os.environ.get("PT_KERNEL_SCHED"):
+    if os.environ.get("PT_HIPCC_FLAGS") or os.environ.get("PT_KERNEL_SCHED") or os.environ.get("PT_ENV_SCHED"):
         return False
     if not os.path.exists(LIB):
         return False
@@ -67,9 +67,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
             # (render_kernel 103 -> 99 VGPRs; C3 +3.5%)
             cmd.insert(1, "-fno-slp-vectorize")
         sched = os.environ.get("PT_KERNEL_SCHED", "ilp")  # experiments: "default" drops the ILP scheduler
-        if (base == "pt_kernels.hip" and sched == "ilp") or (base == "pt_kernels_env.hip" and os.environ.get("PT_ENV_SCHED") == "ilp"):
-            # iterative-ILP machine scheduling: C3 +1.7%, framed C3 +1.8% (the
-            # ENV kernels, -2.9% with it, live in pt_kernels_env.hip without it)
+        env_sched = os.environ.get("PT_ENV_SCHED", "ilp")  # experiments: "default"
+        if (base == "pt_kernels.hip" and sched == "ilp") or (base == "pt_kernels_env.hip" and env_sched == "ilp"):
+            # iterative-ILP machine scheduling: C3 +1.7%, framed C3 +1.8%; the
+            # ENV kernels (their own translation unit) measured -2.9% with it in
+            # round 2 and +0.8% on C5 with the round-3 follow-up rays
             cmd[1:1] = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
         if src.endswith(".cpp") and "pt_api" not in src:
             cmd.insert(1, "-xc++")  # host-only translation units

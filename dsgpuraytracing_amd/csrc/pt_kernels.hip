@@ -148,17 +148,8 @@ struct Trav {
   float tmax;
   int node, sp;
   int prim;
-  int pl;  // a postponed leaf cursor (0: none), PT_POSTPONE
   bool any, found;
 };
-
-// Speculative traversal (Aila & Laine 2009): when a node step's nearest hit
-// child is a leaf and the next one a node, the lane postpones the leaf (tr.pl)
-// and takes the node step, so it keeps stepping nodes with the wave; the leaf
-// is tested in the wave's next leaf iteration or when the stack runs empty.
-#ifndef PT_POSTPONE
-#define PT_POSTPONE 0
-#endif
 
 __device__ __forceinline__ void trav_init(Trav& tr, float3 o, float3 d, float tmax, bool any) {
   const float kTiny = 1e-20f;
@@ -173,7 +164,6 @@ __device__ __forceinline__ void trav_init(Trav& tr, float3 o, float3 d, float tm
   tr.any = any;
   tr.found = false;
   tr.prim = -1;
-  tr.pl = 0;
 }
 
 // Moller-Trumbore terms of one triangle (u, v, t; det = 0 means parallel).
@@ -282,14 +272,7 @@ struct Stack {
 };
 
 __device__ __forceinline__ bool trav_pop(const Stack& stk, Trav& tr) {
-  if (tr.sp == 0) {
-    if (PT_POSTPONE && tr.pl != 0) {  // the postponed leaf is the last thing left
-      tr.node = tr.pl;
-      tr.pl = 0;
-      return false;
-    }
-    return true;
-  }
+  if (tr.sp == 0) return true;
   --tr.sp;
   tr.node = stk.get(tr.sp);
   return false;
@@ -319,8 +302,6 @@ __device__ __forceinline__ bool node_order(const Stack& stk, Trav& tr, const flo
   cswap(d1, r1, d3, r3);
   cswap(d1, r1, d2, r2);
   if (d0 == kMiss) return trav_pop(stk, tr);
-  // postpone the nearest child when it is a leaf and the next hit child a node
-  const bool pp = PT_POSTPONE && tr.pl == 0 && r0 < 0 && r1 >= 0 && d1 != kMiss;
   // push the farther hits (farthest first), continue with the nearest.  The
   // hits are a sorted prefix, so with room for three entries every candidate
   // is written and the top only advances past hits (no branches).
@@ -331,15 +312,14 @@ __device__ __forceinline__ bool node_order(const Stack& stk, Trav& tr, const flo
     stk.lds[sp * PT_BLOCK] = r2;
     sp += d2 != kMiss;
     stk.lds[sp * PT_BLOCK] = r1;
-    sp += d1 != kMiss && !pp;
+    sp += d1 != kMiss;
   } else {
     if (d3 != kMiss) stk.put(sp++, r3);
     if (d2 != kMiss) stk.put(sp++, r2);
-    if (d1 != kMiss && !pp) stk.put(sp++, r1);
+    if (d1 != kMiss) stk.put(sp++, r1);
   }
   tr.sp = sp;
-  tr.node = pp ? r1 : r0;
-  if (PT_POSTPONE) tr.pl = pp ? r0 : tr.pl;
+  tr.node = r0;
   return false;
 }
 
@@ -455,11 +435,8 @@ __device__ __forceinline__ int leaf_count(int cur) { return ((~cur) & 7) + 1; }
 template <bool STATS>
 __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const Stack& stk, Trav& tr,
                                           Counters& ct) {
-  // the lane's current leaf, or (at a node) its postponed one
-  const bool main = !PT_POSTPONE || tr.node < 0;
-  const int lc = main ? tr.node : tr.pl;
-  const int pa = leaf_first(lc);
-  const int n = leaf_count(lc);
+  const int pa = leaf_first(tr.node);
+  const int n = leaf_count(tr.node);
   const bool two = n >= 2;
   const int pb = two ? pa + 1 : pa;
   float4 a0 = prims[pa].v0, a1 = prims[pa].e1, a2 = prims[pa].e2;
@@ -474,13 +451,7 @@ __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const
   if (prim_test<STATS>(a0, a1, a2, pa, tr, ct)) return true;
   if (two && prim_test<STATS>(b0, b1, b2, pb, tr, ct)) return true;
   if (n > 2) {
-    const int next = ~(((pa + 2) << 3) | (n - 3));
-    if (main) tr.node = next;
-    else tr.pl = next;
-    return false;
-  }
-  if (!main) {
-    tr.pl = 0;
+    tr.node = ~(((pa + 2) << 3) | (n - 3));
     return false;
   }
   return trav_pop(stk, tr);
@@ -816,6 +787,9 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   };
 
   for (;;) {
+    // the shading round issues at raised wave priority, traversal at the
+    // base one (C4 +0.6%, C5 +0.4%, C3 within noise: profiles/r3/ab_build_options.txt)
+    __builtin_amdgcn_s_setprio(2);
     // ================= shading phase: lanes whose ray finished =================
     if (mode == M_SHADE) {
       const bool found = tr.found;
@@ -1213,6 +1187,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       if (__ballot(mode == M_FETCH) == 0ull) break;
     }
     // ================= traversal phase =================
+    __builtin_amdgcn_s_setprio(0);
     // Step every in-flight ray one node at a time; leave as soon as `batch`
     // lanes have finished their ray, so finished lanes are refilled together
     // (coherent shading) while the others keep their traversal state.
@@ -1261,8 +1236,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         l_deep += trav && tr.sp > PT_STACK;
       }
       if (leaf_iter) {
-        // (node lanes holding a postponed leaf test it too)
-        if (at_leaf || (PT_POSTPONE && trav && tr.pl != 0)) done = leaf_step<STATS>(P.prims, stk, tr, ct);
+        if (at_leaf) done = leaf_step<STATS>(P.prims, stk, tr, ct);
         if (STATS) n_leafit += lane == 0;
       } else if (trav && !at_leaf) {
         if constexpr (BIN) done = node_step2<STATS>(P.nodes2, stk, tr, ct);
