@@ -61,6 +61,10 @@ WORKLOADS = {
     "c5": dict(scene="c5", w=1920, h=1080, spp=512,
                desc="C5 CBbunny_sub2_c5 (457,228 tris, glass bunny + mirror sphere; CBlucy proxy) + synthetic "
                     "512x256 environment light, 1920x1080 512spp -m 4 -l 1, tiles over N GPUs"),
+    # C5 at BASELINE.json's "~1M tris" scale (sub3 ~1.83M)
+    "c5big": dict(scene="c5big", w=1920, h=1080, spp=512,
+                  desc="C5 CBbunny_sub3_c5 (1,828,877 tris, glass bunny + mirror sphere; CBlucy proxy at BASELINE's "
+                       "~1M-tri scale) + synthetic 512x256 environment light, 1920x1080 512spp -m 4 -l 1"),
 }
 HEADLINE_METRIC = "Mrays/sec + wall-clock render time, CBdragon 1024x1024 @ 64 spp"
 W, H, SPP, DEPTH, NSL, SEED = 1024, 1024, 64, 4, 1, 1
@@ -79,6 +83,8 @@ def workload_scene(wl):
         dae, envmap = scenes.proxy_path(1), None
     elif wl["scene"] == "c5":
         dae, envmap = scenes.c5_path(2), scenes.c5_envmap_path()
+    elif wl["scene"] == "c5big":
+        dae, envmap = scenes.c5_path(3), scenes.c5_envmap_path()
     else:
         dae, envmap = scenes.C1_DAE, None
     cam = os.path.join(ROOT, "assets", wl["cam"]) if wl.get("cam") else None
@@ -402,6 +408,8 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
 
     def reduce_passes():  # weak: sum the N passes onto rank 0, mean over SPP*N samples
         rows = band[0]
+        if rows.numel() == 0:
+            return
         if backend == "gloo":  # host staging (one-GPU rehearsals)
             h = rows.cpu()
             dist.reduce(h, dst=0)
@@ -451,11 +459,13 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
         # carries only the footprint's rows -- the same image, fewer bytes
         # (C3: 53% of the frame's rows).  Every rank computes the same rows.
         y0, y1 = st_perf["footprint"][1], st_perf["footprint"][3]
+        if y1 < y0:  # the empty footprint (the box is off-screen): every pixel is 0, nothing to reduce
+            y0, y1 = 0, -1
         band[0] = frame[y0:y1 + 1]
         frame[:y0].zero_()
         frame[y1 + 1:].zero_()
     # the ranks must group each pixel's samples alike (bit-identical frame)
-    knobs = check_value_knobs({"group_spp": st_perf["group_spp"]})
+    knobs = check_value_knobs({"group_spp": st_perf["group_spp"], "tail_spp": st_perf["tail_spp"]})
     for _ in range(args.warmup):
         step()
     guard.check()
@@ -537,6 +547,8 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
             "dtype": "fp32",
             "data": {"c5": "synthetic: deterministic CBbunny_sub2 glass/mirror proxy for the missing CBlucy.dae + "
                            "seeded 512x256 environment map (SURVEY §8(d))",
+                     "c5big": "synthetic: deterministic CBbunny_sub3 glass/mirror proxy (BASELINE's ~1M tris) for the "
+                              "missing CBlucy.dae + seeded 512x256 environment map (SURVEY §8(d))",
                      "c1": "CBspheres_lambertian.dae from the reference", "c2": "CBspheres_lambertian.dae from the reference"
                      }.get(workload,
                            "synthetic: deterministic CBbunny_sub1 proxy for the missing CBdragon.dae (SURVEY §8(d))"),
@@ -564,7 +576,7 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
             "launch": {"grid_blocks": s_get(dev, "grid_blocks"), "block": 64,
                        "blocks_per_cu_query": s_get(dev, "blocks_per_cu"),
                        "bvh_nodes": s_get(dev, "bvh_nodes"), "bvh_stack": s_get(dev, "bvh_stack"),
-                       "group_spp": s_get(dev, "group_spp")},
+                       "group_spp": s_get(dev, "group_spp"), "tail_spp": s_get(dev, "tail_spp")},
             "image_mean": float(img.mean()),
         }
         rays = st_counts["camera_rays"] + st_counts["bounce_rays"] + st_counts["shadow_rays"]
@@ -684,6 +696,9 @@ def companions(dev0, local, stream, frames):
         multi-GPU (C4, strong) scaling curve;
       * c5_single_gpu: BASELINE C5 (glass/mirror proxy + environment light)
         on this one GPU;
+      * c5big_single_gpu: C5 at BASELINE's "~1M tris" scale (the sub3 proxy,
+        1.83 M triangles: the one workload whose scene leaves the L2s), with
+        its own PMC roofline (profiles/<round>/c5big_summary.json);
       * c3_host_sah: the headline workload over the host binned-SAH tree
         (PT_BVH_BUILD=sah) instead of the default GPU-built tree;
       * c3_per_tile / c3_per_tile_sync: the headline frame driven through the
@@ -698,8 +713,9 @@ def companions(dev0, local, stream, frames):
 
     from dsgpuraytracing_amd.pathtracer import Device, Scene, tile_fifo
     res = {}
-    names = {"c3f": "c3_framed", "c4": "c4_single_gpu", "c5": "c5_single_gpu", "c3": "c3_host_sah"}
-    for name in ("c3f", "c4", "c5", "c3"):
+    names = {"c3f": "c3_framed", "c4": "c4_single_gpu", "c5": "c5_single_gpu", "c5big": "c5big_single_gpu",
+             "c3": "c3_host_sah"}
+    for name in ("c3f", "c4", "c5", "c5big", "c3"):
         wl = WORKLOADS[name]
         host_sah = name == "c3"
         dae, envmap, cam = workload_scene(wl)
@@ -738,6 +754,18 @@ def companions(dev0, local, stream, frames):
             "frames": frames, "culled_samples": st["culled_samples"],
             "ray_casts_per_s_M": round(rays * frames / el / 1e6, 1), "upload_s": round(t_up, 4),
             "bvh": bvh}
+        if name == "c5big":  # its own roofline: the counts of profiles/<round>/c5big_summary.json
+            dev.render_tiles_device(tl, fr.data_ptr(), stream, stats="ref")
+            st_ref = dev.stats()
+            iso = []
+            for _ in range(2):  # lone, synchronised frames: the kernel's own duration
+                torch.cuda.synchronize()
+                dev.render_tiles_device(tl, fr.data_ptr(), stream)
+                torch.cuda.synchronize()
+                iso.append(dev.launch_times(1)[0][0])
+            res[names[name]]["roofline"] = roofline(name, el / frames * 1e3, algorithmic_bytes(st_ref),
+                                                    isolated_ms=float(np.median(iso)), pipelined_ms=float(np.mean(k)),
+                                                    lib_sha=lib_sha256(), kernel_sha=kernel_sha256())
         dev.close()
         del fr
     res.update(per_tile_companions(local))

@@ -179,6 +179,8 @@ struct pt_ctx {
   std::vector<int4> tiles_host[kSlots];  // what `tiles` holds
   DevBuf<int4> blocks[kSlots];           // footprint-clipped 8x8 pixel blocks of the tiles
   std::vector<int4> blocks_host[kSlots];
+  DevBuf<int> tblock0[kSlots];           // first block of each tile (+ the end), for the resolve
+  std::vector<int> tblock0_host[kSlots];
   DevBuf<float> partial[kSlots];   // per-slot sample-group sums
   DevBuf<int> spill[kSlots];       // traversal stack entries beyond PT_STACK
   DevBuf<uint32_t> counter[kSlots];
@@ -206,6 +208,7 @@ struct pt_ctx {
   };
   std::vector<TileJob> tq;
   int tile_batch = 256;  // tiles per launch (PT_TILE_BATCH): 256 beat 16-128 and 1024 (profiles/r3/seam_native_batch_sweep.txt)
+  int fault_tile_launch = 0, n_tile_launches = 0;  // PT_FAULT_TILE_LAUNCH (tests)
   std::mutex tmu;
   std::condition_variable tcv;
   std::deque<TileBatch*> tpending;  // rendered batches awaiting completion, in launch order
@@ -271,6 +274,7 @@ int pt_create(int device, pt_ctx** out) {
     int v = std::atoi(tb);
     if (v >= 1) c->tile_batch = v;
   }
+  if (const char* f = std::getenv("PT_FAULT_TILE_LAUNCH")) c->fault_tile_launch = std::atoi(f);
   // counters + one trace record per wave of the largest stats grid
   HIPCHK(c->stats.reserve(PT_STATS_SLOTS + (size_t)PT_WAVE_TRACE * std::max(c->grid_stats, 64 * c->n_cu)));
   *out = c;
@@ -299,6 +303,7 @@ int pt_destroy(pt_ctx* c) {
   for (int k = 0; k < pt_ctx::kSlots; ++k) {
     c->tiles[k].release();
     c->blocks[k].release();
+    c->tblock0[k].release();
     c->spill[k].release();
     c->partial[k].release();
     c->counter[k].release();
@@ -887,20 +892,15 @@ static int build_tiles(pt_ctx* c, const pt_tile* tiles, int32_t n, std::vector<i
 // a box entirely in front of the pinhole projects inside the rectangle of its
 // 8 projected corners.  Rays start one unit BEHIND the pinhole, so the
 // rectangle is only used when the box lies in front of the pinhole plane;
-// otherwise culling is disabled.  One pixel of margin absorbs rounding.
-static void screen_footprint(const pt_ctx* c, KParams& P) {
-  P.cull_x0 = 0;
-  P.cull_y0 = 0;
-  P.cull_x1 = P.W - 1;
-  P.cull_y1 = P.H - 1;
-  if (std::getenv("PT_NO_FOOTPRINT_CULL")) return;
-  if (c->env_w > 0) return;  // rays that miss the scene see the environment map
+// otherwise (false) no pixel can be culled.  One pixel of margin absorbs
+// rounding.  r = (x0, y0, x1, y1), inclusive, NOT clamped to the frame.
+static bool footprint_rect(const pt_ctx* c, int W, int H, int r[4]) {
   const pt_camera& cam = c->cam;
   for (int i = 0; i < 3; ++i)  // coordinates by dot products need an orthonormal c2w
     for (int j = 0; j < 3; ++j) {
       double dp = 0;
-      for (int r = 0; r < 3; ++r) dp += cam.c2w[3 * r + i] * cam.c2w[3 * r + j];
-      if (std::fabs(dp - (i == j ? 1.0 : 0.0)) > 1e-9) return;
+      for (int k = 0; k < 3; ++k) dp += cam.c2w[3 * k + i] * cam.c2w[3 * k + j];
+      if (std::fabs(dp - (i == j ? 1.0 : 0.0)) > 1e-9) return false;
     }
   double ax = cam.screen_w / cam.screen_dist, ay = cam.screen_h / cam.screen_dist;
   double x0 = 1e300, x1 = -1e300, y0 = 1e300, y1 = -1e300;
@@ -915,18 +915,96 @@ static void screen_footprint(const pt_ctx* c, KParams& P) {
       cz += v[i] * cam.c2w[3 * i + 2];
     }
     double depth = -cz;  // the view direction is -column 2
-    if (!(depth > 1e-6 * (std::fabs(cx) + std::fabs(cy) + 1.0))) return;  // behind / at the pinhole plane
+    if (!(depth > 1e-6 * (std::fabs(cx) + std::fabs(cy) + 1.0))) return false;  // behind / at the pinhole plane
     double fx = 0.5 + cx / depth / ax, fy = 0.5 + cy / depth / ay;
-    x0 = std::min(x0, fx * P.W);
-    x1 = std::max(x1, fx * P.W);
-    y0 = std::min(y0, fy * P.H);
-    y1 = std::max(y1, fy * P.H);
+    x0 = std::min(x0, fx * W);
+    x1 = std::max(x1, fx * W);
+    y0 = std::min(y0, fy * H);
+    y1 = std::max(y1, fy * H);
   }
   // pixel x covers [x, x+1) in fx*W
-  P.cull_x0 = (int)std::max(-1.0, std::floor(x0) - 1);
-  P.cull_x1 = (int)std::min((double)P.W, std::floor(x1) + 1);
-  P.cull_y0 = (int)std::max(-1.0, std::floor(y0) - 1);
-  P.cull_y1 = (int)std::min((double)P.H, std::floor(y1) + 1);
+  r[0] = (int)std::max(-1.0, std::floor(x0) - 1);
+  r[2] = (int)std::min((double)W, std::floor(x1) + 1);
+  r[1] = (int)std::max(-1.0, std::floor(y0) - 1);
+  r[3] = (int)std::min((double)H, std::floor(y1) + 1);
+  return true;
+}
+
+// Pixels whose camera rays can reach the scene in the default mode: the
+// footprint's area inside the frame, or the whole frame with an environment
+// light (misses see the map) or no footprint.  A property of the frame --
+// PT_NO_FOOTPRINT_CULL leaves it alone -- for the sample-group layout.
+static int64_t traced_px(const pt_ctx* c, int W, int H) {
+  int r[4];
+  if (c->env_w > 0 || !footprint_rect(c, W, H, r)) return (int64_t)W * H;
+  const int64_t w = std::min(W - 1, r[2]) - std::max(0, r[0]) + 1, h = std::min(H - 1, r[3]) - std::max(0, r[1]) + 1;
+  return std::max<int64_t>(0, w) * std::max<int64_t>(0, h);
+}
+
+// The culling rectangle: pixels outside [cull_x0, cull_x1] x [cull_y0,
+// cull_y1] see no geometry (not traced, resolved to 0).
+static void screen_footprint(const pt_ctx* c, KParams& P) {
+  P.cull_x0 = 0;
+  P.cull_y0 = 0;
+  P.cull_x1 = P.W - 1;
+  P.cull_y1 = P.H - 1;
+  if (std::getenv("PT_NO_FOOTPRINT_CULL")) return;
+  if (c->env_w > 0) return;  // rays that miss the scene see the environment map
+  int r[4];
+  if (!footprint_rect(c, P.W, P.H, r)) return;
+  P.cull_x0 = r[0];
+  P.cull_y0 = r[1];
+  P.cull_x1 = r[2];
+  P.cull_y1 = r[3];
+}
+
+// Sample groups of a pixel (KParams: n_big groups of group_spp samples, then
+// tail_spp one-sample groups).  The grouping decides the float summation
+// order of a pixel, so it is a function of the FRAME -- its size, spp, the
+// pixels its camera rays can trace -- and the device's resident grid only,
+// never of the launch's tile set or of a stats build: any split of a frame
+// into tile launches (raytrace_tile calls, the multi-GPU shards) sums every
+// pixel in the same order as the whole frame.
+//  * group_spp: 4 (C3 +3.3% over 2; 8 or more lose), halved for small frames
+//    until there are >= 16 work slots per resident lane (C1, C2: 1);
+//  * the tail: about PT_TAIL_SPL (default 12) samples per resident lane, in
+//    one-sample groups handed out after every big group, so a launch ends on
+//    short work slots instead of waiting for the last lanes' 4-sample groups
+//    (the drain: a lone C3 frame took 1.82 ms vs 1.34 ms pipelined).
+struct GroupLayout {
+  int gs, s_a, n_big, tail;
+};
+static GroupLayout group_layout(int64_t frame_px, int64_t traced, int spp, int64_t lanes, int64_t frame_blocks) {
+  GroupLayout L{PT_GROUP_SPP, 0, 0, 0};
+  while (L.gs > 1 && frame_px * ((spp + L.gs - 1) / L.gs) < lanes * 16) L.gs /= 2;
+  if (const char* g = std::getenv("PT_SAMPLE_GROUP")) {  // tuning knob
+    int v = std::atoi(g);
+    if (v > 0) L.gs = v;
+  }
+  L.gs = std::max(1, std::min(L.gs, spp));
+  int64_t tb = 0;
+  if (L.gs > 1) {
+    int64_t per_lane = 12;
+    if (const char* t = std::getenv("PT_TAIL_SPL")) per_lane = std::max(0, std::atoi(t));  // tuning knob
+    tb = (per_lane * lanes + std::max<int64_t>(traced, 1) - 1) / std::max<int64_t>(traced, 1);
+    tb = std::min<int64_t>((tb + 1) & ~(int64_t)1, spp);  // even: chunks stay inside one block
+  }
+  for (;;) {
+    L.n_big = (int)((spp - tb) / L.gs);
+    if (L.n_big > 1 && (L.n_big & 1)) --L.n_big;  // even: chunks stay inside one block
+    L.s_a = L.n_big * L.gs;
+    L.tail = spp - L.s_a;
+    // 32-bit slot indices (the queue head may overshoot by one chunk per
+    // wave) and a group-sum budget of 4 GiB per render slot, for the whole
+    // frame's blocks (so every tile split gets the same layout)
+    const int64_t slots = frame_blocks * 64 * (L.n_big + L.tail);
+    if ((slots + lanes / 64 * PT_CHUNK_MAX < (int64_t)INT32_MAX && slots * 12 <= (4ll << 30)) ||
+        (L.gs >= spp && tb == 0))
+      break;
+    tb = 0;
+    L.gs = std::min(spp, L.gs * 2);
+  }
+  return L;
 }
 
 // One render: the render kernel on the slot's render stream, then the resolve
@@ -1012,6 +1090,10 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   c->last.footprint[1] = std::max(0, P.cull_y0);
   c->last.footprint[2] = std::min(P.W - 1, P.cull_x1);
   c->last.footprint[3] = std::min(P.H - 1, P.cull_y1);
+  if (c->last.footprint[2] < c->last.footprint[0] || c->last.footprint[3] < c->last.footprint[1]) {
+    c->last.footprint[0] = c->last.footprint[1] = 0;  // nothing visible: the empty rectangle
+    c->last.footprint[2] = c->last.footprint[3] = -1;
+  }
   P.shade_batch = c->env_w > 0 ? PT_SHADE_BATCH_ENV : PT_SHADE_BATCH;
   P.leaf_weight = c->env_w > 0 ? PT_LEAF_WEIGHT_ENV : PT_LEAF_WEIGHT;
   if (const char* lw = std::getenv("PT_LEAF_WEIGHT")) {  // tuning knob
@@ -1031,10 +1113,14 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     int dx = -1, dy = -1;
     if (std::sscanf(dp, "%d,%d", &dx, &dy) == 2 && dx >= 0 && dy >= 0 && dx < P.W && dy < P.H) P.dbg_pix = dx + dy * P.W;
   }
-  // Render blocks: <= 8x8 rectangles of each tile clipped to the footprint.
+  // Render blocks: <= 8x8 rectangles of each tile clipped to the footprint,
+  // tile by tile (tb0[i] = the first block of tile i, for the resolve).
   std::vector<int4> bl;
+  std::vector<int> tb0;
+  tb0.reserve(tl.size() + 1);
   int64_t px_in = 0, px_all = 0;
   for (const int4& t : tl) {
+    tb0.push_back((int)bl.size());
     px_all += (int64_t)t.z * t.w;
     int x0 = std::max(t.x, P.cull_x0), x1 = std::min(t.x + t.z - 1, P.cull_x1);
     int y0 = std::max(t.y, P.cull_y0), y1 = std::min(t.y + t.w - 1, P.cull_y1);
@@ -1044,6 +1130,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
         px_in += (int64_t)bl.back().z * bl.back().w;
       }
   }
+  tb0.push_back((int)bl.size());
   c->culled_px = px_all - px_in;
   std::vector<int4>& bh = c->blocks_host[slot];
   if (!c->blocks[slot].p) HIPCHK(c->blocks[slot].reserve(1));  // never a null block list (a launch may cull every block)
@@ -1055,6 +1142,13 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   }
   P.blocks = c->blocks[slot].p;
   P.n_blocks = (int)bl.size();
+  std::vector<int>& th0 = c->tblock0_host[slot];
+  if (tb0 != th0) {
+    th0 = tb0;
+    HIPCHK(c->tblock0[slot].reserve(tb0.size()));
+    HIPCHK(hipMemcpyAsync(c->tblock0[slot].p, th0.data(), th0.size() * sizeof(int), hipMemcpyHostToDevice, rs));
+  }
+  P.tile_block0 = c->tblock0[slot].p;
   // Work slots are (pixel, group of group_spp samples): small enough that
   // the dynamic queue balances the waves (a whole pixel per slot left the
   // launch waiting on a few waves holding 64-sample pixels).
@@ -1067,49 +1161,31 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     int w = std::atoi(g);
     if (w > 0) want = (int64_t)w * c->n_cu;
   }
-  P.group_spp = PT_GROUP_SPP;
-  // Smaller FRAMES get smaller groups (down to one sample): at least ~16 work
-  // slots per lane keep the tail short.  The grouping decides the float summation order of a
-  // pixel, so it is a function of the frame (W, H, spp) and the device's
-  // resident grid only -- never of the launch's tile set or of a stats build:
-  // any split of a frame into tile launches (raytrace_tile calls, the
-  // multi-GPU shards) sums every pixel in the same order as the whole frame.
   const int64_t frame_px = (int64_t)P.W * P.H;
   const int64_t want_plain = std::getenv("PT_WAVES_PER_CU") ? want : c->grid_plain;
-  while (P.group_spp > 1 && frame_px * ((P.spp + P.group_spp - 1) / P.group_spp) < want_plain * PT_BLOCK * 16)
-    P.group_spp /= 2;
-  if (const char* g = std::getenv("PT_SAMPLE_GROUP")) {  // tuning knob
-    int v = std::atoi(g);
-    if (v > 0) P.group_spp = v;
-  }
-  P.group_spp = std::min(P.group_spp, P.spp);
-  const int64_t npx = (int64_t)P.W * P.H;
-  // 32-bit slot and partial indices (the queue head may overshoot by one
-  // chunk per wave); the per-pixel group sums of one render slot stay within
-  // 4 GiB.  The fallback that doubles the group also looks at the FRAME only
-  // (its 8x8 blocks as the whole-frame tile FIFO cuts them), so a tile split
-  // groups each pixel's samples exactly as the whole frame does.
   const int64_t frame_blocks = (int64_t)((P.W + 7) / 8) * ((P.H + 7) / 8);
-  for (;;) {
-    P.n_groups = (P.spp + P.group_spp - 1) / P.group_spp;
-    const bool fits = frame_blocks * 64 * P.n_groups + want_plain * PT_CHUNK_MAX < (int64_t)UINT32_MAX &&
-                      npx * P.n_groups * 12 <= (4ll << 30);
-    if (fits || P.n_groups == 1) break;
-    P.group_spp *= 2;
-  }
-  const int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
-  if (slots + want * PT_CHUNK_MAX >= (int64_t)UINT32_MAX || npx * P.n_groups >= (int64_t)UINT32_MAX)
-    return fail(PT_E_INVALID, "frame too large for one launch");
-  HIPCHK(c->partial[slot].reserve((size_t)(npx * P.n_groups) * 3));
+  const GroupLayout L = group_layout(frame_px, traced_px(c, P.W, P.H), P.spp, want_plain * PT_BLOCK, frame_blocks);
+  P.group_spp = L.gs;
+  P.s_a = L.s_a;
+  P.n_big = L.n_big;
+  P.tail_spp = L.tail;
+  const int64_t slots = (int64_t)bl.size() * 64 * (L.n_big + L.tail);
+  if (slots + want * PT_CHUNK_MAX >= (int64_t)INT32_MAX) return fail(PT_E_INVALID, "frame too large for one launch");
+  P.slots_a = (uint32_t)((int64_t)bl.size() * 64 * L.n_big);
+  pt_fastdiv_init((uint32_t)std::max(1, L.n_big), &P.big_m, &P.big_sh);
+  pt_fastdiv_init((uint32_t)std::max(1, L.tail), &P.tail_m, &P.tail_sh);
+  P.sblocks = (L.n_big % 2 == 0 && L.tail % 2 == 0) ? 1 : 0;
+  // group sums: 12 B per work slot of THIS launch (a rank's share of a split
+  // frame holds only its own blocks' sums)
+  HIPCHK(c->partial[slot].reserve((size_t)std::max<int64_t>(slots, 1) * 3));
   P.partial = c->partial[slot].p;
-  c->last.partial_bytes = (int64_t)npx * P.n_groups * 12;
+  c->last.partial_bytes = slots * 12;
   auto log2_exact = [](int v) {  // log2(v) for a power of two, else -1
     int k = 0;
     while ((1 << k) < v && k < 30) ++k;
     return (1 << k) == v ? k : -1;
   };
   P.group_shift = log2_exact(P.group_spp);
-  P.ngroup_shift = log2_exact(P.n_groups);
   int64_t max_grid = std::max<int64_t>(1, (slots + PT_BLOCK - 1) / PT_BLOCK);
   int grid = (int)std::min<int64_t>(want, max_grid);
   if (stats && (size_t)grid * PT_WAVE_TRACE + PT_STATS_SLOTS > c->stats.n) grid = (int)((c->stats.n - PT_STATS_SLOTS) / PT_WAVE_TRACE);
@@ -1135,6 +1211,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   HIPCHK(hipEventRecord(c->ev_free[slot], s));
   c->last.grid_blocks = grid;
   c->last.group_spp = P.group_spp;
+  c->last.tail_spp = P.tail_spp;
   c->last.blocks_per_cu = (int32_t)(want / std::max(1, c->n_cu));
   int64_t px = 0;
   for (const int4& t : tl) px += (int64_t)t.z * t.w;
@@ -1331,12 +1408,38 @@ static void tile_worker_stop(pt_ctx* c) {
   c->tfree.clear();
 }
 
+// A batch that could not be launched: its tiles are dropped, so the failure is
+// also kept for the next pt_tile_finish (which would otherwise report PT_OK for
+// tiles it never rendered), whoever called tile_launch.
+static int tile_launch_failed(pt_ctx* c, int rc) {
+  std::lock_guard<std::mutex> lk(c->tmu);
+  if (c->terr == PT_OK) {
+    c->terr = rc;
+    c->terrmsg = std::string("tile launch: ") + pt_last_error();
+  }
+  return rc;
+}
+
+// Fault injection for the seam's error path (tests): PT_FAULT_TILE_LAUNCH=k
+// at pt_create makes the context's k-th batch launch fail before it renders.
+static bool tile_fault_injected(pt_ctx* c) {
+  return c->fault_tile_launch > 0 && ++c->n_tile_launches == c->fault_tile_launch;
+}
+
+static int tile_launch_impl(pt_ctx* c);
+
 // Renders the queued tiles as one launch (nothing queued: nothing to do).
 static int tile_launch(pt_ctx* c) {
   if (!c || c->tq.empty()) return PT_OK;
+  const int rc = tile_launch_impl(c);
+  return rc ? tile_launch_failed(c, rc) : PT_OK;
+}
+
+static int tile_launch_impl(pt_ctx* c) {
   constexpr int kMaxBatchesInFlight = 8;  // bounds the pinned staging memory
   std::vector<pt_ctx::TileJob> jobs;
   jobs.swap(c->tq);
+  if (tile_fault_injected(c)) return fail(PT_E_HIP, "pt_tile_submit: injected launch failure (PT_FAULT_TILE_LAUNCH)");
   HIPCHK(hipSetDevice(c->device));
   const size_t W = (size_t)c->params.width, H = (size_t)c->params.height;
   std::vector<int4> tl;
@@ -1423,7 +1526,10 @@ int pt_tile_submit(pt_ctx* c, const pt_tile* tile, float* hdr_out_host, uint32_t
 
 int pt_tile_finish(pt_ctx* c) {
   if (!c) return fail(PT_E_INVALID, "NULL context");
-  if (int rc = tile_launch(c)) return rc;
+  // Whatever happens to the last launch, every batch already in flight is
+  // waited for: the completion thread writes into the caller's buffers, which
+  // the caller may free or reuse as soon as this returns.
+  (void)tile_launch(c);  // (a failure is recorded in terr)
   int err = PT_OK;
   std::string msg;
   {

@@ -119,10 +119,25 @@ struct KParams {
   int n_lights;
   int n_bsdfs;
   int n_tiles;     // 32x32 (or smaller) tiles: 1024 pixels each
-  int group_spp;   // samples per work slot (a slot is one pixel's sample group)
-  int n_groups;    // ceil(spp / group_spp): slots per pixel
+  // Sample groups (work slots) of a pixel, a function of the frame only
+  // (launch(): pt_api.cpp group_layout): samples [0, s_a) in n_big groups of
+  // group_spp, then tail_spp one-sample groups [s_a, spp).  The queue hands
+  // out every pixel's big groups first (phase A) and the one-sample groups
+  // last (phase B), so the launch ends on short work slots.
+  int group_spp;   // samples per phase-A slot
   int group_shift;   // log2(group_spp) when a power of two, else -1 (shifts instead of divisions)
-  int ngroup_shift;  // log2(n_groups) when a power of two, else -1
+  int s_a;         // samples in phase-A groups (n_big * group_spp)
+  int n_big;       // phase-A groups per pixel
+  int tail_spp;    // phase-B (one-sample) groups per pixel
+  // Work slot / group-sum index: phase A (block b, group j, pixel q of the
+  // 8x8 block) -> (b * n_big + j) * 64 + q; phase B (tail sample t) ->
+  // slots_a + (b * tail_spp + t) * 64 + q.  A unit is 64 slots (one group of
+  // one block); unit -> block by fastdiv (pt_fastdiv).
+  uint32_t slots_a;                 // phase-A slots: n_blocks * 64 * n_big
+  uint32_t big_m, big_sh;           // fastdiv by n_big
+  uint32_t tail_m, tail_sh;         // fastdiv by tail_spp
+  int sblocks;                      // a 128-slot chunk lies in one block (n_big, tail_spp even): scalar block loads
+  const int* tile_block0;           // first block of each tile (n_tiles + 1 entries), for the resolve
   const DNode* nodes;
   const DNode2* nodes2;  // the binary tree (reference-count launch only)
   const DPrim* prims;
@@ -139,7 +154,7 @@ struct KParams {
   const int4* tiles;  // (x, y, w, h)
   float* out;         // W*H*3, or n_tiles*1024*3 when packed
   int packed;         // PT_FLAG_PACKED: tile i's pixel (x, y) -> out[3 * (i*1024 + (y-ty)*32 + (x-tx))]
-  float* partial;     // W*H*n_groups*3: each sample group's sum, resolved into `out` in group order
+  float* partial;     // 3 floats per work slot: each sample group's sum, resolved into `out` in group order
   const int4* blocks;  // (x, y, w<=8, h<=8): footprint-clipped pixel blocks of the tiles
   int n_blocks;
   uint32_t* work_counter;
@@ -152,6 +167,27 @@ struct KParams {
   float root_lo[3], root_hi[3];  // scene bounds (root box, rounded outward)
   int cull_x0, cull_y0, cull_x1, cull_y1;  // pixels outside [x0,x1]x[y0,y1] see no geometry
 };
+
+// q = u / d for u < 2^31 and a runtime divisor d >= 1, without a division:
+// q = m ? mulhi(u, m) >> sh : u >> sh (Granlund & Montgomery 1994).  For d
+// a power of two m = 0; otherwise with 2^(l-1) < d < 2^l, m = ceil(2^(31+l) / d)
+// < 2^32 and sh = l - 1: u*m / 2^(31+l) = u/d + u*e / (d * 2^(31+l)) with
+// e = m*d - 2^(31+l) < d, and the error term stays below 1/d for u < 2^31, so
+// the floor is exact (tests/test_abi.py checks it exhaustively for small d).
+inline void pt_fastdiv_init(uint32_t d, uint32_t* m, uint32_t* sh) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  if ((1ull << l) == d) {
+    *m = 0;
+    *sh = l;
+  } else {
+    *m = (uint32_t)((((uint64_t)1 << (31 + l)) + d - 1) / d);
+    *sh = l - 1;
+  }
+}
+__device__ __forceinline__ uint32_t pt_fastdiv(uint32_t u, uint32_t m, uint32_t sh) {
+  return m ? __umulhi(u, m) >> sh : u >> sh;
+}
 
 // GPU BVH build (lbvh.hip).  Inputs in upload order; outputs hipMalloc'd by
 // the builder (the caller owns and frees them).

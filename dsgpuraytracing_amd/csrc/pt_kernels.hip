@@ -586,25 +586,12 @@ __device__ __forceinline__ void env_sample(const KP& P, float r1, float r2, floa
 // Lane modes of the persistent kernel.
 enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 // What follows a lane's shadow ray (the `shadow` state; 0 = not a shadow ray).
-enum : int { SH_RESUME = 1, SH_FOLLOW = 2, SH_GROUP_END = 3, SH_STORE = 4, SH_STORE_FOLLOW = 5 };
+enum : int { SH_RESUME = 1, SH_FOLLOW = 2, SH_STORE = 3, SH_STORE_FOLLOW = 4 };
 // Launch parameters re-read per round (see render_kernel): on for the
 // environment-light build (C5 +6.8%, no VGPR spills instead of 8), off for the
 // common one (C3 -1.1%, C4 +0.6%: profiles/r3/ab_kernarg_round.txt).
 #ifndef PT_KARG_ROUND
 #define PT_KARG_ROUND PT_ENV_TU
-#endif
-#ifndef PT_FOLLOW
-#define PT_FOLLOW 1
-#endif
-#ifndef PT_EARLY_STORE
-#if PT_ENV_TU
-#ifndef PT_EARLY_STORE_ENV
-#define PT_EARLY_STORE_ENV 1
-#endif
-#define PT_EARLY_STORE PT_EARLY_STORE_ENV
-#else
-#define PT_EARLY_STORE 1
-#endif
 #endif
 
 // Wave-clock sections of the STATS build: every shader clock of a wave's
@@ -694,17 +681,21 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // the ray in flight: 0 extension (camera / bounce) ray, else a shadow ray
   // followed by -- SH_RESUME: the shading round (NEE resumes at the cursor);
   // SH_FOLLOW: the next extension ray, already sampled (origin in hp,
-  // direction in ns), started inside the traversal loop; SH_GROUP_END: the
-  // shading round that stores the finished group and refills; SH_STORE: the
-  // group already ended -- its total without the light sample is stored, the
-  // total with it waits in pend and is stored over it (at oslot) if the
-  // shadow ray is clear, then the lane retires (the queue is drained) or, with
-  // SH_STORE_FOLLOW, goes on with the next group's camera ray in (hp, ns)
+  // direction in ns), started inside the traversal loop; SH_STORE: the
+  // group already ended and the lane was refilled -- acc keeps the group's
+  // total without the light sample, pend the total with it, and ONE store at
+  // oslot writes the right one when the shadow ray ends; then the lane
+  // retires (the queue is drained) or, with SH_STORE_FOLLOW, goes on with the
+  // next group's camera ray parked in (hp, ns).  While a store is pending the
+  // new group's sum is 0: nothing reaches it before its parked ray starts
+  // (camera rays that miss are parked too when they would see the
+  // environment map).
   int shadow = 0;
   uint32_t oslot = 0;
-  // the work slot (pixel, sample group) this lane renders: its pixel as packed
-  // coordinates (x | y << 16; W, H <= 65535) and its current sample; the
-  // group is sample / group_spp
+  // the work slot (pixel, sample group) this lane renders: its index (where
+  // the group's sum goes), its pixel as packed coordinates (x | y << 16;
+  // W, H <= 65535) and its current sample
+  uint32_t myslot = 0;
   int pix = 0, sample = 0;
   // the sample's stream and the counter word of its next draw (ptrng::draw_at)
   uint32_t rbase = 0, rdim = ptrng::kDrawInit;
@@ -746,24 +737,16 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     slot_lat_max = d_ > slot_lat_max ? d_ : slot_lat_max;        \
   }
 
-  const uint32_t n_groups = (uint32_t)P.n_groups;
-  // group arithmetic by shifts when the sizes are powers of two (the usual
-  // case; wave-uniform branches), the exact divisions otherwise
-  auto group_of = [&](int s) -> int { return P.group_shift >= 0 ? s >> P.group_shift : s / P.group_spp; };
-  auto group_starts = [&](int s) -> bool {
-    return P.group_shift >= 0 ? (s & (P.group_spp - 1)) == 0 : s % P.group_spp == 0;
-  };
-  auto pixel_of_slot = [&](uint32_t slot) -> uint32_t {
-    return P.ngroup_shift >= 0 ? slot >> P.ngroup_shift : slot / n_groups;
+  // the lane's group ends before sample s: the last phase-A group ends at
+  // s_a, every phase-B group after one sample (a shift when group_spp is a
+  // power of two, the usual case; wave-uniform branch)
+  auto group_ends = [&](int s) -> bool {
+    return s >= P.s_a || (P.group_shift >= 0 ? (s & (P.group_spp - 1)) == 0 : s % P.group_spp == 0);
   };
   // the pixel index from the packed coordinates: one multiply-add, no
   // division per camera ray
   auto pix_index = [&](int p) -> int { return (p & 0xffff) + (int)((uint32_t)p >> 16) * P.W; };
-  // partial-sum slot of a finished group: (pixel, group of the last sample)
-  auto slot_of = [&](int p, int s_next) -> size_t {
-    return (size_t)pix_index(p) * n_groups + (uint32_t)group_of(s_next - 1);
-  };
-  const uint32_t total_slots = (uint32_t)P.n_blocks * 64u * n_groups;
+  const uint32_t total_slots = P.slots_a + (uint32_t)P.n_blocks * 64u * (uint32_t)P.tail_spp;
   const int batch = P.shade_batch;
   // Camera::generate_ray (camera.cpp:113-129) for the lane's pixel and
   // current sample, at the jittered position of raytrace_pixel
@@ -791,12 +774,13 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // light sample (or store the group's total with it) and go on with the
   // next extension ray -- or retire -- without a shading round.
   auto follow_on = [&](bool done) {
-    if (PT_FOLLOW && __ballot(done && shadow >= SH_FOLLOW && shadow != SH_GROUP_END) != 0ull) {
-      if (done && shadow >= SH_FOLLOW && shadow != SH_GROUP_END) {
+    if (__ballot(done && shadow >= SH_FOLLOW) != 0ull) {
+      if (done && shadow >= SH_FOLLOW) {
         if (shadow == SH_FOLLOW) {
           if (!tr.found) acc = acc + pend;
-        } else if (!tr.found) {
-          store3(P.partial + 3 * (size_t)oslot, pend);  // the group's total with the light sample
+        } else {  // the finished group's one store: its total with the light sample if the shadow ray is clear
+          store3(P.partial + 3 * (size_t)oslot, tr.found ? acc : pend);
+          acc = f3(0, 0, 0);  // the new group's sum starts here
         }
         if (shadow == SH_STORE) {
           mode = M_DONE;
@@ -820,14 +804,13 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     if (mode == M_SHADE) {
       const bool found = tr.found;
       bool finish = false;  // the sample is complete
-      bool group_end = false;  // the group's last sample ended with the shadow ray just finished
+      bool group_end = false;  // the group's last sample ended: store its sum
       bool after = false;      // the sample's last shadow ray is emitted: the bounce / camera ray follows it
       int stage;            // 0: NEE (+ bounce), 2: none
-      if (shadow) {
+      if (shadow) {  // (SH_RESUME: the follow-ups end inside the traversal loop)
         if (!found) acc = acc + pend;  // unoccluded (the light sample was already counted)
         if (DBG && pix_index(pix) == P.dbg_pix) printf("    shadow %s (pend %.6g) prim %d t %.9g\n", found ? "occluded" : "clear", pend.x, tr.prim, tr.tmax);
-        group_end = PT_FOLLOW && shadow == SH_GROUP_END;
-        stage = group_end ? 2 : 0;
+        stage = 0;
         shadow = 0;
       } else if (!found) {
         // miss: the environment map if there is one and includeLe (pathtracer.cpp:411-427)
@@ -946,7 +929,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           break;
         }
         // the shadow ray just emitted is the vertex's last light sample
-        const bool emit_last = PT_FOLLOW && emitted && li + 1 >= P.n_lights &&
+        const bool emit_last = emitted && li + 1 >= P.n_lights &&
                                ls >= ((__float_as_int(light_f(li, 0)) | 2) == 2 ? 1 : P.ns_area);
         cur = (cur & 0xffu) | ((uint32_t)ls << 8) | ((uint32_t)li << 16);
         PT_STAMP(S_NEE);
@@ -1044,28 +1027,22 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       }
       if (finish) {
         ++sample;
-        if (sample < P.spp && !group_starts(sample)) {
+        if (!group_ends(sample)) {
           mode = M_CAMERA;  // after a shadow ray: the camera ray goes to (hp, ns), behind it
           if (after) shadow = SH_FOLLOW;
-        } else if (after) {
-          if (PT_EARLY_STORE) {  // store now, refill in this round (the shadow ray waits)
-            PT_FENCE3(pend);  // (no contraction into pend's last multiply: the sum rounds as at the shadow ray's return)
-            pend = acc + pend;
-            oslot = (uint32_t)slot_of(pix, sample);
-            store3(P.partial + 3 * (size_t)oslot, acc);
-            PT_SLOT_DONE();
-            shadow = SH_STORE;
-            mode = M_FETCH;
-          } else {
-            shadow = SH_GROUP_END;
-            mode = M_TRAV;
-          }
+        } else if (after) {  // refill in this round; the one store waits for the shadow ray
+          PT_FENCE3(pend);  // (no contraction into pend's last multiply: the sum rounds as at the shadow ray's return)
+          pend = acc + pend;
+          oslot = myslot;
+          PT_SLOT_DONE();
+          shadow = SH_STORE;
+          mode = M_FETCH;
         } else {
           group_end = true;
         }
       }
       if (group_end) {
-        store3(P.partial + 3 * slot_of(pix, sample), acc);
+        store3(P.partial + 3 * (size_t)myslot, acc);
         PT_SLOT_DONE();
         mode = M_FETCH;
       }
@@ -1107,26 +1084,36 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             if (STATS) n_atomics += lane == 0;
           }
         }
-        // A chunk of 128 slots (128-aligned) lies inside one 8x8 block when a
-        // block holds a multiple of 128 slots (n_groups a power of two >= 2),
-        // and the lanes are served from at most two chunks -- the rest of the
-        // old one and the new one: both block records are read through the
-        // scalar cache (wave-uniform addresses) instead of one vector-memory
-        // load per lane, which every refill round would wait on (C5 +1%,
-        // framed C3 +0.3%, C3 neutral: profiles/r3/ab_scalar_blocks.txt).
-        const bool sblocks = P.ngroup_shift >= 1 && total_slots > 0u;  // (no blocks: nothing to read)
+        // Work slots -> (block, group, pixel): see KParams.  A unit of 64
+        // slots is one group of one 8x8 block, its slots the block's pixels
+        // (neighbouring lanes get neighbouring pixels: coherent rays); a
+        // unit's block is a fastdiv of its index.
+        auto block_of = [&](uint32_t slot) -> uint32_t {
+          const bool tl = slot >= P.slots_a;
+          const uint32_t u = (slot - (tl ? P.slots_a : 0u)) >> 6;
+          return tl ? pt_fastdiv(u, P.tail_m, P.tail_sh) : pt_fastdiv(u, P.big_m, P.big_sh);
+        };
+        // A chunk of 128 slots (128-aligned) lies inside one block when both
+        // phases hold an even number of groups per pixel, and the lanes are
+        // served from at most two chunks -- the rest of the old one and the
+        // new one: both block records are read through the scalar cache
+        // (wave-uniform addresses) instead of one vector-memory load per lane,
+        // which every refill round would wait on (C5 +1%, framed C3 +0.3%,
+        // C3 neutral: profiles/r3/ab_scalar_blocks.txt).
+        const bool sblocks = P.sblocks && total_slots > 0u;  // (no blocks: nothing to read)
         int4 b_old = make_int4(0, 0, 0, 0), b_new = make_int4(0, 0, 0, 0);
+        uint32_t k_old = 0, k_new = 0;
         if (sblocks) {
           typedef __attribute__((address_space(4))) const pt_v4i cst_v4i;
           const cst_v4i* cb = (const cst_v4i*)P.blocks;
-          const uint32_t sh = (uint32_t)P.ngroup_shift + 6u;  // slot -> block index
-          const uint32_t last = total_slots > 0u ? (total_slots - 1u) >> sh : 0u;
           if (avail > 0u) {
-            const pt_v4i v = cb[min(chunk_next >> sh, last)];
+            k_old = block_of(min(chunk_next, total_slots - 1u));
+            const pt_v4i v = cb[k_old];
             b_old = make_int4(v.x, v.y, v.z, v.w);
           }
           if (cnt > avail) {
-            const pt_v4i v = cb[min(nbase >> sh, last)];
+            k_new = block_of(min(nbase, total_slots - 1u));
+            const pt_v4i v = cb[k_new];
             b_new = make_int4(v.x, v.y, v.z, v.w);
           }
         }
@@ -1134,24 +1121,29 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
           uint32_t slot = rank < avail ? chunk_next + rank : nbase + (rank - avail);
           if (slot >= total_slots) {
-            mode = (PT_EARLY_STORE && shadow) ? M_TRAV : M_DONE;  // (a pending shadow ray is traced first)
+            mode = shadow ? M_TRAV : M_DONE;  // (a pending shadow ray is traced first)
             if (STATS && w_empty == 0ull) w_empty = wall_clock64();
           } else {
-            // slot = (block * 64 + pixel-in-block) * n_groups + group: the
-            // groups of one pixel sit on neighbouring lanes (coherent rays).
             // Blocks are <= 8x8 pixel rectangles of the tiles, clipped to the
             // scene's screen footprint (pixels outside are written 0 by
             // resolve_kernel: every ray through them misses the root box).
-            uint32_t bq = pixel_of_slot(slot);
-            uint32_t g = slot - bq * n_groups;
-            int4 b;  // (other groupings: one vector-memory load per lane)
-            if (sblocks) b = rank < avail ? b_old : b_new;
-            else b = P.blocks[bq >> 6];
-            int qx = (int)(bq & 7u), qy = (int)((bq >> 3) & 7u);
+            const bool tl = slot >= P.slots_a;
+            uint32_t k;
+            int4 b;  // (odd group counts: one vector-memory load per lane)
+            if (sblocks) {
+              k = rank < avail ? k_old : k_new;
+              b = rank < avail ? b_old : b_new;
+            } else {
+              k = block_of(slot);
+              b = P.blocks[k];
+            }
+            const uint32_t j = ((slot - (tl ? P.slots_a : 0u)) >> 6) - k * (uint32_t)(tl ? P.tail_spp : P.n_big);
+            const int qx = (int)(slot & 7u), qy = (int)((slot >> 3) & 7u);
             if (qx < b.z && qy < b.w) {
               pix = (b.x + qx) | ((b.y + qy) << 16);
-              sample = (int)g * P.group_spp;
-              acc = f3(0, 0, 0);
+              sample = tl ? P.s_a + (int)j : (int)j * P.group_spp;
+              myslot = slot;
+              if (!shadow) acc = f3(0, 0, 0);  // (SH_STORE: acc holds the last group's total until its store)
               if (STATS) slot_t0 = wall_clock64();
               mode = M_CAMERA;
             }
@@ -1175,7 +1167,10 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         Trav cr;
         const bool in = camera_ray(cr);
         if (!shadow) tr = cr;
-        if (in) {
+        // Behind a pending shadow ray, a camera ray that would see the
+        // environment map is parked too: its radiance is then added after the
+        // light sample, in the order of trace_ray.
+        if (in || (ENV && shadow)) {
           T = f3(1, 1, 1);
           cur = 0;  // depth 0
           includeLe = true;
@@ -1188,25 +1183,19 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           break;
         }
         // miss: the sample sees the environment (includeLe) or nothing
-        if (ENV) acc = acc + env_dir(P, cr.d);
+        if (ENV) acc = acc + env_dir(P, cr.d);  // (no shadow ray pending: see above)
         ++sample;
-        if (sample >= P.spp || group_starts(sample)) {
-          if (shadow == SH_FOLLOW && PT_EARLY_STORE) {  // the pending light sample belongs to this group
+        if (group_ends(sample)) {
+          if (shadow == SH_FOLLOW) {  // the pending light sample belongs to this group: one store, deferred
             PT_FENCE3(pend);  // (no contraction into pend's last multiply: the sum rounds as at the shadow ray's return)
             pend = acc + pend;
-            oslot = (uint32_t)slot_of(pix, sample);
-            store3(P.partial + 3 * (size_t)oslot, acc);
-            PT_SLOT_DONE();
+            oslot = myslot;
             shadow = SH_STORE;
-            mode = M_FETCH;
-          } else if (shadow == SH_FOLLOW) {
-            shadow = SH_GROUP_END;
-            mode = M_TRAV;
-          } else {  // (no pending light sample, or one of an earlier group)
-            store3(P.partial + 3 * slot_of(pix, sample), acc);
-            PT_SLOT_DONE();
-            mode = M_FETCH;
+          } else {  // SH_STORE: acc is the previous group's; this one saw nothing
+            store3(P.partial + 3 * (size_t)myslot, shadow ? f3(0, 0, 0) : acc);
           }
+          PT_SLOT_DONE();
+          mode = M_FETCH;
         }
       }
       PT_STAMP(S_CAMERA);
@@ -1357,63 +1346,41 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
 #undef P
 #endif
 
-// Lanes that resolve one pixel: the pixel's groups are read as one coalesced
-// run (the per-pixel partials are n_groups * 12 B contiguous).
-__host__ __device__ __forceinline__ int resolve_team(int n_groups) {
-  int k = 1;
-  while (k < n_groups && k < 64) k <<= 1;
-  return k;
-}
-
 #if !PT_ENV_TU  // (pt_kernels_env.hip emits only the ENV render kernels)
-// Sums each pixel's sample groups in a fixed order (so the sum is a fixed
-// function of the pixel, independent of scheduling and of the tile -> GPU
-// assignment) and writes the pixel's average, SampleBuffer-style
-// (pathtracer.cpp:577-581).  A team of k lanes (power of two) per pixel: lane
-// j sums groups j, j+k, j+2k, ... in order, then the team adds its k partial
-// sums by a fixed butterfly.  One lane per pixel read 12-B words n_groups * 12
-// B apart (C5: 3 KB stride, 1.4 TB/s); the team reads contiguous runs.
-// One workgroup per tile: a tile outside the scene's screen footprint is
-// written 0 row by row (no team, no partial-sum reads); otherwise the 256
-// lanes sweep the tile's rows 256/k pixels at a time (consecutive pixels'
-// group sums are contiguous).  One wave per 16 pixels measured 0.27 ms on C3
-// and 2.2 ms on C4/C5, mostly workgroup dispatch for the culled three
-// quarters of the frame.
+// Sums each pixel's sample groups in group order (phase-A groups, then the
+// phase-B one-sample groups), so the sum is a fixed function of the pixel,
+// independent of scheduling and of the tile -> GPU assignment, and writes the
+// pixel's average, SampleBuffer-style (pathtracer.cpp:577-581).  One
+// workgroup per tile: the tile's pixels outside the scene's screen footprint
+// are written 0; then its blocks, four at a time, one lane per pixel: the 64
+// lanes of a block read each group's 64 sums as one contiguous 768-B run.
 __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
   const int ti = (int)blockIdx.x;
   const int4 tile = P.tiles[ti];
   const int tid = (int)threadIdx.x;
-  const bool outside = tile.x > P.cull_x1 || tile.x + tile.z - 1 < P.cull_x0 || tile.y > P.cull_y1 ||
-                       tile.y + tile.w - 1 < P.cull_y0;
-  if (outside) {
-    const int rowf = tile.z * 3;  // floats per tile row
-    for (int i = tid; i < rowf * tile.w; i += 256) {
-      const int r = i / rowf, c = i - r * rowf;
-      const size_t o = P.packed ? ((size_t)ti * 1024u + (size_t)r * 32u) * 3u + (size_t)c
-                                : ((size_t)(tile.y + r) * (size_t)P.W + (size_t)tile.x) * 3u + (size_t)c;
-      P.out[o] = 0.0f;
-    }
-    return;
+  auto out_at = [&](int x, int y) -> float* {
+    const size_t o = P.packed ? (size_t)ti * 1024u + (size_t)(y - tile.y) * 32u + (size_t)(x - tile.x)
+                              : (size_t)x + (size_t)y * (size_t)P.W;
+    return P.out + 3 * o;
+  };
+  for (int i = tid; i < 1024; i += 256) {
+    const int x = tile.x + (i & 31), y = tile.y + (i >> 5);
+    if ((i & 31) < tile.z && (i >> 5) < tile.w && culled(P, x, y)) store3(out_at(x, y), f3(0, 0, 0));
   }
-  const int k = resolve_team(P.n_groups);
-  const int per = 256 / k;  // pixels per sweep step
-  const int j = tid & (k - 1);
   const float inv_spp = (float)(1.0 / (double)P.spp);
-  for (int base = 0; base < 1024; base += per) {  // uniform trip count: every lane reaches the shuffles
-    const int q = base + tid / k;                 // pixel of the tile, row-major 32 x 32
-    const int x = tile.x + (q & 31), y = tile.y + (q >> 5);
-    const bool in_tile = (q & 31) < tile.z && (q >> 5) < tile.w;
+  const int q = tid & 63, qx = q & 7, qy = q >> 3;
+  const int b1 = P.tile_block0[ti + 1];
+  for (int k = P.tile_block0[ti] + (tid >> 6); k < b1; k += 4) {
+    const int4 b = P.blocks[k];
+    if (qx >= b.z || qy >= b.w) continue;
     float3 acc = f3(0, 0, 0);
-    if (in_tile && !culled(P, x, y)) {
-      const float* p = P.partial + 3 * ((size_t)x + (size_t)y * (size_t)P.W) * (size_t)P.n_groups;
-      for (int g = j; g < P.n_groups; g += k) acc = acc + ld3(p + 3 * g);
-    }
-    for (int off = 1; off < k; off <<= 1)
-      acc = acc + f3(__shfl_xor(acc.x, off), __shfl_xor(acc.y, off), __shfl_xor(acc.z, off));
-    if (in_tile && j == 0) {
-      const size_t o = P.packed ? (size_t)ti * 1024u + (size_t)q : (size_t)x + (size_t)y * (size_t)P.W;
-      store3(P.out + 3 * o, acc * inv_spp);
-    }
+    const float* pa = P.partial + 3 * ((size_t)k * (size_t)P.n_big * 64u + (size_t)q);
+#pragma unroll 4
+    for (int j = 0; j < P.n_big; ++j) acc = acc + ld3(pa + 192 * (size_t)j);
+    const float* pb = P.partial + 3 * ((size_t)P.slots_a + (size_t)k * (size_t)P.tail_spp * 64u + (size_t)q);
+#pragma unroll 4
+    for (int t = 0; t < P.tail_spp; ++t) acc = acc + ld3(pb + 192 * (size_t)t);
+    store3(out_at(b.x + qx, b.y + qy), acc * inv_spp);
   }
 }
 

@@ -78,6 +78,7 @@ class Device:
         p = native.pt_params(width=width, height=height, spp=spp, max_depth=max_depth,
                              ns_area_light=ns_area_light, seed=seed & 0xFFFFFFFF, sample_base=sample_base)
         check(self._lib.pt_set_params(self.handle, ctypes.byref(p)))
+        self._frame = (int(height), int(width))
 
     @staticmethod
     def _tiles(tiles: Sequence[Tuple[int, int, int, int]]):
@@ -89,8 +90,18 @@ class Device:
             arr = np.ascontiguousarray(np.asarray(tiles, dtype=np.int32).reshape(-1, 4))
         return arr, arr.ctypes.data_as(ctypes.POINTER(native.pt_tile))
 
+    def _check_frame(self, arr: np.ndarray, channels: int, dtype, what: str):
+        """The native side writes (x + y*W)*channels elements of `arr` for the
+        frame of the last set_params: anything smaller is refused here."""
+        hw = getattr(self, "_frame", None)
+        if hw is None:  # no frame yet: the native call refuses to render (PT_E_NOSCENE)
+            return
+        if arr.dtype != dtype or not arr.flags.c_contiguous or arr.shape != (hw[0], hw[1], channels):
+            raise ValueError(f"{what}: need a C-contiguous {np.dtype(dtype).name} array of shape "
+                             f"{(hw[0], hw[1], channels)}, got {arr.dtype} {arr.shape}")
+
     def render_tiles(self, tiles, out: np.ndarray, stats: bool = False):
-        assert out.dtype == np.float32 and out.flags.c_contiguous
+        self._check_frame(out, 3, np.float32, "render_tiles")
         keep, arr = self._tiles(tiles)
         flags = _flags(stats)
         check(self._lib.pt_render_tiles(self.handle, arr, len(keep), out.ctypes.data, flags))
@@ -106,10 +117,13 @@ class Device:
     def submit_tile(self, tile, hdr: np.ndarray, rgba: Optional[np.ndarray] = None):
         """pt_tile_submit: queue one tile; its pixels land in `hdr` ((H, W, 3)
         float32) and, toColor'd, in `rgba` ((H, W, 4) uint8) when its batch
-        completes.  Both arrays must stay alive until finish_tiles()."""
-        assert hdr.dtype == np.float32 and hdr.flags.c_contiguous
+        completes.  Both arrays must stay alive until finish_tiles() returns
+        (whatever it returns: it waits for every launched batch first).  The
+        completion thread writes them long after this call, so their shapes
+        are checked against the frame of the last set_params here."""
+        self._check_frame(hdr, 3, np.float32, "submit_tile (hdr)")
         if rgba is not None:
-            assert rgba.dtype == np.uint8 and rgba.flags.c_contiguous and rgba.shape[-1] == 4
+            self._check_frame(rgba, 4, np.uint8, "submit_tile (rgba)")
         t = native.pt_tile(*[int(v) for v in tile])
         check(self._lib.pt_tile_submit(self.handle, ctypes.byref(t), hdr.ctypes.data,
                                        None if rgba is None else rgba.ctypes.data))
@@ -316,8 +330,8 @@ class PathTracer:
         the 32x32 FIFO and call raytrace_tile on each, through ONE context
         (calls serialised by a lock, as INTEGRATION.md's adapter does).
         asynchronous=True: raytrace_tile is pt_tile_submit (tiles batched into
-        launches, each completed into sampleBuffer/frameBuffer on a stream
-        callback; the last worker's pt_tile_finish waits for all);
+        launches, each completed into sampleBuffer/frameBuffer by the context's
+        completion thread; the last worker's pt_tile_finish waits for all);
         asynchronous=False: one synchronous pt_render_tiles launch per tile."""
         import queue
         import threading

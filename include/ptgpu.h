@@ -211,12 +211,17 @@ typedef struct pt_stats {
                               (queue drained), stepping a leaf; node steps = node_visits */
   int64_t deep_stack_steps; /* traversal lane-steps taken while the ray's stack held entries beyond the
                               PT_STACK (24) kept in LDS, i.e. in the global spill area */
-  int64_t partial_bytes;   /* device bytes of the sample-group sums one render slot holds for the last
-                              launch's frame (W*H*ceil(spp/group_spp)*12; two slots pipeline renders) */
+  int64_t partial_bytes;   /* device bytes of the sample-group sums of the last launch: 12 B per work slot
+                              of its own blocks (pixels * (spp/group_spp + tail_spp) * 12 at most; a rank
+                              rendering 1/N of a frame's tiles holds 1/N of them; two render slots
+                              pipeline renders) */
   int32_t footprint[4];    /* the scene's screen footprint of the last launch, x0, y0, x1, y1 inclusive and
                               clamped to the frame: every pixel outside it has radiance 0 for every sample
                               (its camera ray misses the scene box; not traced).  The whole frame when
-                              culling is off (environment light, camera not in front of the box). */
+                              culling is off (environment light, camera not in front of the box); the
+                              empty rectangle (0, 0, -1, -1) when the box is entirely off-screen. */
+  int32_t tail_spp;        /* of spp: samples per pixel in one-sample work slots handed out last (the
+                              launch ends on short slots); the others are in groups of group_spp */
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */
@@ -267,7 +272,11 @@ int pt_render_tiles_device(pt_ctx* ctx, const pt_tile* tiles, int32_t n_tiles, f
  * submitted tile.  Tiles render with the scene/camera/params of submission
  * (the setters and the synchronous renders first launch what is queued).  The
  * pixels equal those of a whole-frame pt_render_tiles bit for bit.  A failed
- * completion (HIP error) is reported by the next pt_tile_finish. */
+ * launch or completion is returned by the call that hit it (a launch) and
+ * ALSO by the next pt_tile_finish: its tiles were not rendered.  Whatever it
+ * returns, pt_tile_finish returns only after every launched batch has been
+ * completed, so the caller's buffers stay in use until pt_tile_finish returns
+ * and are free afterwards, on success or error. */
 int pt_tile_submit(pt_ctx* ctx, const pt_tile* tile, float* hdr_out_host, uint32_t* rgba_out_host);
 int pt_tile_finish(pt_ctx* ctx);
 /* Batched BVHAccel::intersect.  Rays: origin o[3n], direction d[3n] (normalised),

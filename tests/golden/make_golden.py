@@ -16,9 +16,9 @@ available on the GPU box) and stores inputs + outputs as small PTDUMP files:
   <scene>env_<W>x<H>...        scenes / renders with the EnvironmentLight (-e)
   CBspheres_refraction_*       the glass sphere of CBspheres.dae as a <refraction>
                                material (RefractionBSDF, bsdf.cpp:90-111)
-  c3proxy_128x128_s64_* / c5proxy_128x128_s64_*
+  c3proxy_128x128_s64_* / c5proxy_128x128_s64_* / c5bigproxy_128x128_s64_*
                                reference renders of the BASELINE C3 / C5 proxy scenes
-                               (scenes.proxy_path(1); scenes.c5_path(2) + its env map)
+                               (scenes.proxy_path(1); scenes.c5_path(2) and c5_path(3) + the env map)
                                at 128x128, 64 spp, two seeds (statistical parity)
   tocolor_in.ptd / tocolor_ref.ptd
                                HDR edge cases -> HDRImageBuffer::toColor's RGBA8
@@ -146,12 +146,16 @@ def make_tocolor():
     run(["--mode", "tocolor", "--in", src, "--out", os.path.join(HERE, "tocolor_ref.ptd")])
 
 
-def make_baseline_scenes():
+def make_baseline_scenes(only=None):
     """The reference's own renders of the C3 and C5 proxies (default camera,
-    -m 4 -l 1) at 128x128, 64 spp, seeds 1 and 2."""
+    -m 4 -l 1) at 128x128, 64 spp, seeds 1 and 2; c5bigproxy is C5 at
+    BASELINE's "~1M tris" scale (CBbunny_sub3_c5, 1,828,877 primitives)."""
     from dsgpuraytracing_amd import scenes
     for name, dae, env in (("c3proxy", scenes.proxy_path(1), None),
-                           ("c5proxy", scenes.c5_path(2), scenes.c5_envmap_path())):
+                           ("c5proxy", scenes.c5_path(2), scenes.c5_envmap_path()),
+                           ("c5bigproxy", scenes.c5_path(3), scenes.c5_envmap_path())):
+        if only and name != only:
+            continue
         for seed in (1, 2):
             out = os.path.join(HERE, f"{name}_128x128_s64_m4_l1_seed{seed}.hdr.ptd")
             args = [dae, "-w", "128", "-h", "128", "-s", "64", "-m", "4", "-l", "1", "--seed", str(seed), "--out", out]
@@ -172,6 +176,8 @@ def main():
         return make_tocolor()
     if only == "baseline":
         return make_baseline_scenes()
+    if only == "c5big":
+        return make_baseline_scenes("c5bigproxy")
     make_env()
     if only:
         return

@@ -58,3 +58,36 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(native.pt_bvh_node) == 6 * 8 + 4 * 8
     assert ctypes.sizeof(native.pt_params) == 28  # + sample_base
     assert ctypes.sizeof(native.pt_tile) == 16
+
+
+def _fastdiv_init(d):
+    """pt_fastdiv_init (csrc/pt_device.h), restated."""
+    l = 0
+    while (1 << l) < d:
+        l += 1
+    if (1 << l) == d:
+        return 0, l
+    return ((1 << (31 + l)) + d - 1) // d, l - 1
+
+
+def _fastdiv(u, m, sh):
+    return (u * m >> 32) >> sh if m else u >> sh
+
+
+def test_fastdiv_exact():
+    """The kernel's unit -> block division (pt_fastdiv: multiply-high and
+    shift) equals integer division for every divisor up to 4096 over u < 2^31:
+    exhaustively for small u, at every multiple of d and its neighbours near
+    the top of the range, and at random points."""
+    import numpy as np
+    rng = np.random.default_rng(5)
+    top = (1 << 31) - 1
+    for d in list(range(1, 4097)) + [65535, 65536, 100003, (1 << 20) + 1]:
+        m, sh = _fastdiv_init(d)
+        assert m < (1 << 32)
+        us = list(range(0, 2000)) + [top, top - 1] + [int(x) for x in rng.integers(0, top, 200)]
+        k = top // d
+        us += [k * d - 1, k * d, min(top, k * d + d - 1), (k - 1) * d, (k - 1) * d - 1]
+        for u in us:
+            if 0 <= u <= top:
+                assert _fastdiv(u, m, sh) == u // d, (d, u)

@@ -139,16 +139,16 @@ def test_failing_rank_stops_every_rank(tmp_path, world, fail_rank):
         assert float(secs) < 15  # seconds, far below the 20 s group timeout
 
 
-def _knob_worker(rank, world, port, out_dir):
+def _knob_worker(rank, world, port, out_dir, knob="PT_SAMPLE_GROUP", value="8"):
     import sys
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     from dsgpuraytracing_amd.dist import RankFailure, check_value_knobs
     dist.init_process_group("gloo", rank=rank, world_size=world)
     if rank == 1:
-        os.environ["PT_SAMPLE_GROUP"] = "8"
+        os.environ[knob] = value
     else:
-        os.environ.pop("PT_SAMPLE_GROUP", None)
+        os.environ.pop(knob, None)
     code = 0
     try:
         check_value_knobs({"group_spp": 4})
@@ -162,17 +162,20 @@ def _knob_worker(rank, world, port, out_dir):
     sys.exit(code)
 
 
-def test_value_knobs_must_agree(tmp_path):
-    """PT_SAMPLE_GROUP changes each pixel's float summation order: ranks that
-    differ would break the bit-identity of the assembled frame, so the split
-    refuses to start."""
+@pytest.mark.parametrize("knob,value", [("PT_SAMPLE_GROUP", "8"), ("PT_TAIL_SPL", "4"), ("PT_SAH_BINS", "64"),
+                                        ("PT_SAH_CI", "1.5"), ("PT_SAH_LEAF", "2"), ("PT_NO_FOOTPRINT_CULL", "1")])
+def test_value_knobs_must_agree(tmp_path, knob, value):
+    """PT_SAMPLE_GROUP / PT_TAIL_SPL change each pixel's float summation order
+    (so does PT_NO_FOOTPRINT_CULL's traced set), the PT_SAH_* knobs the host
+    SAH tree and so its tie-breaks: ranks that differ would break the
+    bit-identity of the assembled frame, so the split refuses to start."""
     ctx = mp.get_context("spawn")
     port = _free_port()
-    ps = [ctx.Process(target=_knob_worker, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    ps = [ctx.Process(target=_knob_worker, args=(r, 2, port, str(tmp_path), knob, value)) for r in range(2)]
     for p in ps:
         p.start()
     for p in ps:
         p.join(60)
     assert [p.exitcode for p in ps] == [3, 3]
     for r in range(2):
-        assert "PT_SAMPLE_GROUP" in open(tmp_path / f"knob{r}.txt").read()
+        assert knob in open(tmp_path / f"knob{r}.txt").read()

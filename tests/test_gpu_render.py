@@ -133,14 +133,16 @@ def test_hip_refraction_statistical_vs_reference_golden():
     assert bias <= 3 * sigma
 
 
-@pytest.mark.parametrize("name", ["c3proxy", "c5proxy"])
+@pytest.mark.parametrize("name", ["c3proxy", "c5proxy", "c5bigproxy"])
 def test_hip_baseline_proxy_statistical_vs_reference_golden(name):
     """The BASELINE C3 / C5 proxy scenes at 128x128 @ 64 spp vs the reference
-    binary's own renders (two seeds: the noise floor).  Same criterion as the
-    fixture scenes: mean per-pixel RGB-L2 <= 1.10 x the
-    reference's seed-to-seed distance, image-mean bias <= 3 sigma."""
+    binary's own renders (two seeds: the noise floor); c5bigproxy is C5 at
+    BASELINE's "~1M tris" scale (CBbunny_sub3_c5, 1,828,877 primitives).  Same
+    criterion as the fixture scenes: mean per-pixel RGB-L2
+    <= 1.10 x the reference's seed-to-seed distance, image-mean bias <= 3 sigma."""
     from dsgpuraytracing_amd import scenes
-    dae, env = (scenes.proxy_path(1), None) if name == "c3proxy" else (scenes.c5_path(2), scenes.c5_envmap_path())
+    dae, env = {"c3proxy": (scenes.proxy_path(1), None), "c5proxy": (scenes.c5_path(2), scenes.c5_envmap_path()),
+                "c5bigproxy": (scenes.c5_path(3), scenes.c5_envmap_path())}[name]
     r1 = ptdump.read(golden(f"{name}_128x128_s64_m4_l1_seed1.hdr.ptd"))["hdr"].reshape(128, 128, 3)
     r2 = ptdump.read(golden(f"{name}_128x128_s64_m4_l1_seed2.hdr.ptd"))["hdr"].reshape(128, 128, 3)
     sc = Scene.from_dae(dae, 128, 128, envmap=env)
@@ -712,6 +714,43 @@ def test_hip_tile_workers_seam_bit_identical(monkeypatch, batch, threads, asynch
     pt.frameBuffer[...] = 0
     pt.render_tile_workers(num_threads=threads, asynchronous=asynchronous, tiles=tiles[::-1])
     assert np.array_equal(pt.sampleBuffer, whole.sampleBuffer)
+
+
+def test_hip_tile_finish_drains_after_a_failed_launch(monkeypatch):
+    """a batch launch that fails (injected: PT_FAULT_TILE_LAUNCH=3,
+    one tile per batch) is reported by the submit that hit it AND by the next
+    pt_tile_finish, which still waits for every batch launched before it: the
+    tiles of batches 1-2 are complete in the caller's buffers when finish
+    returns, the dropped tile is untouched, and the context keeps working."""
+    from dsgpuraytracing_amd.pathtracer import Device
+    monkeypatch.setenv("PT_TILE_BATCH", "1")
+    monkeypatch.setenv("PT_FAULT_TILE_LAUNCH", "3")
+    sc = Scene.from_dump(golden("c1_default_64x64.scene.ptd"))
+    w = h = 64
+    dev = Device(0)
+    dev.upload_scene(sc)
+    dev.set_camera(sc.camera)
+    dev.set_params(w, h, 64, 4, 1, 9)
+    whole = np.zeros((h, w, 3), np.float32)
+    dev.render_tiles(tile_fifo(w, h), whole)
+    hdr = np.full((h, w, 3), -1.0, np.float32)
+    tiles = tile_fifo(w, h)  # 4 tiles
+    dev.submit_tile(tiles[0], hdr)
+    dev.submit_tile(tiles[1], hdr)
+    with pytest.raises(native.PtError) as e:
+        dev.submit_tile(tiles[2], hdr)  # the 3rd launch fails
+    assert "injected" in str(e.value)
+    with pytest.raises(native.PtError) as e:
+        dev.finish_tiles()  # reported again: tile 2 was never rendered
+    assert "injected" in str(e.value)
+    for t, done in zip(tiles[:3], (True, True, False)):
+        x, y, tw, th = t
+        part, ref = hdr[y:y + th, x:x + tw], whole[y:y + th, x:x + tw]
+        assert np.array_equal(part, ref) if done else (part == -1.0).all()
+    dev.submit_tile(tiles[2], hdr)
+    dev.submit_tile(tiles[3], hdr)
+    dev.finish_tiles()  # the error was consumed: this frame completes cleanly
+    assert np.array_equal(hdr, whole)
 
 
 @pytest.mark.parametrize("w,h,threads", [(256, 192, 8), (200, 136, 3)])

@@ -27,7 +27,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dsgpuraytracing_amd.elfsha import kernel_sha256  # noqa: E402
 
 # render_kernel<STATS, DBG, BIN, ENV, GTAB>: the timed launch of each workload
-KERNELS = {"c5": "render_kernel<false, false, false, true, false>"}
+KERNELS = {"c5": "render_kernel<false, false, false, true, false>", "c5big": "render_kernel<false, false, false, true, false>"}
 KERNEL = "render_kernel<false, false, false, false, false>"
 
 
