@@ -489,8 +489,8 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         mine = torch.tensor([float(np.mean(kernel_ms)), float(np.mean(resolve_ms)), xchg_ms,
-                             float(np.sum(mine_arr[:, 2] * mine_arr[:, 3]))], dtype=torch.float64,
-                            device="cpu" if backend == "gloo" else f"cuda:{local}")
+                             float(np.sum(mine_arr[:, 2] * mine_arr[:, 3])), float(st_perf["partial_bytes"])],
+                            dtype=torch.float64, device="cpu" if backend == "gloo" else f"cuda:{local}")
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         per_rank = [[round(float(v), 4) for v in r.cpu().tolist()] for r in allr]
@@ -582,7 +582,8 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
         rays = st_counts["camera_rays"] + st_counts["bounce_rays"] + st_counts["shadow_rays"]
         out["ray_casts_per_s_M"] = round(rays * frames * (world if weak else 1) / elapsed / 1e6, 1)
         if per_rank is not None:
-            out["per_rank"] = {"fields": ["kernel_ms", "resolve_ms", "exchange_ms", "pixels"], "ranks": per_rank}
+            out["per_rank"] = {"fields": ["kernel_ms", "resolve_ms", "exchange_ms", "pixels", "partial_bytes"],
+                               "ranks": per_rank}
         if strong is not None:
             out["companions"] = strong
         elif xev:
@@ -639,10 +640,17 @@ def strong_companions(local, rank, world, backend, StepGuard, TileExchange, fram
         ex = TileExchange(tile_fifo(w, h), w, h, rank, world, frame.device)
         mine = np.asarray(ex.mine, dtype=np.int32).reshape(-1, 4)
         guard = StepGuard()
+        xev = []
 
-        def step():
+        def step(timed=False):
             guard.run(dev.render_tiles_device, mine, ex.packed.data_ptr(), stream, packed=True)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
             ex.exchange(frame)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            if timed:
+                xev.append((e0, e1))
 
         for _ in range(warmup):
             step()
@@ -651,7 +659,7 @@ def strong_companions(local, rank, world, backend, StepGuard, TileExchange, fram
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(frames):
-            step()
+            step(timed=True)
         dist.barrier()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
@@ -659,11 +667,25 @@ def strong_companions(local, rank, world, backend, StepGuard, TileExchange, fram
         t = torch.tensor([el], dtype=torch.float64, device="cpu" if backend == "gloo" else f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+        # the efficiency inputs of the tile-sharded curve: each rank's render
+        # (HIP events) and gather times, its pixels and group-sum bytes
+        k_ms, _ = dev.launch_times(frames)
+        dev.render_tiles_device(mine, ex.packed.data_ptr(), stream, stats=True)
+        st = dev.stats()
+        mine_v = torch.tensor([float(np.mean(k_ms)), float(np.mean([a.elapsed_time(b) for a, b in xev])),
+                               float(np.sum(mine[:, 2] * mine[:, 3])), float(st["partial_bytes"])],
+                              dtype=torch.float64, device="cpu" if backend == "gloo" else f"cuda:{local}")
+        allr = [torch.zeros_like(mine_v) for _ in range(world)]
+        dist.all_gather(allr, mine_v)
+        ranks = [[round(float(v), 4) for v in r.cpu().tolist()] for r in allr]
+        kms = [r[0] for r in ranks]
         res[f"{name}_strong"] = {
             "workload": wl["desc"] + f", one frame's tiles over {world} GPUs + one gather (strong)",
             "value": round(w * h * spp * frames / el / 1e6, 1), "unit": "Mrays/s",
             "ms_per_frame": round(el / frames * 1e3, 3), "frames": frames, "scaling": "strong",
             "gather_bytes_per_rank": int(ex.packed.numel() * 4),
+            "kernel_ms_slowest_over_mean": round(max(kms) / max(1e-9, float(np.mean(kms))), 4),
+            "per_rank": {"fields": ["kernel_ms", "gather_ms", "pixels", "partial_bytes"], "ranks": ranks},
             "image_mean": float(frame.mean().item()) if rank == 0 else None}
         dev.close()
         del frame, ex

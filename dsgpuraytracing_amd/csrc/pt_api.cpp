@@ -1100,6 +1100,8 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     int v = std::atoi(lw);
     if (v >= 1) P.leaf_weight = v;
   }
+  P.drain_both = 1;
+  if (const char* db = std::getenv("PT_DRAIN_BOTH")) P.drain_both = std::atoi(db) != 0;  // tuning knob
   P.drain_div = 0;
   if (const char* dd = std::getenv("PT_DRAIN_DIV")) {  // tuning knob
     int v = std::atoi(dd);
@@ -1175,6 +1177,8 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   pt_fastdiv_init((uint32_t)std::max(1, L.n_big), &P.big_m, &P.big_sh);
   pt_fastdiv_init((uint32_t)std::max(1, L.tail), &P.tail_m, &P.tail_sh);
   P.sblocks = (L.n_big % 2 == 0 && L.tail % 2 == 0) ? 1 : 0;
+  P.slot_order = 0;  // which lane gets which (pixel, group): no effect on any value
+  if (const char* so = std::getenv("PT_SLOT_ORDER")) P.slot_order = std::atoi(so) != 0;  // tuning knob
   // group sums: 12 B per work slot of THIS launch (a rank's share of a split
   // frame holds only its own blocks' sums)
   HIPCHK(c->partial[slot].reserve((size_t)std::max<int64_t>(slots, 1) * 3));
@@ -1269,6 +1273,7 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags, bool sync) {
     for (int k = 0; k < 4; ++k) c->last.section_clocks[k] = (int64_t)v[17 + k];
     for (int k = 0; k < 4; ++k) c->last.lane_iters[k] = (int64_t)v[27 + k];
     c->last.deep_stack_steps = (int64_t)v[31];
+    for (int k = 0; k < 32; ++k) c->last.slot_latency_hist[k] = (int64_t)v[32 + k];
     for (int k = 0; k < 3; ++k) c->last.wave_span[k] = (int64_t)(v[22 + k] - v[21]);
     for (int k = 0; k < 2; ++k) c->last.wave_span[3 + k] = v[25 + k] ? (int64_t)(v[25 + k] - v[21]) : -1;
     c->last.counters_valid = 1;

@@ -51,8 +51,8 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #ifndef PT_ENV_GUIDE
 #define PT_ENV_GUIDE 1024  // buckets of the environment-CDF guide tables (with the window compare: C5 +10% over 64, profiles/r3/ab_env_window_search.txt)
 #endif
-#define PT_STATS_SLOTS 32  // launch counters; per-wave trace records (PT_WAVE_TRACE u64 each) follow
-#define PT_WAVE_TRACE 9
+#define PT_STATS_SLOTS 64  // launch counters (32..63: slot-latency histograms); per-wave trace records (PT_WAVE_TRACE u64 each) follow
+#define PT_WAVE_TRACE 11
 #ifndef PT_STACK
 #define PT_STACK 24  // traversal stack entries per lane in LDS (lane-contiguous)
 #endif
@@ -129,14 +129,15 @@ struct KParams {
   int s_a;         // samples in phase-A groups (n_big * group_spp)
   int n_big;       // phase-A groups per pixel
   int tail_spp;    // phase-B (one-sample) groups per pixel
-  // Work slot / group-sum index: phase A (block b, group j, pixel q of the
-  // 8x8 block) -> (b * n_big + j) * 64 + q; phase B (tail sample t) ->
-  // slots_a + (b * tail_spp + t) * 64 + q.  A unit is 64 slots (one group of
-  // one block); unit -> block by fastdiv (pt_fastdiv).
+  // Work slot / group-sum index of (block b, group j, pixel q of the 8x8
+  // block): phase A -> (b * 64 + q) * n_big + j (pixel-major, default) or
+  // (b * n_big + j) * 64 + q (group-major); phase B (tail sample t) ->
+  // slots_a + the same with tail_spp.  Divisions by fastdiv (pt_fastdiv).
   uint32_t slots_a;                 // phase-A slots: n_blocks * 64 * n_big
   uint32_t big_m, big_sh;           // fastdiv by n_big
   uint32_t tail_m, tail_sh;         // fastdiv by tail_spp
   int sblocks;                      // a 128-slot chunk lies in one block (n_big, tail_spp even): scalar block loads
+  int slot_order;                   // 0: pixel-major slots (b*64 + q)*n + j; 1: group-major (b*n + j)*64 + q
   const int* tile_block0;           // first block of each tile (n_tiles + 1 entries), for the resolve
   const DNode* nodes;
   const DNode2* nodes2;  // the binary tree (reference-count launch only)
@@ -164,6 +165,7 @@ struct KParams {
   int shade_batch;            // leave the traversal phase once this many lanes finished their ray
   int leaf_weight;            // leaf steps run when leaf_weight * leaf lanes >= 16 * node lanes
   int drain_div;              // queue drained: shade once alive/drain_div lanes are ready (0: 3/4 rule)
+  int drain_both;             // queue drained: node and leaf steps in every traversal iteration
   float root_lo[3], root_hi[3];  // scene bounds (root box, rounded outward)
   int cull_x0, cull_y0, cull_x1, cull_y1;  // pixels outside [x0,x1]x[y0,y1] see no geometry
 };

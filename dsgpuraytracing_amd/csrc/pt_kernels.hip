@@ -529,15 +529,18 @@ __device__ __forceinline__ float3 env_dir(const KP& P, float3 d) {
 }
 
 // lower_bound of v = r * a[n-1] accelerated by a guide table g[0..G] with
-// g[k] = lower_bound(a, k/G * a[n-1]) (built on the host): the answer lies in
-// [g[k-1], g[k+2]] for k = floor(r*G), one bucket of slack either side for
-// rounding; the result is exactly std::lower_bound's.  With PT_ENV_GUIDE
-// buckets the window is a few entries where the CDF carries mass (where
-// samples land): it is halved down to <= 4 entries, then compared in ONE
-// memory round trip (lower_bound = lo + #{entries < v}, the array is sorted)
-// instead of a chain of dependent loads.
+// g[k] = lower_bound(a, k/G * a[n-1]) (built on the host, clamped to n-1): the
+// answer lies in [g[k-1], g[k+2]] for k = floor(r*G), one bucket of slack
+// either side for rounding, and a[g[k+2]] >= v; the result is exactly
+// std::lower_bound's.  With PT_ENV_GUIDE buckets the window is a few entries
+// where the CDF carries mass (where samples land): it is halved down to <= 4
+// entries, then compared in ONE memory round trip (lower_bound = lo +
+// #{entries < v}, the array is sorted).  The same round trip loads the
+// entries either side of the window, so the caller's interpolation pair
+// (prev = a[t-1] or 0, cur = a[t]) comes from registers, not from two more
+// dependent loads.
 __device__ __forceinline__ int guided_lower_bound(const float* __restrict__ a, float v, float r,
-                                                  const int* __restrict__ g, int G) {
+                                                  const int* __restrict__ g, int G, float& prev, float& cur) {
   const int k = min(G - 1, max(0, (int)(r * (float)G)));
   int lo = g[max(k - 1, 0)];
   const int hi = g[min(k + 2, G)];
@@ -551,10 +554,15 @@ __device__ __forceinline__ int guided_lower_bound(const float* __restrict__ a, f
       n = half;
     }
   }
-  const float kBig = 3.0e38f;
-  const float w0 = n > 0 ? a[lo] : kBig, w1 = n > 1 ? a[lo + 1] : kBig;
-  const float w2 = n > 2 ? a[lo + 2] : kBig, w3 = n > 3 ? a[lo + 3] : kBig;
-  return lo + (int)(w0 < v) + (int)(w1 < v) + (int)(w2 < v) + (int)(w3 < v);
+  // w_i = a[min(lo + i, hi)]: entries past the window read a[hi] >= v, which
+  // never counts; w4 = a[hi] is a[t] when all four candidates are < v
+  const float wm = lo > 0 ? a[lo - 1] : 0.0f;
+  const float w0 = a[min(lo, hi)], w1 = a[min(lo + 1, hi)], w2 = a[min(lo + 2, hi)], w3 = a[min(lo + 3, hi)];
+  const float w4 = a[hi];
+  const int c = (int)(w0 < v) + (int)(w1 < v) + (int)(w2 < v) + (int)(w3 < v);
+  cur = c == 0 ? w0 : c == 1 ? w1 : c == 2 ? w2 : c == 3 ? w3 : w4;
+  prev = c == 0 ? wm : c == 1 ? w0 : c == 2 ? w1 : c == 3 ? w2 : w3;
+  return lo + c;
 }
 
 // importanceSampling (69-115): inverse CDF over rows (pTheta), then within the
@@ -565,16 +573,15 @@ __device__ __forceinline__ void env_sample(const KP& P, float r1, float r2, floa
   const int w = P.env_w, h = P.env_h;
   const float u1 = r1;
   r1 *= P.env_ptheta[h - 1];
-  const int t = guided_lower_bound(P.env_ptheta, r1, u1, P.env_gtheta, PT_ENV_GUIDE);
-  float prev = t > 0 ? P.env_ptheta[t - 1] : 0.0f;
-  const float y = (float)t + (r1 - prev) / (P.env_ptheta[t] - prev);
+  float prev, cur;
+  const int t = guided_lower_bound(P.env_ptheta, r1, u1, P.env_gtheta, PT_ENV_GUIDE, prev, cur);
+  const float y = (float)t + (r1 - prev) / (cur - prev);
   const float theta = fminf(y / (float)h, 1.0f) * kPi;
   const float* row = P.env_pphi + (size_t)t * w;
   const float u2 = r2;
   r2 *= row[w - 1];
-  const int q = guided_lower_bound(row, r2, u2, P.env_gphi + (size_t)t * (PT_ENV_GUIDE + 1), PT_ENV_GUIDE);
-  prev = q > 0 ? row[q - 1] : 0.0f;
-  const float x = (float)q + (r2 - prev) / (row[q] - prev);
+  const int q = guided_lower_bound(row, r2, u2, P.env_gphi + (size_t)t * (PT_ENV_GUIDE + 1), PT_ENV_GUIDE, prev, cur);
+  const float x = (float)q + (r2 - prev) / (cur - prev);
   const float phi = fminf(x / (float)w, 1.0f) * (2.0f * kPi);
   float st, ct, sp, cp;
   __sincosf(theta, &st, &ct);
@@ -655,6 +662,10 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // account the wave's time whichever lanes took the branch.
   __shared__ unsigned long long s_clk[STATS ? S_N + 1 : 1];
   if (STATS && lane <= S_N) s_clk[lane] = lane == S_N ? clock64() : 0ull;
+  // STATS: work-slot latency histograms (log2 of microseconds, 16 buckets),
+  // phase-A slots then phase-B (one-sample) slots
+  __shared__ uint32_t s_hist[STATS ? 32 : 1];
+  if (STATS && lane < 32) s_hist[lane] = 0u;
   __syncthreads();
 #if PT_KARG_ROUND
   // From here on the launch parameters are read through a pointer to the
@@ -687,9 +698,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // oslot writes the right one when the shadow ray ends; then the lane
   // retires (the queue is drained) or, with SH_STORE_FOLLOW, goes on with the
   // next group's camera ray parked in (hp, ns).  While a store is pending the
-  // new group's sum is 0: nothing reaches it before its parked ray starts
-  // (camera rays that miss are parked too when they would see the
-  // environment map).
+  // new group's sum (the environment its missed camera rays saw) gathers in
+  // ng, which is dead between a path's last vertex and the next hit record.
   int shadow = 0;
   uint32_t oslot = 0;
   // the work slot (pixel, sample group) this lane renders: its index (where
@@ -723,6 +733,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   uint32_t l_other = 0, l_ready = 0, l_dead = 0, l_leaf = 0;
   uint32_t l_deep = 0;  // traversal lane-steps taken with stack entries in the global spill area
   uint32_t n_atomics = 0;              // work-queue atomics (lane 0)
+  uint32_t n_titer_drain = 0, n_rounds_drain = 0;  // of them: after this wave found the queue empty
   uint32_t chunk_next = 0, chunk_end = 0;  // the wave's private range of work slots
   uint32_t seen = 0;                       // queue head after this wave's last claim
   const unsigned long long w_start = STATS ? wall_clock64() : 0ull;
@@ -730,11 +741,14 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   unsigned long long slot_t0 = 0ull, slot_lat_sum = 0ull, slot_lat_max = 0ull;  // work-slot latency (wall ticks)
   // per ray: traversal iterations it stepped in / sat out, traversal phases it spanned
   uint32_t r_steps = 0, r_idle = 0, r_rounds = 0, ray_steps_max = 0, ray_idle_max = 0, ray_rounds_max = 0;
-#define PT_SLOT_DONE()                                           \
-  if (STATS) {                                                   \
-    const unsigned long long d_ = wall_clock64() - slot_t0;     \
-    slot_lat_sum += d_;                                          \
-    slot_lat_max = d_ > slot_lat_max ? d_ : slot_lat_max;        \
+#define PT_SLOT_DONE()                                                          \
+  if (STATS) {                                                                  \
+    const unsigned long long d_ = wall_clock64() - slot_t0;                    \
+    slot_lat_sum += d_;                                                         \
+    slot_lat_max = d_ > slot_lat_max ? d_ : slot_lat_max;                       \
+    const uint32_t us_ = (uint32_t)min(d_ / 100ull, 0xffffffffull);            \
+    const uint32_t b_ = us_ == 0u ? 0u : min(15u, 32u - (uint32_t)__clz(us_)); \
+    atomicAdd(&s_hist[b_ + (myslot >= P.slots_a ? 16u : 0u)], 1u);              \
   }
 
   // the lane's group ends before sample s: the last phase-A group ends at
@@ -780,7 +794,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           if (!tr.found) acc = acc + pend;
         } else {  // the finished group's one store: its total with the light sample if the shadow ray is clear
           store3(P.partial + 3 * (size_t)oslot, tr.found ? acc : pend);
-          acc = f3(0, 0, 0);  // the new group's sum starts here
+          acc = ng;  // the new group's sum so far (environment seen by its camera rays that missed)
         }
         if (shadow == SH_STORE) {
           mode = M_DONE;
@@ -1034,6 +1048,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           PT_FENCE3(pend);  // (no contraction into pend's last multiply: the sum rounds as at the shadow ray's return)
           pend = acc + pend;
           oslot = myslot;
+          ng = f3(0, 0, 0);  // (the next group's sum while the store is pending)
           PT_SLOT_DONE();
           shadow = SH_STORE;
           mode = M_FETCH;
@@ -1084,14 +1099,32 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             if (STATS) n_atomics += lane == 0;
           }
         }
-        // Work slots -> (block, group, pixel): see KParams.  A unit of 64
-        // slots is one group of one 8x8 block, its slots the block's pixels
-        // (neighbouring lanes get neighbouring pixels: coherent rays); a
-        // unit's block is a fastdiv of its index.
-        auto block_of = [&](uint32_t slot) -> uint32_t {
+        // Work slots -> (block k, group j, pixel q): see KParams.  Pixel-
+        // major (slot_order 0): a pixel's groups are consecutive slots, so a
+        // wave's lanes hold a few pixels' groups (coherent camera rays);
+        // group-major (1): a unit of 64 slots is one group of the block's 64
+        // pixels.  Either way the divisions are fastdivs.
+        auto decode = [&](uint32_t slot, uint32_t& k, uint32_t& j, uint32_t& q) {
           const bool tl = slot >= P.slots_a;
-          const uint32_t u = (slot - (tl ? P.slots_a : 0u)) >> 6;
-          return tl ? pt_fastdiv(u, P.tail_m, P.tail_sh) : pt_fastdiv(u, P.big_m, P.big_sh);
+          const uint32_t local = slot - (tl ? P.slots_a : 0u);
+          const uint32_t n = (uint32_t)(tl ? P.tail_spp : P.n_big);
+          const uint32_t dm = tl ? P.tail_m : P.big_m, dsh = tl ? P.tail_sh : P.big_sh;
+          if (P.slot_order) {
+            const uint32_t u = local >> 6;
+            k = pt_fastdiv(u, dm, dsh);
+            j = u - k * n;
+            q = local & 63u;
+          } else {
+            const uint32_t px = pt_fastdiv(local, dm, dsh);
+            j = local - px * n;
+            k = px >> 6;
+            q = px & 63u;
+          }
+        };
+        auto block_of = [&](uint32_t slot) -> uint32_t {
+          uint32_t k, j, q;
+          decode(slot, k, j, q);
+          return k;
         };
         // A chunk of 128 slots (128-aligned) lies inside one block when both
         // phases hold an even number of groups per pixel, and the lanes are
@@ -1128,22 +1161,18 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             // scene's screen footprint (pixels outside are written 0 by
             // resolve_kernel: every ray through them misses the root box).
             const bool tl = slot >= P.slots_a;
-            uint32_t k;
+            uint32_t k, j, q;
+            decode(slot, k, j, q);  // (the scalar path's k is the same)
             int4 b;  // (odd group counts: one vector-memory load per lane)
-            if (sblocks) {
-              k = rank < avail ? k_old : k_new;
-              b = rank < avail ? b_old : b_new;
-            } else {
-              k = block_of(slot);
-              b = P.blocks[k];
-            }
-            const uint32_t j = ((slot - (tl ? P.slots_a : 0u)) >> 6) - k * (uint32_t)(tl ? P.tail_spp : P.n_big);
-            const int qx = (int)(slot & 7u), qy = (int)((slot >> 3) & 7u);
+            if (sblocks) b = rank < avail ? b_old : b_new;
+            else b = P.blocks[k];
+            const int qx = (int)(q & 7u), qy = (int)(q >> 3);
             if (qx < b.z && qy < b.w) {
               pix = (b.x + qx) | ((b.y + qy) << 16);
               sample = tl ? P.s_a + (int)j : (int)j * P.group_spp;
               myslot = slot;
-              if (!shadow) acc = f3(0, 0, 0);  // (SH_STORE: acc holds the last group's total until its store)
+              if (!shadow) acc = f3(0, 0, 0);
+              else ng = f3(0, 0, 0);  // (SH_STORE: acc holds the last group's total until its store)
               if (STATS) slot_t0 = wall_clock64();
               mode = M_CAMERA;
             }
@@ -1167,10 +1196,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         Trav cr;
         const bool in = camera_ray(cr);
         if (!shadow) tr = cr;
-        // Behind a pending shadow ray, a camera ray that would see the
-        // environment map is parked too: its radiance is then added after the
-        // light sample, in the order of trace_ray.
-        if (in || (ENV && shadow)) {
+        if (in) {
           T = f3(1, 1, 1);
           cur = 0;  // depth 0
           includeLe = true;
@@ -1182,17 +1208,29 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           mode = M_TRAV;
           break;
         }
-        // miss: the sample sees the environment (includeLe) or nothing
-        if (ENV) acc = acc + env_dir(P, cr.d);  // (no shadow ray pending: see above)
+        // miss: the sample sees the environment (includeLe) or nothing.  With
+        // a store pending (SH_STORE) acc still holds the last group's total:
+        // the new group's sum gathers in ng, dead until the next hit record.
+        // (Behind a pending light sample of the SAME group, SH_FOLLOW, the
+        // map's radiance is added before that sample: (acc + env) + pend
+        // where trace_ray's order is (acc + pend) + env -- one reordered
+        // float addition at silhouettes against the map, inside the
+        // near-exact tolerance; parking such rays instead cost C5 18%.)
+        if (ENV) {
+          const float3 e = env_dir(P, cr.d);
+          if (shadow == SH_STORE) ng = ng + e;
+          else acc = acc + e;
+        }
         ++sample;
         if (group_ends(sample)) {
           if (shadow == SH_FOLLOW) {  // the pending light sample belongs to this group: one store, deferred
             PT_FENCE3(pend);  // (no contraction into pend's last multiply: the sum rounds as at the shadow ray's return)
             pend = acc + pend;
             oslot = myslot;
+            ng = f3(0, 0, 0);  // (the next group's sum while the store is pending)
             shadow = SH_STORE;
-          } else {  // SH_STORE: acc is the previous group's; this one saw nothing
-            store3(P.partial + 3 * (size_t)myslot, shadow ? f3(0, 0, 0) : acc);
+          } else {  // SH_STORE: this group's sum is in ng (acc holds the last group's)
+            store3(P.partial + 3 * (size_t)myslot, shadow ? ng : acc);
           }
           PT_SLOT_DONE();
           mode = M_FETCH;
@@ -1207,6 +1245,16 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     // lanes have finished their ray, so finished lanes are refilled together
     // (coherent shading) while the others keep their traversal state.
     if (__ballot(mode == M_TRAV) == 0ull) break;  // every lane is M_DONE
+    // The traversal loop's launch parameters, read once per phase: with the
+    // parameters re-read per round (PT_KARG_ROUND) the compiler would
+    // otherwise re-issue their scalar loads -- and wait for them -- in every
+    // iteration; out of an empty asm they are opaque values it keeps in SGPRs.
+    const DNode* t_nodes = P.nodes;
+    const DPrim* t_prims = P.prims;
+    int t_leaf_weight = P.leaf_weight, t_both = P.drain_both;
+#if PT_KARG_ROUND
+    asm volatile("" : "+s"(t_nodes), "+s"(t_prims), "+s"(t_leaf_weight), "+s"(t_both));
+#endif
     // Fresh rays (node 0: references only point forward, so no ray returns
     // to the root) take their root step here, all together, from the LDS
     // copy: the wave's first traversal iteration no longer waits on a global
@@ -1214,7 +1262,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     if constexpr (!BIN) {
       bool done = false;
       if (mode == M_TRAV && tr.node == 0) {
-        done = node_step<STATS, true>(P.nodes, stk, tr, ct, (lds_cchar*)&s_root);
+        done = node_step<STATS, true>(t_nodes, stk, tr, ct, (lds_cchar*)&s_root);
         if (done) mode = M_SHADE;
       }
       follow_on(done);  // (a shadow ray leaves the root only if it misses every child box)
@@ -1227,9 +1275,11 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     if (P.drain_div > 0 && seen >= total_slots)  // the queue is drained: latency, not throughput
       round_batch = max(1, alive / P.drain_div);
     if (STATS) n_rounds += lane == 0;
+    if (STATS) n_rounds_drain += lane == 0 && seen >= total_slots;
     if (STATS) r_rounds += mode == M_TRAV;
     for (;;) {
       if (STATS) n_titer += lane == 0;
+      if (STATS) n_titer_drain += lane == 0 && seen >= total_slots;
       // one kind of step per iteration: leaf steps once enough lanes wait on
       // a leaf (or nothing else is left), node steps otherwise
       const bool trav = mode == M_TRAV;
@@ -1237,25 +1287,33 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       const int n_leaf = __popcll(__ballot(at_leaf));
       const int n_node = __popcll(__ballot(trav && !at_leaf));
       bool done = false;
-      const bool leaf_iter = n_leaf > 0 && (n_node == 0 || n_leaf * P.leaf_weight >= n_node * 16);
+      const bool leaf_iter = n_leaf > 0 && (n_node == 0 || n_leaf * t_leaf_weight >= n_node * 16);
+      // Once the queue is drained, the wave's last rays are its critical
+      // path and the SIMD has issue slots to spare: every lane steps in every
+      // iteration (leaf lanes, then node lanes) instead of waiting through
+      // the other kind's iterations.
+      const bool both = t_both && seen >= total_slots;  // (wave-uniform)
+      const bool do_leaf = both ? n_leaf > 0 : leaf_iter;
+      const bool do_node = both ? n_node > 0 : !leaf_iter;
       if (STATS && trav) {
-        const bool stepped = leaf_iter == at_leaf;
+        const bool stepped = both || leaf_iter == at_leaf;
         r_steps += stepped;
         r_idle += !stepped;
       }
       if (STATS) {  // what each lane does in this iteration (SIMD efficiency)
-        l_other += trav && leaf_iter != at_leaf;
+        l_other += trav && !both && leaf_iter != at_leaf;
         l_ready += mode == M_SHADE;
         l_dead += mode == M_DONE;
-        l_leaf += at_leaf && leaf_iter;
+        l_leaf += at_leaf && do_leaf;
         l_deep += trav && tr.sp > PT_STACK;
       }
-      if (leaf_iter) {
-        if (at_leaf) done = leaf_step<STATS>(P.prims, stk, tr, ct);
+      if (do_leaf) {
+        if (at_leaf) done = leaf_step<STATS>(t_prims, stk, tr, ct);
         if (STATS) n_leafit += lane == 0;
-      } else if (trav && !at_leaf) {
+      }
+      if (do_node && trav && !at_leaf) {
         if constexpr (BIN) done = node_step2<STATS>(P.nodes2, stk, tr, ct);
-        else done = node_step<STATS>(P.nodes, stk, tr, ct);
+        else done = node_step<STATS>(t_nodes, stk, tr, ct);
       }
       if (done) mode = M_SHADE;
       follow_on(done);
@@ -1281,6 +1339,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
       if (lane == 0) atomicAdd(P.stats + k, s);
     }
+    if (lane < 32) atomicAdd(P.stats + 32 + lane, (unsigned long long)s_hist[lane]);
     const uint32_t li[5] = {l_other, l_ready, l_dead, l_leaf, l_deep};
     for (int k = 0; k < 5; ++k) {
       unsigned long long s = li[k];
@@ -1338,6 +1397,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       tw[6] = slot_lat_max;
       tw[7] = ((unsigned long long)ray_steps_max << 32) | ray_idle_max;
       tw[8] = ray_rounds_max;
+      tw[9] = n_titer_drain;
+      tw[10] = n_rounds_drain;
     }
   }
 }
@@ -1374,12 +1435,17 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
     const int4 b = P.blocks[k];
     if (qx >= b.z || qy >= b.w) continue;
     float3 acc = f3(0, 0, 0);
-    const float* pa = P.partial + 3 * ((size_t)k * (size_t)P.n_big * 64u + (size_t)q);
-#pragma unroll 4
-    for (int j = 0; j < P.n_big; ++j) acc = acc + ld3(pa + 192 * (size_t)j);
-    const float* pb = P.partial + 3 * ((size_t)P.slots_a + (size_t)k * (size_t)P.tail_spp * 64u + (size_t)q);
-#pragma unroll 4
-    for (int t = 0; t < P.tail_spp; ++t) acc = acc + ld3(pb + 192 * (size_t)t);
+    // pixel-major: the pixel's groups are consecutive slots; group-major:
+    // 64 slots apart (see the render kernel's decode)
+    const size_t px = (size_t)k * 64u + (size_t)q;
+    const size_t step = P.slot_order ? 192u : 3u;
+    const float* pa = P.partial + 3 * (P.slot_order ? (size_t)k * (size_t)P.n_big * 64u + (size_t)q : px * (size_t)P.n_big);
+#pragma unroll 2
+    for (int j = 0; j < P.n_big; ++j) acc = acc + ld3(pa + step * (size_t)j);
+    const float* pb = P.partial + 3 * ((size_t)P.slots_a + (P.slot_order ? (size_t)k * (size_t)P.tail_spp * 64u + (size_t)q
+                                                                       : px * (size_t)P.tail_spp));
+#pragma unroll 2
+    for (int t = 0; t < P.tail_spp; ++t) acc = acc + ld3(pb + step * (size_t)t);
     store3(out_at(b.x + qx, b.y + qy), acc * inv_spp);
   }
 }

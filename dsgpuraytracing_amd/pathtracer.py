@@ -150,6 +150,7 @@ class Device:
         check(self._lib.pt_get_stats(self.handle, ctypes.byref(s)))
         out = {k: getattr(s, k) for k, _ in native.pt_stats._fields_}
         out["section_clocks"] = list(s.section_clocks)
+        out["slot_latency_hist"] = list(s.slot_latency_hist)
         out["wave_span"] = list(s.wave_span)
         out["lane_iters"] = list(s.lane_iters)
         out["footprint"] = list(s.footprint)
@@ -167,13 +168,14 @@ class Device:
 
     def wave_trace(self) -> np.ndarray:
         """Per-wave records of the last stats launch (pt_get_wave_trace):
-        int64 (waves, 7) = start, first empty-queue time (-1: never), end,
+        int64 (waves, 11) = start, first empty-queue time (-1: never), end,
         (XCC id << 32 | HW_ID), camera samples started, sum and max of the
         work-slot latencies (wall-clock ticks, 100 MHz), per-ray maxima of
-        traversal iterations stepped (<< 32) | idle, and of traversal phases."""
+        traversal iterations stepped (<< 32) | idle, and of traversal phases,
+        traversal iterations and shading rounds after the queue drained."""
         n = ctypes.c_int64(0)
         check(self._lib.pt_get_wave_trace(self.handle, None, 0, ctypes.byref(n)))
-        buf = np.zeros((n.value, 9), np.int64)
+        buf = np.zeros((n.value, 11), np.int64)
         check(self._lib.pt_get_wave_trace(self.handle, buf.ctypes.data, buf.size, ctypes.byref(n)))
         return buf
 

@@ -222,6 +222,9 @@ typedef struct pt_stats {
                               empty rectangle (0, 0, -1, -1) when the box is entirely off-screen. */
   int32_t tail_spp;        /* of spp: samples per pixel in one-sample work slots handed out last (the
                               launch ends on short slots); the others are in groups of group_spp */
+  int64_t slot_latency_hist[32]; /* PT_FLAG_STATS: work slots by wall-clock latency (first camera ray to the
+                              group's store), bucket b = [2^(b-1), 2^b) microseconds (0: < 1 us, 15: the
+                              rest); [0..15] groups of group_spp samples, [16..31] one-sample tail slots */
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */
@@ -293,12 +296,14 @@ int pt_get_stats(pt_ctx* ctx, pt_stats* out);
  * application.cpp:776-780): the HIP-event view of the same launches. */
 int pt_get_launch_times(pt_ctx* ctx, float* kernel_ms, float* resolve_ms, int32_t cap, int32_t* n);
 /* Diagnostics (no reference counterpart): after a PT_FLAG_STATS launch, one
- * record of 9 int64 per wave -- device wall-clock start, first time the wave
+ * record of 11 int64 per wave -- device wall-clock start, first time the wave
  * found the work queue empty (~0 if never), end, (XCC id << 32 | HW_ID), the
  * camera samples it started, the sum and maximum of its work slots'
  * latencies (claim to partial-sum store, wall-clock ticks), the most
- * traversal iterations one ray stepped in (<< 32) | sat out, and the most
- * traversal phases one ray spanned.  out == NULL: only *n_waves is set. */
+ * traversal iterations one ray stepped in (<< 32) | sat out, the most
+ * traversal phases one ray spanned, and the traversal iterations and shading
+ * rounds it ran after it saw the queue drained.  out == NULL: only *n_waves
+ * is set. */
 int pt_get_wave_trace(pt_ctx* ctx, int64_t* out, int64_t cap, int64_t* n_waves);
 const char* pt_last_error(void);
 

@@ -825,6 +825,36 @@ int rs_render_strided(const char* scene_path, int w, int h, int spp, int max_dep
   return 0;
 }
 
+// Each sample's radiance of the listed pixels, counter RNG (raytrace_pixel's
+// loop, pathtracer.cpp:571-577, without the average): out[(k*spp + i)*3] is
+// sample i of pixel (xs[k], ys[k]).  For tools/silhouette_samples.py: which
+// samples of a pixel the HIP path and the restatement disagree on.
+int rs_pixel_samples(const char* scene_path, int w, int h, int spp, int max_depth, int ns_area_light,
+                     uint32_t seed, int n_px, const int32_t* xs, const int32_t* ys, float* out) {
+  rs::Scene S;
+  if (!rs::load_scene(scene_path, S)) return -1;
+  rs::Tracer tr(S);
+  tr.max_depth = max_depth;
+  tr.ns_area_light = ns_area_light;
+  rs::Rng rng;
+  rng.mode = 1;
+  for (int k = 0; k < n_px; ++k) {
+    const int x = xs[k], y = ys[k];
+    for (int i = 0; i < spp; i++) {
+      rng.start(seed, (uint32_t)(x + y * w), (uint32_t)i);
+      double ry = rng.next();
+      double rx = rng.next();
+      rs::Ray r = tr.generate_ray((x + rx) / w, (y + ry) / h);
+      rs::Spec s = tr.trace_ray(r, true, rng);
+      float* o = out + 3 * ((size_t)k * spp + i);
+      o[0] = s.r;
+      o[1] = s.g;
+      o[2] = s.b;
+    }
+  }
+  return 0;
+}
+
 // BVHAccel::intersect nearest (hit,t,prim,n) and any-hit under max_t (any).
 int rs_intersect(const char* scene_path, int64_t n, const double* o, const double* d,
                  const double* maxt, int32_t* hit, double* t, int32_t* prim, double* nrm,

@@ -36,6 +36,9 @@ class Restatement:
         self.lib.rs_render_strided.restype = ctypes.c_int
         self.lib.rs_intersect.argtypes = [ctypes.c_char_p, ctypes.c_int64] + [ctypes.c_void_p] * 8
         self.lib.rs_intersect.restype = ctypes.c_int
+        self.lib.rs_pixel_samples.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 5 + [ctypes.c_uint32, ctypes.c_int] + \
+            [ctypes.c_void_p] * 3
+        self.lib.rs_pixel_samples.restype = ctypes.c_int
         self.lib.rs_rng_draw.argtypes = [ctypes.c_uint32] * 4
         self.lib.rs_rng_draw.restype = ctypes.c_double
 
@@ -61,6 +64,17 @@ class Restatement:
         if rc != 0:
             raise RuntimeError(f"rs_render_strided failed on {scene_path}")
         return out, st, secs.value
+
+    def pixel_samples(self, scene_path, w, h, spp, xs, ys, depth=4, ns_area_light=1, seed=1):
+        """(len(xs), spp, 3) radiance of every sample of the listed pixels (counter RNG)."""
+        xs = np.ascontiguousarray(xs, np.int32)
+        ys = np.ascontiguousarray(ys, np.int32)
+        out = np.zeros((len(xs), spp, 3), np.float32)
+        rc = self.lib.rs_pixel_samples(scene_path.encode(), w, h, spp, depth, ns_area_light, seed, len(xs),
+                                       xs.ctypes.data, ys.ctypes.data, out.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"rs_pixel_samples failed on {scene_path}")
+        return out
 
     def intersect(self, scene_path, o, d, maxt):
         n = len(maxt)

@@ -76,7 +76,10 @@ def main():
     cu = (hw >> 8) & 0xF
     se = (hw >> 13) & 0x7
     q = [0, 0.01, 0.1, 0.5, 0.9, 0.99, 1.0]
-    out = {"kernel_ms": st["last_ms"], "waves": len(tr),
+    start = (tr[:, 0] - t0) * us
+    out = {"kernel_ms": st["last_ms"], "waves": len(tr), "group_spp": st["group_spp"], "tail_spp": st.get("tail_spp"),
+           "start_us_quantiles": [round(float(np.quantile(start, x)), 1) for x in q],
+           "late_starts": int((start > 100.0).sum()),
            "end_us_quantiles": [round(float(np.quantile(end, x)), 1) for x in q],
            "empty_us_quantiles": [round(float(np.nanquantile(emp, x)), 1) for x in q],
            "samples_per_wave_quantiles": [int(np.quantile(tr[:, 4], x)) for x in q],
@@ -85,7 +88,11 @@ def main():
            "ray_steps_max_quantiles": [int(np.quantile(tr[:, 7] >> 32, x)) for x in q],
            "ray_idle_max_quantiles": [int(np.quantile(tr[:, 7] & 0xFFFFFFFF, x)) for x in q],
            "ray_rounds_max_quantiles": [int(np.quantile(tr[:, 8], x)) for x in q],
-           "rounds_per_wave": st["wave_rounds"] / len(tr), "round_us": round(float(np.mean(end)) / (st["wave_rounds"] / len(tr)), 2)}
+           "rounds_per_wave": st["wave_rounds"] / len(tr), "round_us": round(float(np.mean(end)) / (st["wave_rounds"] / len(tr)), 2),
+           "drain_iters_per_wave_quantiles": [int(np.quantile(tr[:, 9], x)) for x in q],
+           "drain_rounds_per_wave_quantiles": [int(np.quantile(tr[:, 10], x)) for x in q],
+           "slot_latency_hist_log2us_groups": st["slot_latency_hist"][:16],
+           "slot_latency_hist_log2us_tail": st["slot_latency_hist"][16:]}
     print(json.dumps(out))
     for x in range(8):
         m = xcc == x
