@@ -465,7 +465,7 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
         frame[:y0].zero_()
         frame[y1 + 1:].zero_()
     # the ranks must group each pixel's samples alike (bit-identical frame)
-    knobs = check_value_knobs({"group_spp": st_perf["group_spp"], "tail_spp": st_perf["tail_spp"]})
+    knobs = check_value_knobs({"group_spp": st_perf["group_spp"]})
     for _ in range(args.warmup):
         step()
     guard.check()
@@ -576,7 +576,7 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
             "launch": {"grid_blocks": s_get(dev, "grid_blocks"), "block": 64,
                        "blocks_per_cu_query": s_get(dev, "blocks_per_cu"),
                        "bvh_nodes": s_get(dev, "bvh_nodes"), "bvh_stack": s_get(dev, "bvh_stack"),
-                       "group_spp": s_get(dev, "group_spp"), "tail_spp": s_get(dev, "tail_spp")},
+                       "group_spp": s_get(dev, "group_spp")},
             "image_mean": float(img.mean()),
         }
         rays = st_counts["camera_rays"] + st_counts["bounce_rays"] + st_counts["shadow_rays"]

@@ -144,6 +144,7 @@ struct pt_ctx {
   static constexpr int kRing = 256;
   hipEvent_t ev[kRing][3] = {};
   int64_t n_launches = 0;   // launches recorded so far (ring slot = index % kRing)
+  bool census_valid = false;  // the last launch was a PT_CENSUS plain launch (its trace area holds start/end/CU)
   bool times_pending = false;  // c->last's times belong to a launch not yet synchronised
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;  // the current launch's triple
   DevBuf<DNode> nodes;
@@ -930,17 +931,6 @@ static bool footprint_rect(const pt_ctx* c, int W, int H, int r[4]) {
   return true;
 }
 
-// Pixels whose camera rays can reach the scene in the default mode: the
-// footprint's area inside the frame, or the whole frame with an environment
-// light (misses see the map) or no footprint.  A property of the frame --
-// PT_NO_FOOTPRINT_CULL leaves it alone -- for the sample-group layout.
-static int64_t traced_px(const pt_ctx* c, int W, int H) {
-  int r[4];
-  if (c->env_w > 0 || !footprint_rect(c, W, H, r)) return (int64_t)W * H;
-  const int64_t w = std::min(W - 1, r[2]) - std::max(0, r[0]) + 1, h = std::min(H - 1, r[3]) - std::max(0, r[1]) + 1;
-  return std::max<int64_t>(0, w) * std::max<int64_t>(0, h);
-}
-
 // The culling rectangle: pixels outside [cull_x0, cull_x1] x [cull_y0,
 // cull_y1] see no geometry (not traced, resolved to 0).
 static void screen_footprint(const pt_ctx* c, KParams& P) {
@@ -958,53 +948,33 @@ static void screen_footprint(const pt_ctx* c, KParams& P) {
   P.cull_y1 = r[3];
 }
 
-// Sample groups of a pixel (KParams: n_big groups of group_spp samples, then
-// tail_spp one-sample groups).  The grouping decides the float summation
-// order of a pixel, so it is a function of the FRAME -- its size, spp, the
-// pixels its camera rays can trace -- and the device's resident grid only,
-// never of the launch's tile set or of a stats build: any split of a frame
-// into tile launches (raytrace_tile calls, the multi-GPU shards) sums every
-// pixel in the same order as the whole frame.
-//  * group_spp: 4 (C3 +3.3% over 2; 8 or more lose), halved for small frames
-//    until there are >= 16 work slots per resident lane (C1, C2: 1);
-//  * the tail: about PT_TAIL_SPL (default 12) samples per resident lane, in
-//    one-sample groups handed out after every big group, so a launch ends on
-//    short work slots instead of waiting for the last lanes' 4-sample groups
-//    (the drain: a lone C3 frame took 1.82 ms vs 1.34 ms pipelined).
-struct GroupLayout {
-  int gs, s_a, n_big, tail;
-};
-static GroupLayout group_layout(int64_t frame_px, int64_t traced, int spp, int64_t lanes, int64_t frame_blocks) {
-  GroupLayout L{PT_GROUP_SPP, 0, 0, 0};
-  while (L.gs > 1 && frame_px * ((spp + L.gs - 1) / L.gs) < lanes * 16) L.gs /= 2;
+// Sample groups of a pixel (KParams: n_groups groups of group_spp samples,
+// the last one possibly short).  The grouping decides the float summation
+// order of a pixel, so it is a function of the FRAME -- its size and spp --
+// and the device's resident grid only, never of the launch's tile set or of
+// a stats build: any split of a frame into tile launches (raytrace_tile
+// calls, the multi-GPU shards) sums every pixel in the same order as the
+// whole frame.  group_spp: 4 (C3 +3.3% over 2; 8 or more lose), halved for
+// small frames until there are >= 16 work slots per resident lane (C1, C2: 1).
+// (A tail of one-sample groups handed out last, to end the launch on short
+// work slots, measured -2% pipelined for +2% on a lone frame: DESIGN.md §4.)
+static int group_size(int64_t frame_px, int spp, int64_t lanes, int64_t frame_blocks) {
+  int gs = PT_GROUP_SPP;
+  while (gs > 1 && frame_px * ((spp + gs - 1) / gs) < lanes * 16) gs /= 2;
   if (const char* g = std::getenv("PT_SAMPLE_GROUP")) {  // tuning knob
     int v = std::atoi(g);
-    if (v > 0) L.gs = v;
+    if (v > 0) gs = v;
   }
-  L.gs = std::max(1, std::min(L.gs, spp));
-  int64_t tb = 0;
-  if (L.gs > 1) {
-    int64_t per_lane = 12;
-    if (const char* t = std::getenv("PT_TAIL_SPL")) per_lane = std::max(0, std::atoi(t));  // tuning knob
-    tb = (per_lane * lanes + std::max<int64_t>(traced, 1) - 1) / std::max<int64_t>(traced, 1);
-    tb = std::min<int64_t>((tb + 1) & ~(int64_t)1, spp);  // even: chunks stay inside one block
-  }
+  gs = std::max(1, std::min(gs, spp));
   for (;;) {
-    L.n_big = (int)((spp - tb) / L.gs);
-    if (L.n_big > 1 && (L.n_big & 1)) --L.n_big;  // even: chunks stay inside one block
-    L.s_a = L.n_big * L.gs;
-    L.tail = spp - L.s_a;
-    // 32-bit slot indices (the queue head may overshoot by one chunk per
-    // wave) and a group-sum budget of 4 GiB per render slot, for the whole
-    // frame's blocks (so every tile split gets the same layout)
-    const int64_t slots = frame_blocks * 64 * (L.n_big + L.tail);
-    if ((slots + lanes / 64 * PT_CHUNK_MAX < (int64_t)INT32_MAX && slots * 12 <= (4ll << 30)) ||
-        (L.gs >= spp && tb == 0))
-      break;
-    tb = 0;
-    L.gs = std::min(spp, L.gs * 2);
+    // 32-bit slot indices (they may overshoot by a static and a claimed
+    // chunk per wave) and a group-sum budget of 4 GiB per render slot, for the
+    // whole frame's blocks (so every tile split gets the same layout)
+    const int64_t slots = frame_blocks * 64 * ((spp + gs - 1) / gs);
+    if ((slots + 2 * (lanes / 64) * PT_CHUNK_MAX < (int64_t)INT32_MAX && slots * 12 <= (4ll << 30)) || gs >= spp) break;
+    gs = std::min(spp, gs * 2);
   }
-  return L;
+  return gs;
 }
 
 // One render: the render kernel on the slot's render stream, then the resolve
@@ -1100,8 +1070,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     int v = std::atoi(lw);
     if (v >= 1) P.leaf_weight = v;
   }
-  P.drain_both = 1;
-  if (const char* db = std::getenv("PT_DRAIN_BOTH")) P.drain_both = std::atoi(db) != 0;  // tuning knob
+  P.census = std::getenv("PT_CENSUS") && !stats ? 1 : 0;  // diagnostics (tools/wave_trace.py --census)
   P.drain_div = 0;
   if (const char* dd = std::getenv("PT_DRAIN_DIV")) {  // tuning knob
     int v = std::atoi(dd);
@@ -1166,19 +1135,13 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   const int64_t frame_px = (int64_t)P.W * P.H;
   const int64_t want_plain = std::getenv("PT_WAVES_PER_CU") ? want : c->grid_plain;
   const int64_t frame_blocks = (int64_t)((P.W + 7) / 8) * ((P.H + 7) / 8);
-  const GroupLayout L = group_layout(frame_px, traced_px(c, P.W, P.H), P.spp, want_plain * PT_BLOCK, frame_blocks);
-  P.group_spp = L.gs;
-  P.s_a = L.s_a;
-  P.n_big = L.n_big;
-  P.tail_spp = L.tail;
-  const int64_t slots = (int64_t)bl.size() * 64 * (L.n_big + L.tail);
-  if (slots + want * PT_CHUNK_MAX >= (int64_t)INT32_MAX) return fail(PT_E_INVALID, "frame too large for one launch");
-  P.slots_a = (uint32_t)((int64_t)bl.size() * 64 * L.n_big);
-  pt_fastdiv_init((uint32_t)std::max(1, L.n_big), &P.big_m, &P.big_sh);
-  pt_fastdiv_init((uint32_t)std::max(1, L.tail), &P.tail_m, &P.tail_sh);
-  P.sblocks = (L.n_big % 2 == 0 && L.tail % 2 == 0) ? 1 : 0;
-  P.slot_order = 0;  // which lane gets which (pixel, group): no effect on any value
-  if (const char* so = std::getenv("PT_SLOT_ORDER")) P.slot_order = std::atoi(so) != 0;  // tuning knob
+  P.group_spp = group_size(frame_px, P.spp, want_plain * PT_BLOCK, frame_blocks);
+  P.n_groups = (P.spp + P.group_spp - 1) / P.group_spp;
+  const int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
+  // (slot indices reach past the end by up to a static chunk plus a claimed one per wave)
+  if (slots + 2 * want * PT_CHUNK_MAX >= (int64_t)INT32_MAX) return fail(PT_E_INVALID, "frame too large for one launch");
+  pt_fastdiv_init((uint32_t)P.n_groups, &P.grp_m, &P.grp_sh);
+  P.sblocks = P.n_groups % 2 == 0 ? 1 : 0;
   // group sums: 12 B per work slot of THIS launch (a rank's share of a split
   // frame holds only its own blocks' sums)
   HIPCHK(c->partial[slot].reserve((size_t)std::max<int64_t>(slots, 1) * 3));
@@ -1192,7 +1155,8 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.group_shift = log2_exact(P.group_spp);
   int64_t max_grid = std::max<int64_t>(1, (slots + PT_BLOCK - 1) / PT_BLOCK);
   int grid = (int)std::min<int64_t>(want, max_grid);
-  if (stats && (size_t)grid * PT_WAVE_TRACE + PT_STATS_SLOTS > c->stats.n) grid = (int)((c->stats.n - PT_STATS_SLOTS) / PT_WAVE_TRACE);
+  if ((stats || P.census) && (size_t)grid * PT_WAVE_TRACE + PT_STATS_SLOTS > c->stats.n)
+    grid = (int)((c->stats.n - PT_STATS_SLOTS) / PT_WAVE_TRACE);
   grid = std::max(1, grid);
   P.stack_spill = nullptr;
   if (c->bvh_stack > PT_STACK) {  // worst-case depth beyond the LDS stack
@@ -1213,9 +1177,9 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   HIPCHK(ptk_launch_resolve(&P, s));
   HIPCHK(hipEventRecord(c->ev2, s));
   HIPCHK(hipEventRecord(c->ev_free[slot], s));
+  c->census_valid = P.census != 0;
   c->last.grid_blocks = grid;
   c->last.group_spp = P.group_spp;
-  c->last.tail_spp = P.tail_spp;
   c->last.blocks_per_cu = (int32_t)(want / std::max(1, c->n_cu));
   int64_t px = 0;
   for (const int4& t : tl) px += (int64_t)t.z * t.w;
@@ -1620,7 +1584,8 @@ int pt_get_launch_times(pt_ctx* c, float* kernel_ms, float* resolve_ms, int32_t 
 
 int pt_get_wave_trace(pt_ctx* c, int64_t* out, int64_t cap, int64_t* n_waves) {
   if (!c || !n_waves) return fail(PT_E_INVALID, "pt_get_wave_trace: NULL argument");
-  if (!c->last.counters_valid) return fail(PT_E_INVALID, "pt_get_wave_trace: the last launch had no counters");
+  if (!c->last.counters_valid && !c->census_valid)
+    return fail(PT_E_INVALID, "pt_get_wave_trace: the last launch had no counters (or census)");
   const int64_t n = c->last.grid_blocks;
   *n_waves = n;
   if (!out) return PT_OK;

@@ -120,24 +120,16 @@ struct KParams {
   int n_bsdfs;
   int n_tiles;     // 32x32 (or smaller) tiles: 1024 pixels each
   // Sample groups (work slots) of a pixel, a function of the frame only
-  // (launch(): pt_api.cpp group_layout): samples [0, s_a) in n_big groups of
-  // group_spp, then tail_spp one-sample groups [s_a, spp).  The queue hands
-  // out every pixel's big groups first (phase A) and the one-sample groups
-  // last (phase B), so the launch ends on short work slots.
-  int group_spp;   // samples per phase-A slot
+  // (launch(): pt_api.cpp group_layout): group j holds samples
+  // [j * group_spp, min((j + 1) * group_spp, spp)).
+  int group_spp;   // samples per work slot
   int group_shift;   // log2(group_spp) when a power of two, else -1 (shifts instead of divisions)
-  int s_a;         // samples in phase-A groups (n_big * group_spp)
-  int n_big;       // phase-A groups per pixel
-  int tail_spp;    // phase-B (one-sample) groups per pixel
-  // Work slot / group-sum index of (block b, group j, pixel q of the 8x8
-  // block): phase A -> (b * 64 + q) * n_big + j (pixel-major, default) or
-  // (b * n_big + j) * 64 + q (group-major); phase B (tail sample t) ->
-  // slots_a + the same with tail_spp.  Divisions by fastdiv (pt_fastdiv).
-  uint32_t slots_a;                 // phase-A slots: n_blocks * 64 * n_big
-  uint32_t big_m, big_sh;           // fastdiv by n_big
-  uint32_t tail_m, tail_sh;         // fastdiv by tail_spp
-  int sblocks;                      // a 128-slot chunk lies in one block (n_big, tail_spp even): scalar block loads
-  int slot_order;                   // 0: pixel-major slots (b*64 + q)*n + j; 1: group-major (b*n + j)*64 + q
+  int n_groups;    // ceil(spp / group_spp): work slots per pixel
+  // Work slot / group-sum index of (block b, pixel q of the 8x8 block, group
+  // j): (b * 64 + q) * n_groups + j -- a pixel's groups are consecutive, so a
+  // wave's lanes hold a few pixels' groups (coherent camera rays).
+  uint32_t grp_m, grp_sh;           // fastdiv by n_groups (pt_fastdiv)
+  int sblocks;                      // a 128-slot chunk lies in one block (n_groups even): scalar block loads
   const int* tile_block0;           // first block of each tile (n_tiles + 1 entries), for the resolve
   const DNode* nodes;
   const DNode2* nodes2;  // the binary tree (reference-count launch only)
@@ -165,7 +157,7 @@ struct KParams {
   int shade_batch;            // leave the traversal phase once this many lanes finished their ray
   int leaf_weight;            // leaf steps run when leaf_weight * leaf lanes >= 16 * node lanes
   int drain_div;              // queue drained: shade once alive/drain_div lanes are ready (0: 3/4 rule)
-  int drain_both;             // queue drained: node and leaf steps in every traversal iteration
+  int census;                 // plain build: record each wave's start / end / CU in the trace area (PT_CENSUS)
   float root_lo[3], root_hi[3];  // scene bounds (root box, rounded outward)
   int cull_x0, cull_y0, cull_x1, cull_y1;  // pixels outside [x0,x1]x[y0,y1] see no geometry
 };

@@ -539,6 +539,9 @@ __device__ __forceinline__ float3 env_dir(const KP& P, float3 d) {
 // entries either side of the window, so the caller's interpolation pair
 // (prev = a[t-1] or 0, cur = a[t]) comes from registers, not from two more
 // dependent loads.
+#ifndef PT_ENV_PAIR
+#define PT_ENV_PAIR 1
+#endif
 __device__ __forceinline__ int guided_lower_bound(const float* __restrict__ a, float v, float r,
                                                   const int* __restrict__ g, int G, float& prev, float& cur) {
   const int k = min(G - 1, max(0, (int)(r * (float)G)));
@@ -554,6 +557,7 @@ __device__ __forceinline__ int guided_lower_bound(const float* __restrict__ a, f
       n = half;
     }
   }
+#if PT_ENV_PAIR
   // w_i = a[min(lo + i, hi)]: entries past the window read a[hi] >= v, which
   // never counts; w4 = a[hi] is a[t] when all four candidates are < v
   const float wm = lo > 0 ? a[lo - 1] : 0.0f;
@@ -563,6 +567,15 @@ __device__ __forceinline__ int guided_lower_bound(const float* __restrict__ a, f
   cur = c == 0 ? w0 : c == 1 ? w1 : c == 2 ? w2 : c == 3 ? w3 : w4;
   prev = c == 0 ? wm : c == 1 ? w0 : c == 2 ? w1 : c == 3 ? w2 : w3;
   return lo + c;
+#else
+  const float kBig = 3.0e38f;
+  const float w0 = n > 0 ? a[lo] : kBig, w1 = n > 1 ? a[lo + 1] : kBig;
+  const float w2 = n > 2 ? a[lo + 2] : kBig, w3 = n > 3 ? a[lo + 3] : kBig;
+  const int t = lo + (int)(w0 < v) + (int)(w1 < v) + (int)(w2 < v) + (int)(w3 < v);
+  prev = t > 0 ? a[t - 1] : 0.0f;
+  cur = a[t];
+  return t;
+#endif
 }
 
 // importanceSampling (69-115): inverse CDF over rows (pTheta), then within the
@@ -595,10 +608,15 @@ enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 // What follows a lane's shadow ray (the `shadow` state; 0 = not a shadow ray).
 enum : int { SH_RESUME = 1, SH_FOLLOW = 2, SH_STORE = 3, SH_STORE_FOLLOW = 4 };
 // Launch parameters re-read per round (see render_kernel): on for the
-// environment-light build (C5 +6.8%, no VGPR spills instead of 8), off for the
-// common one (C3 -1.1%, C4 +0.6%: profiles/r3/ab_kernarg_round.txt).
+// environment-light build since round 3 (C5 +6.8%, no VGPR spills instead of
+// 8) and for the common one since round 4 (C3 +0.9%, 71 SGPR spills to VGPR
+// lanes removed; it measured C3 -1.1% on the round-3 kernel:
+// profiles/r3/ab_kernarg_round.txt, profiles/r4/ab_layout.txt).
 #ifndef PT_KARG_ROUND
-#define PT_KARG_ROUND PT_ENV_TU
+#define PT_KARG_ROUND 1
+#endif
+#ifndef PT_STATIC_FIRST
+#define PT_STATIC_FIRST 1
 #endif
 
 // Wave-clock sections of the STATS build: every shader clock of a wave's
@@ -662,8 +680,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // account the wave's time whichever lanes took the branch.
   __shared__ unsigned long long s_clk[STATS ? S_N + 1 : 1];
   if (STATS && lane <= S_N) s_clk[lane] = lane == S_N ? clock64() : 0ull;
-  // STATS: work-slot latency histograms (log2 of microseconds, 16 buckets),
-  // phase-A slots then phase-B (one-sample) slots
+  // STATS: work-slot latency histogram (log2 of microseconds, 32 buckets)
   __shared__ uint32_t s_hist[STATS ? 32 : 1];
   if (STATS && lane < 32) s_hist[lane] = 0u;
   __syncthreads();
@@ -736,7 +753,17 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   uint32_t n_titer_drain = 0, n_rounds_drain = 0;  // of them: after this wave found the queue empty
   uint32_t chunk_next = 0, chunk_end = 0;  // the wave's private range of work slots
   uint32_t seen = 0;                       // queue head after this wave's last claim
+  bool first_claim = true;                 // the first chunk is the wave's own (no atomic)
   const unsigned long long w_start = STATS ? wall_clock64() : 0ull;
+  // Residency census of the plain build (PT_CENSUS=1, diagnostics): when
+  // each wave started and ended, and where it ran -- which waves of the grid
+  // were resident from the start.
+  unsigned long long* const census = (!STATS && P.census) ? P.stats + PT_STATS_SLOTS + PT_WAVE_TRACE * (size_t)wave_id : nullptr;
+  if (census && lane == 0) {
+    census[0] = wall_clock64();
+    census[3] = ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32) |
+                (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+  }
   unsigned long long w_empty = 0ull;  // when this wave first found the queue empty
   unsigned long long slot_t0 = 0ull, slot_lat_sum = 0ull, slot_lat_max = 0ull;  // work-slot latency (wall ticks)
   // per ray: traversal iterations it stepped in / sat out, traversal phases it spanned
@@ -747,20 +774,19 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     slot_lat_sum += d_;                                                         \
     slot_lat_max = d_ > slot_lat_max ? d_ : slot_lat_max;                       \
     const uint32_t us_ = (uint32_t)min(d_ / 100ull, 0xffffffffull);            \
-    const uint32_t b_ = us_ == 0u ? 0u : min(15u, 32u - (uint32_t)__clz(us_)); \
-    atomicAdd(&s_hist[b_ + (myslot >= P.slots_a ? 16u : 0u)], 1u);              \
+    const uint32_t b_ = us_ == 0u ? 0u : min(31u, 32u - (uint32_t)__clz(us_)); \
+    atomicAdd(&s_hist[b_], 1u);                                                 \
   }
 
-  // the lane's group ends before sample s: the last phase-A group ends at
-  // s_a, every phase-B group after one sample (a shift when group_spp is a
-  // power of two, the usual case; wave-uniform branch)
+  // the lane's group ends before sample s (a shift when group_spp is a power
+  // of two, the usual case; wave-uniform branch; the last group may be short)
   auto group_ends = [&](int s) -> bool {
-    return s >= P.s_a || (P.group_shift >= 0 ? (s & (P.group_spp - 1)) == 0 : s % P.group_spp == 0);
+    return s >= P.spp || (P.group_shift >= 0 ? (s & (P.group_spp - 1)) == 0 : s % P.group_spp == 0);
   };
   // the pixel index from the packed coordinates: one multiply-add, no
   // division per camera ray
   auto pix_index = [&](int p) -> int { return (p & 0xffff) + (int)((uint32_t)p >> 16) * P.W; };
-  const uint32_t total_slots = P.slots_a + (uint32_t)P.n_blocks * 64u * (uint32_t)P.tail_spp;
+  const uint32_t total_slots = (uint32_t)P.n_blocks * 64u * (uint32_t)P.n_groups;
   const int batch = P.shade_batch;
   // Camera::generate_ray (camera.cpp:113-129) for the lane's pixel and
   // current sample, at the jittered position of raytrace_pixel
@@ -1090,44 +1116,35 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             // the XCDs far from its channel) stalled every round of the
             // remaining paths (C3: the XCDs' median drain 380 vs 680 us).
             nbase = total_slots;
+          } else if (PT_STATIC_FIRST && first_claim) {
+            // The wave's first chunk is dealt statically (chunk wave_id): at
+            // the launch's start every wave would otherwise queue on the one
+            // head at once (memory-side atomics, serialised), and the last
+            // ones would wait for thousands of others before their first ray.
+            csize = PT_CHUNK_MAX;
+            nbase = wave_id * (uint32_t)PT_CHUNK_MAX;
+            seen = nbase + csize;
+            first_claim = false;
           } else {
             const uint32_t left = total_slots - seen;
             csize = min((uint32_t)PT_CHUNK_MAX, max((uint32_t)PT_CHUNK, left / (PT_CHUNK_DIV * n_waves))) & ~63u;
             if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
-            nbase = __builtin_amdgcn_readfirstlane(__shfl(nbase, 0));  // wave-uniform: an SGPR
+            // (the head counts the chunks after the statically dealt ones)
+            nbase = __builtin_amdgcn_readfirstlane(__shfl(nbase, 0)) + (PT_STATIC_FIRST ? n_waves * (uint32_t)PT_CHUNK_MAX : 0u);
             seen = nbase + csize;
             if (STATS) n_atomics += lane == 0;
           }
         }
-        // Work slots -> (block k, group j, pixel q): see KParams.  Pixel-
-        // major (slot_order 0): a pixel's groups are consecutive slots, so a
-        // wave's lanes hold a few pixels' groups (coherent camera rays);
-        // group-major (1): a unit of 64 slots is one group of the block's 64
-        // pixels.  Either way the divisions are fastdivs.
+        // Work slots -> (block k, pixel q, group j): see KParams (a fastdiv)
         auto decode = [&](uint32_t slot, uint32_t& k, uint32_t& j, uint32_t& q) {
-          const bool tl = slot >= P.slots_a;
-          const uint32_t local = slot - (tl ? P.slots_a : 0u);
-          const uint32_t n = (uint32_t)(tl ? P.tail_spp : P.n_big);
-          const uint32_t dm = tl ? P.tail_m : P.big_m, dsh = tl ? P.tail_sh : P.big_sh;
-          if (P.slot_order) {
-            const uint32_t u = local >> 6;
-            k = pt_fastdiv(u, dm, dsh);
-            j = u - k * n;
-            q = local & 63u;
-          } else {
-            const uint32_t px = pt_fastdiv(local, dm, dsh);
-            j = local - px * n;
-            k = px >> 6;
-            q = px & 63u;
-          }
+          const uint32_t px = pt_fastdiv(slot, P.grp_m, P.grp_sh);
+          j = slot - px * (uint32_t)P.n_groups;
+          k = px >> 6;
+          q = px & 63u;
         };
-        auto block_of = [&](uint32_t slot) -> uint32_t {
-          uint32_t k, j, q;
-          decode(slot, k, j, q);
-          return k;
-        };
-        // A chunk of 128 slots (128-aligned) lies inside one block when both
-        // phases hold an even number of groups per pixel, and the lanes are
+        auto block_of = [&](uint32_t slot) -> uint32_t { return pt_fastdiv(slot, P.grp_m, P.grp_sh) >> 6; };
+        // A chunk of 128 slots (128-aligned) lies inside one block when a
+        // pixel has an even number of groups, and the lanes are
         // served from at most two chunks -- the rest of the old one and the
         // new one: both block records are read through the scalar cache
         // (wave-uniform addresses) instead of one vector-memory load per lane,
@@ -1160,7 +1177,6 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             // Blocks are <= 8x8 pixel rectangles of the tiles, clipped to the
             // scene's screen footprint (pixels outside are written 0 by
             // resolve_kernel: every ray through them misses the root box).
-            const bool tl = slot >= P.slots_a;
             uint32_t k, j, q;
             decode(slot, k, j, q);  // (the scalar path's k is the same)
             int4 b;  // (odd group counts: one vector-memory load per lane)
@@ -1169,7 +1185,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             const int qx = (int)(q & 7u), qy = (int)(q >> 3);
             if (qx < b.z && qy < b.w) {
               pix = (b.x + qx) | ((b.y + qy) << 16);
-              sample = tl ? P.s_a + (int)j : (int)j * P.group_spp;
+              sample = (int)j * P.group_spp;
               myslot = slot;
               if (!shadow) acc = f3(0, 0, 0);
               else ng = f3(0, 0, 0);  // (SH_STORE: acc holds the last group's total until its store)
@@ -1245,16 +1261,13 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     // lanes have finished their ray, so finished lanes are refilled together
     // (coherent shading) while the others keep their traversal state.
     if (__ballot(mode == M_TRAV) == 0ull) break;  // every lane is M_DONE
-    // The traversal loop's launch parameters, read once per phase: with the
-    // parameters re-read per round (PT_KARG_ROUND) the compiler would
-    // otherwise re-issue their scalar loads -- and wait for them -- in every
-    // iteration; out of an empty asm they are opaque values it keeps in SGPRs.
+    // (Pinning the loop's parameters in SGPRs for the phase through an empty
+    // asm -- so the re-read parameters are not re-loaded per iteration --
+    // measured C5 -2.5%, C3 -3%: the scalar loads hide behind the node
+    // step's vector loads; profiles/r4/ab_layout.txt)
     const DNode* t_nodes = P.nodes;
     const DPrim* t_prims = P.prims;
-    int t_leaf_weight = P.leaf_weight, t_both = P.drain_both;
-#if PT_KARG_ROUND
-    asm volatile("" : "+s"(t_nodes), "+s"(t_prims), "+s"(t_leaf_weight), "+s"(t_both));
-#endif
+    const int t_leaf_weight = P.leaf_weight;
     // Fresh rays (node 0: references only point forward, so no ray returns
     // to the root) take their root step here, all together, from the LDS
     // copy: the wave's first traversal iteration no longer waits on a global
@@ -1288,30 +1301,26 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       const int n_node = __popcll(__ballot(trav && !at_leaf));
       bool done = false;
       const bool leaf_iter = n_leaf > 0 && (n_node == 0 || n_leaf * t_leaf_weight >= n_node * 16);
-      // Once the queue is drained, the wave's last rays are its critical
-      // path and the SIMD has issue slots to spare: every lane steps in every
-      // iteration (leaf lanes, then node lanes) instead of waiting through
-      // the other kind's iterations.
-      const bool both = t_both && seen >= total_slots;  // (wave-uniform)
-      const bool do_leaf = both ? n_leaf > 0 : leaf_iter;
-      const bool do_node = both ? n_node > 0 : !leaf_iter;
       if (STATS && trav) {
-        const bool stepped = both || leaf_iter == at_leaf;
+        const bool stepped = leaf_iter == at_leaf;
         r_steps += stepped;
         r_idle += !stepped;
       }
       if (STATS) {  // what each lane does in this iteration (SIMD efficiency)
-        l_other += trav && !both && leaf_iter != at_leaf;
+        l_other += trav && leaf_iter != at_leaf;
         l_ready += mode == M_SHADE;
         l_dead += mode == M_DONE;
-        l_leaf += at_leaf && do_leaf;
+        l_leaf += at_leaf && leaf_iter;
         l_deep += trav && tr.sp > PT_STACK;
       }
-      if (do_leaf) {
+      // (if / else-if: two independent ifs -- a leaf-step block and a
+      // node-step block, as a both-kinds drain mode needs -- measured C3 -2%,
+      // and stepping both kinds once the queue is drained did not win it back:
+      // profiles/r4/ab_bisect_2.txt)
+      if (leaf_iter) {
         if (at_leaf) done = leaf_step<STATS>(t_prims, stk, tr, ct);
         if (STATS) n_leafit += lane == 0;
-      }
-      if (do_node && trav && !at_leaf) {
+      } else if (trav && !at_leaf) {
         if constexpr (BIN) done = node_step2<STATS>(P.nodes2, stk, tr, ct);
         else done = node_step<STATS>(t_nodes, stk, tr, ct);
       }
@@ -1330,6 +1339,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     PT_STAMP(S_TRAV);
   }
 
+  if (census && lane == 0) census[2] = wall_clock64();
   if (STATS) {
     PT_STAMP(S_OTHER);
     unsigned long long v[11] = {n_cam, n_bounce, n_shadow, ct.nodes, ct.tris, ct.spheres, n_hits,
@@ -1408,13 +1418,13 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
 #endif
 
 #if !PT_ENV_TU  // (pt_kernels_env.hip emits only the ENV render kernels)
-// Sums each pixel's sample groups in group order (phase-A groups, then the
-// phase-B one-sample groups), so the sum is a fixed function of the pixel,
-// independent of scheduling and of the tile -> GPU assignment, and writes the
-// pixel's average, SampleBuffer-style (pathtracer.cpp:577-581).  One
-// workgroup per tile: the tile's pixels outside the scene's screen footprint
-// are written 0; then its blocks, four at a time, one lane per pixel: the 64
-// lanes of a block read each group's 64 sums as one contiguous 768-B run.
+// Sums each pixel's sample groups in group order, so the sum is a fixed
+// function of the pixel, independent of scheduling and of the tile -> GPU
+// assignment, and writes the pixel's average, SampleBuffer-style
+// (pathtracer.cpp:577-581).  One workgroup per tile: the tile's pixels outside
+// the scene's screen footprint are written 0; then its blocks, four at a time,
+// one lane per pixel: a block's 64 pixels' group sums are one contiguous run
+// of 64 * n_groups * 12 B (pixel-major).
 __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
   const int ti = (int)blockIdx.x;
   const int4 tile = P.tiles[ti];
@@ -1435,17 +1445,9 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
     const int4 b = P.blocks[k];
     if (qx >= b.z || qy >= b.w) continue;
     float3 acc = f3(0, 0, 0);
-    // pixel-major: the pixel's groups are consecutive slots; group-major:
-    // 64 slots apart (see the render kernel's decode)
-    const size_t px = (size_t)k * 64u + (size_t)q;
-    const size_t step = P.slot_order ? 192u : 3u;
-    const float* pa = P.partial + 3 * (P.slot_order ? (size_t)k * (size_t)P.n_big * 64u + (size_t)q : px * (size_t)P.n_big);
+    const float* pa = P.partial + 3 * ((size_t)k * 64u + (size_t)q) * (size_t)P.n_groups;
 #pragma unroll 2
-    for (int j = 0; j < P.n_big; ++j) acc = acc + ld3(pa + step * (size_t)j);
-    const float* pb = P.partial + 3 * ((size_t)P.slots_a + (P.slot_order ? (size_t)k * (size_t)P.tail_spp * 64u + (size_t)q
-                                                                       : px * (size_t)P.tail_spp));
-#pragma unroll 2
-    for (int t = 0; t < P.tail_spp; ++t) acc = acc + ld3(pb + step * (size_t)t);
+    for (int j = 0; j < P.n_groups; ++j) acc = acc + ld3(pa + 3 * (size_t)j);
     store3(out_at(b.x + qx, b.y + qy), acc * inv_spp);
   }
 }

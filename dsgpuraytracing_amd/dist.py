@@ -150,14 +150,12 @@ def render_sharded(render_packed: Callable[[List[Tile], object], None], frame, t
 
 
 # Environment knobs of libptgpu.so that change pixel VALUES (not only speed):
-# the sample grouping fixes each pixel's float summation order, the render
-# tree decides ties between equidistant primitives.  Ranks that disagree on
-# them would assemble a frame that is not the 1-GPU frame bit for bit.
-# Environment settings that change pixel values or a pixel's float summation
-# order: the sample grouping (group size, the one-sample tail, the resident
-# grid it is sized by, the footprint it is sized over), the render tree
-# (its tie-breaks between primitives at equal distance) and the library.
-VALUE_KNOBS = ("PT_SAMPLE_GROUP", "PT_TAIL_SPL", "PT_WAVES_PER_CU", "PT_NO_FOOTPRINT_CULL", "PT_BVH_BUILD",
+# the sample grouping (group size, the resident grid it is sized by) fixes
+# each pixel's float summation order, the render tree (its tie-breaks between
+# equidistant primitives) and the footprint cull decide values, and so does
+# the library.  Ranks that disagree on them would assemble a frame that is not
+# the 1-GPU frame bit for bit.
+VALUE_KNOBS = ("PT_SAMPLE_GROUP", "PT_WAVES_PER_CU", "PT_NO_FOOTPRINT_CULL", "PT_BVH_BUILD",
                "PT_COLLAPSE", "PT_LBVH_PASSES", "PT_LBVH_CI", "PT_LBVH_MAXLEAF", "PT_SAH_BINS", "PT_SAH_CI",
                "PT_SAH_LEAF", "PT_LIB")
 DEFAULT_TIMEOUT_S = 120

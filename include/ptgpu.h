@@ -212,7 +212,7 @@ typedef struct pt_stats {
   int64_t deep_stack_steps; /* traversal lane-steps taken while the ray's stack held entries beyond the
                               PT_STACK (24) kept in LDS, i.e. in the global spill area */
   int64_t partial_bytes;   /* device bytes of the sample-group sums of the last launch: 12 B per work slot
-                              of its own blocks (pixels * (spp/group_spp + tail_spp) * 12 at most; a rank
+                              of its own blocks (pixels * ceil(spp/group_spp) * 12 at most; a rank
                               rendering 1/N of a frame's tiles holds 1/N of them; two render slots
                               pipeline renders) */
   int32_t footprint[4];    /* the scene's screen footprint of the last launch, x0, y0, x1, y1 inclusive and
@@ -220,11 +220,9 @@ typedef struct pt_stats {
                               (its camera ray misses the scene box; not traced).  The whole frame when
                               culling is off (environment light, camera not in front of the box); the
                               empty rectangle (0, 0, -1, -1) when the box is entirely off-screen. */
-  int32_t tail_spp;        /* of spp: samples per pixel in one-sample work slots handed out last (the
-                              launch ends on short slots); the others are in groups of group_spp */
   int64_t slot_latency_hist[32]; /* PT_FLAG_STATS: work slots by wall-clock latency (first camera ray to the
-                              group's store), bucket b = [2^(b-1), 2^b) microseconds (0: < 1 us, 15: the
-                              rest); [0..15] groups of group_spp samples, [16..31] one-sample tail slots */
+                              group's store), bucket b = [2^(b-1), 2^b) microseconds (0: < 1 us, 31: the
+                              rest) */
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */

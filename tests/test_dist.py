@@ -162,13 +162,14 @@ def _knob_worker(rank, world, port, out_dir, knob="PT_SAMPLE_GROUP", value="8"):
     sys.exit(code)
 
 
-@pytest.mark.parametrize("knob,value", [("PT_SAMPLE_GROUP", "8"), ("PT_TAIL_SPL", "4"), ("PT_SAH_BINS", "64"),
+@pytest.mark.parametrize("knob,value", [("PT_SAMPLE_GROUP", "8"), ("PT_WAVES_PER_CU", "12"), ("PT_SAH_BINS", "64"),
                                         ("PT_SAH_CI", "1.5"), ("PT_SAH_LEAF", "2"), ("PT_NO_FOOTPRINT_CULL", "1")])
 def test_value_knobs_must_agree(tmp_path, knob, value):
-    """PT_SAMPLE_GROUP / PT_TAIL_SPL change each pixel's float summation order
-    (so does PT_NO_FOOTPRINT_CULL's traced set), the PT_SAH_* knobs the host
-    SAH tree and so its tie-breaks: ranks that differ would break the
-    bit-identity of the assembled frame, so the split refuses to start."""
+    """PT_SAMPLE_GROUP / PT_WAVES_PER_CU change each pixel's float summation
+    order (the group size), the PT_SAH_* knobs the host SAH tree and so its
+    tie-breaks, PT_NO_FOOTPRINT_CULL which pixels are traced: ranks that
+    differ could break the bit-identity of the assembled frame, so the split
+    refuses to start."""
     ctx = mp.get_context("spawn")
     port = _free_port()
     ps = [ctx.Process(target=_knob_worker, args=(r, 2, port, str(tmp_path), knob, value)) for r in range(2)]

@@ -4,7 +4,7 @@
 # over `bench.py --workload <wl>` with PT_PIPELINE=0 (every launch alone), then
 # the render kernel's per-launch averages per arm (tools/pmc_valu_summary.py).
 # An arm is "name=lib.so" or "name=lib.so,VAR=v,VAR2=v".
-# Usage: tools/pmc_valu.sh <workload> r3=_variants/r3.so new=_variants/new.so,PT_TAIL_SPL=0
+# Usage: tools/pmc_valu.sh <workload> r3=_variants/r3.so new=_variants/new.so,PT_SAMPLE_GROUP=8
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 WL=$1; shift

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--out", default=None)
     ap.add_argument("--share", type=int, default=0, help="N: rank 0's share of an N-GPU split (packed output)")
+    ap.add_argument("--census", action="store_true",
+                    help="the PLAIN build's residency instead (PT_CENSUS=1): wave starts/ends per CU, no counters")
     args = ap.parse_args()
     import torch
 
@@ -60,6 +62,28 @@ def main():
         ex = TileExchange(tile_fifo(w, h), w, h, 0, args.share, frame.device)
         tiles = np.asarray(ex.mine, np.int32)
         out_ptr, packed = ex.packed.data_ptr(), True
+    if args.census:
+        os.environ["PT_CENSUS"] = "1"
+        for _ in range(3):  # lone launches: each synchronised before the next
+            dev.render_tiles_device(tiles, out_ptr, stream, packed=packed)
+            torch.cuda.synchronize()
+        tr = dev.wave_trace()
+        t0 = tr[:, 0].min()
+        start = (tr[:, 0] - t0) * 0.01
+        end = (tr[:, 2] - t0) * 0.01
+        xcc = (tr[:, 3] >> 32) & 0xF
+        hw = tr[:, 3] & 0xFFFFFFFF
+        cu_key = xcc * 256 + ((hw >> 8) & 0xFF)  # XCC, then HW_ID's CU / SH / SE fields
+        early = start < 100.0
+        per_cu = np.bincount(np.unique(cu_key[early], return_inverse=True)[1])
+        q = [0, 0.01, 0.1, 0.5, 0.9, 0.99, 1.0]
+        print(json.dumps({"census": True, "waves": len(tr), "kernel_ms": dev.launch_times(1)[0][0].item(),
+                          "start_us_quantiles": [round(float(np.quantile(start, x)), 1) for x in q],
+                          "end_us_quantiles": [round(float(np.quantile(end, x)), 1) for x in q],
+                          "late_starts": int((~early).sum()), "cus_seen": int(len(np.unique(cu_key))),
+                          "early_waves_per_cu_min_max": [int(per_cu.min()), int(per_cu.max())],
+                          "early_waves_per_cu_hist": np.bincount(per_cu).tolist()}))
+        return
     for _ in range(2):
         dev.render_tiles_device(tiles, out_ptr, stream, stats=True, packed=packed)
     torch.cuda.synchronize()
@@ -77,7 +101,7 @@ def main():
     se = (hw >> 13) & 0x7
     q = [0, 0.01, 0.1, 0.5, 0.9, 0.99, 1.0]
     start = (tr[:, 0] - t0) * us
-    out = {"kernel_ms": st["last_ms"], "waves": len(tr), "group_spp": st["group_spp"], "tail_spp": st.get("tail_spp"),
+    out = {"kernel_ms": st["last_ms"], "waves": len(tr), "group_spp": st["group_spp"],
            "start_us_quantiles": [round(float(np.quantile(start, x)), 1) for x in q],
            "late_starts": int((start > 100.0).sum()),
            "end_us_quantiles": [round(float(np.quantile(end, x)), 1) for x in q],
@@ -91,8 +115,7 @@ def main():
            "rounds_per_wave": st["wave_rounds"] / len(tr), "round_us": round(float(np.mean(end)) / (st["wave_rounds"] / len(tr)), 2),
            "drain_iters_per_wave_quantiles": [int(np.quantile(tr[:, 9], x)) for x in q],
            "drain_rounds_per_wave_quantiles": [int(np.quantile(tr[:, 10], x)) for x in q],
-           "slot_latency_hist_log2us_groups": st["slot_latency_hist"][:16],
-           "slot_latency_hist_log2us_tail": st["slot_latency_hist"][16:]}
+           "slot_latency_hist_log2us": st["slot_latency_hist"]}
     print(json.dumps(out))
     for x in range(8):
         m = xcc == x
