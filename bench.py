@@ -643,7 +643,8 @@ def strong_companions(local, rank, world, backend, StepGuard, TileExchange, fram
         xev = []
 
         def step(timed=False):
-            guard.run(dev.render_tiles_device, mine, ex.packed.data_ptr(), stream, packed=True)
+            guard.run(dev.render_tiles_device, mine, ex.packed.data_ptr(), stream, packed=True,
+                      out_floats=ex.packed.numel())
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
             ex.exchange(frame)
@@ -670,7 +671,8 @@ def strong_companions(local, rank, world, backend, StepGuard, TileExchange, fram
         # the efficiency inputs of the tile-sharded curve: each rank's render
         # (HIP events) and gather times, its pixels and group-sum bytes
         k_ms, _ = dev.launch_times(frames)
-        dev.render_tiles_device(mine, ex.packed.data_ptr(), stream, stats=True)
+        dev.render_tiles_device(mine, ex.packed.data_ptr(), stream, stats=True, packed=True,
+                                out_floats=ex.packed.numel())
         st = dev.stats()
         mine_v = torch.tensor([float(np.mean(k_ms)), float(np.mean([a.elapsed_time(b) for a, b in xev])),
                                float(np.sum(mine[:, 2] * mine[:, 3])), float(st["partial_bytes"])],

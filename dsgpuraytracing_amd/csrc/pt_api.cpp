@@ -85,6 +85,7 @@ struct EnvTables {
   std::vector<float4> tex;
   std::vector<float> p_theta, p_phi, p_theta_phi;
   std::vector<int> g_theta, g_phi;  // guide tables (PT_ENV_GUIDE buckets)
+  std::vector<EnvRec> r_theta, r_phi;  // their bucket records
 };
 
 // g[k] = lower_bound(a, k/G * a[n-1]), k = 0..G
@@ -94,6 +95,20 @@ static void build_guide(const float* a, int n, int* g) {
     const float v = (float)((double)k / PT_ENV_GUIDE) * total;
     g[k] = (int)(std::lower_bound(a, a + n, v) - a);
     if (g[k] > n - 1) g[k] = n - 1;
+  }
+}
+// The bucket records of a (n entries) from its guide table g (EnvRec).
+static void build_records(const float* a, const int* g, EnvRec* r) {
+  for (int k = 0; k < PT_ENV_GUIDE; ++k) {
+    EnvRec& e = r[k];
+    e.lo = g[std::max(k - 1, 0)];
+    e.hi = g[std::min(k + 2, PT_ENV_GUIDE)];
+    e.wm = e.lo > 0 ? a[e.lo - 1] : 0.0f;
+    e.w0 = a[std::min(e.lo, e.hi)];
+    e.w1 = a[std::min(e.lo + 1, e.hi)];
+    e.w2 = a[std::min(e.lo + 2, e.hi)];
+    e.w3 = a[std::min(e.lo + 3, e.hi)];
+    e.w4 = a[e.hi];
   }
 }
 #pragma clang fp contract(off)
@@ -131,6 +146,11 @@ void build_env_tables(const float* rgb, int w, int h, EnvTables& t) {
   build_guide(t.p_theta.data(), h, t.g_theta.data());
   t.g_phi.resize((size_t)h * (PT_ENV_GUIDE + 1));
   for (int y = 0; y < h; y++) build_guide(&t.p_phi[(size_t)y * w], w, &t.g_phi[(size_t)y * (PT_ENV_GUIDE + 1)]);
+  t.r_theta.resize(PT_ENV_GUIDE);
+  build_records(t.p_theta.data(), t.g_theta.data(), t.r_theta.data());
+  t.r_phi.resize((size_t)h * PT_ENV_GUIDE);
+  for (int y = 0; y < h; y++)
+    build_records(&t.p_phi[(size_t)y * w], &t.g_phi[(size_t)y * (PT_ENV_GUIDE + 1)], &t.r_phi[(size_t)y * PT_ENV_GUIDE]);
 }
 #pragma clang fp contract(on)
 
@@ -156,7 +176,7 @@ struct pt_ctx {
   DevBuf<float> norms_ref;
   DevBuf<float4> env_tex;          // environment map RGB (w*h, .w unused)
   DevBuf<float> env_ptheta, env_pphi, env_pdf;  // EnvironmentLight tables
-  DevBuf<int> env_gtheta, env_gphi;               // their guide tables
+  DevBuf<EnvRec> env_rtheta, env_rphi;            // their guide tables' bucket records
   int env_w = 0, env_h = 0;
   DevBuf<DPrim> prims;
   DevBuf<float> norms;
@@ -295,8 +315,8 @@ int pt_destroy(pt_ctx* c) {
   c->env_ptheta.release();
   c->env_pphi.release();
   c->env_pdf.release();
-  c->env_gtheta.release();
-  c->env_gphi.release();
+  c->env_rtheta.release();
+  c->env_rphi.release();
   c->prims.release();
   c->norms.release();
   c->bsdfs.release();
@@ -832,10 +852,10 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
     HIPCHK(hipMemcpy(c->env_ptheta.p, env.p_theta.data(), env.p_theta.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->env_pphi.p, env.p_phi.data(), env.p_phi.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->env_pdf.p, env.p_theta_phi.data(), env.p_theta_phi.size() * 4, hipMemcpyHostToDevice));
-    HIPCHK(c->env_gtheta.reserve(env.g_theta.size()));
-    HIPCHK(c->env_gphi.reserve(env.g_phi.size()));
-    HIPCHK(hipMemcpy(c->env_gtheta.p, env.g_theta.data(), env.g_theta.size() * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->env_gphi.p, env.g_phi.data(), env.g_phi.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(c->env_rtheta.reserve(env.r_theta.size()));
+    HIPCHK(c->env_rphi.reserve(env.r_phi.size()));
+    HIPCHK(hipMemcpy(c->env_rtheta.p, env.r_theta.data(), env.r_theta.size() * sizeof(EnvRec), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->env_rphi.p, env.r_phi.data(), env.r_phi.size() * sizeof(EnvRec), hipMemcpyHostToDevice));
   }
   c->n_lights = (int)ls.size();
   c->n_bsdfs = (int)bs.size();
@@ -1043,8 +1063,8 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.env_ptheta = c->env_ptheta.p;
   P.env_pphi = c->env_pphi.p;
   P.env_pdf = c->env_pdf.p;
-  P.env_gtheta = c->env_gtheta.p;
-  P.env_gphi = c->env_gphi.p;
+  P.env_rtheta = c->env_rtheta.p;
+  P.env_rphi = c->env_rphi.p;
   P.tiles = c->tiles[slot].p;
   P.out = out_dev;
   P.packed = (flags & PT_FLAG_PACKED) ? 1 : 0;

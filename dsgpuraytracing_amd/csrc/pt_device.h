@@ -48,6 +48,16 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #ifndef PT_LEAF_WEIGHT_ENV
 #define PT_LEAF_WEIGHT_ENV 16
 #endif
+// One guide bucket k of a running-sum array a (environment-light CDFs), in
+// one 32-B record so that a lower_bound whose window is short needs ONE
+// memory round trip: the window [lo, hi] = [g[k-1], g[k+2]] of the guide
+// table g, and the window's values w_i = a[min(lo + i, hi)] (i < 4), w4 =
+// a[hi], wm = a[lo - 1] (0 at lo = 0).  Windows longer than four entries
+// (hi - lo > 4) are halved on the array itself.
+struct alignas(32) EnvRec {
+  int lo, hi;
+  float wm, w0, w1, w2, w3, w4;
+};
 #ifndef PT_ENV_GUIDE
 #define PT_ENV_GUIDE 1024  // buckets of the environment-CDF guide tables (with the window compare: C5 +10% over 64, profiles/r3/ab_env_window_search.txt)
 #endif
@@ -142,8 +152,8 @@ struct KParams {
   const float* env_ptheta;   // EnvironmentLight::pTheta (running sums over rows)
   const float* env_pphi;     // pPhiGivenTheta (running sums within each row)
   const float* env_pdf;      // pThetaPhi
-  const int* env_gtheta;     // guide table of env_ptheta (PT_ENV_GUIDE + 1 entries)
-  const int* env_gphi;       // guide tables of the rows of env_pphi (h x (PT_ENV_GUIDE + 1))
+  const struct EnvRec* env_rtheta;  // bucket records of env_ptheta (PT_ENV_GUIDE)
+  const struct EnvRec* env_rphi;    // bucket records of the rows of env_pphi (h x PT_ENV_GUIDE)
   const int4* tiles;  // (x, y, w, h)
   float* out;         // W*H*3, or n_tiles*1024*3 when packed
   int packed;         // PT_FLAG_PACKED: tile i's pixel (x, y) -> out[3 * (i*1024 + (y-ty)*32 + (x-tx))]

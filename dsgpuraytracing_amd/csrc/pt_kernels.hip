@@ -379,6 +379,9 @@ __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, const
   }
   if (STATS) ct.nodes++;
   const float3 oi = f3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+  // (The 24 plane distances as packed v_pk_fma_f32 pairs -- half the FMA
+  // issues, same roundings -- measured C3 -2.4%, C4 -1.9%, C5 -1.1%:
+  // profiles/r4/ab_packed_node.txt)
   const float* NX = &nx.x; const float* FX = &fx.x; const float* NY = &ny.x;
   const float* FY = &fy.x; const float* NZ = &nz.x; const float* FZ = &fz.x;
 #pragma unroll
@@ -533,49 +536,40 @@ __device__ __forceinline__ float3 env_dir(const KP& P, float3 d) {
 // answer lies in [g[k-1], g[k+2]] for k = floor(r*G), one bucket of slack
 // either side for rounding, and a[g[k+2]] >= v; the result is exactly
 // std::lower_bound's.  With PT_ENV_GUIDE buckets the window is a few entries
-// where the CDF carries mass (where samples land): it is halved down to <= 4
-// entries, then compared in ONE memory round trip (lower_bound = lo +
-// #{entries < v}, the array is sorted).  The same round trip loads the
-// entries either side of the window, so the caller's interpolation pair
-// (prev = a[t-1] or 0, cur = a[t]) comes from registers, not from two more
-// dependent loads.
-#ifndef PT_ENV_PAIR
-#define PT_ENV_PAIR 1
-#endif
-__device__ __forceinline__ int guided_lower_bound(const float* __restrict__ a, float v, float r,
-                                                  const int* __restrict__ g, int G, float& prev, float& cur) {
+// where the CDF carries mass (where samples land).  Bucket k's record (EnvRec)
+// holds the window and its values, so the usual short window (<= 4 entries)
+// costs ONE memory round trip -- two 16-B loads of one 32-B record -- and
+// lower_bound = lo + #{entries < v} (the array is sorted); the caller's
+// interpolation pair (prev = a[t-1] or 0, cur = a[t]) comes from the same
+// registers.  A longer window is halved down to <= 4 entries on the array
+// and re-read.  (Guide table, then window: two dependent round trips, C5 -1.9%:
+// profiles/r4/ab_env_records.txt.)
+__device__ __forceinline__ int record_lower_bound(const float* __restrict__ a, float v, float r,
+                                                  const EnvRec* __restrict__ rec, int G, float& prev, float& cur) {
   const int k = min(G - 1, max(0, (int)(r * (float)G)));
-  int lo = g[max(k - 1, 0)];
-  const int hi = g[min(k + 2, G)];
-  int n = hi - lo;  // candidates [lo, hi); hi itself satisfies a[hi] >= v
-  while (n > 4) {
-    const int half = n >> 1;
-    if (a[lo + half] < v) {
-      lo += half + 1;
-      n -= half + 1;
-    } else {
-      n = half;
+  typedef float rf4 __attribute__((ext_vector_type(4)));
+  const rf4 q0 = *(const rf4*)&rec[k].lo, q1 = *(const rf4*)&rec[k].w1;
+  int lo = __float_as_int(q0.x);
+  const int hi = __float_as_int(q0.y);
+  float wm = q0.z, w0 = q0.w, w1 = q1.x, w2 = q1.y, w3 = q1.z, w4 = q1.w;
+  int n = hi - lo;
+  if (n > 4) {  // (rare: where the CDF is flat, the window spans more entries)
+    while (n > 4) {
+      const int half = n >> 1;
+      if (a[lo + half] < v) {
+        lo += half + 1;
+        n -= half + 1;
+      } else {
+        n = half;
+      }
     }
+    wm = lo > 0 ? a[lo - 1] : 0.0f;
+    w0 = a[min(lo, hi)], w1 = a[min(lo + 1, hi)], w2 = a[min(lo + 2, hi)], w3 = a[min(lo + 3, hi)];
   }
-#if PT_ENV_PAIR
-  // w_i = a[min(lo + i, hi)]: entries past the window read a[hi] >= v, which
-  // never counts; w4 = a[hi] is a[t] when all four candidates are < v
-  const float wm = lo > 0 ? a[lo - 1] : 0.0f;
-  const float w0 = a[min(lo, hi)], w1 = a[min(lo + 1, hi)], w2 = a[min(lo + 2, hi)], w3 = a[min(lo + 3, hi)];
-  const float w4 = a[hi];
   const int c = (int)(w0 < v) + (int)(w1 < v) + (int)(w2 < v) + (int)(w3 < v);
   cur = c == 0 ? w0 : c == 1 ? w1 : c == 2 ? w2 : c == 3 ? w3 : w4;
   prev = c == 0 ? wm : c == 1 ? w0 : c == 2 ? w1 : c == 3 ? w2 : w3;
   return lo + c;
-#else
-  const float kBig = 3.0e38f;
-  const float w0 = n > 0 ? a[lo] : kBig, w1 = n > 1 ? a[lo + 1] : kBig;
-  const float w2 = n > 2 ? a[lo + 2] : kBig, w3 = n > 3 ? a[lo + 3] : kBig;
-  const int t = lo + (int)(w0 < v) + (int)(w1 < v) + (int)(w2 < v) + (int)(w3 < v);
-  prev = t > 0 ? a[t - 1] : 0.0f;
-  cur = a[t];
-  return t;
-#endif
 }
 
 // importanceSampling (69-115): inverse CDF over rows (pTheta), then within the
@@ -587,13 +581,13 @@ __device__ __forceinline__ void env_sample(const KP& P, float r1, float r2, floa
   const float u1 = r1;
   r1 *= P.env_ptheta[h - 1];
   float prev, cur;
-  const int t = guided_lower_bound(P.env_ptheta, r1, u1, P.env_gtheta, PT_ENV_GUIDE, prev, cur);
+  const int t = record_lower_bound(P.env_ptheta, r1, u1, P.env_rtheta, PT_ENV_GUIDE, prev, cur);
   const float y = (float)t + (r1 - prev) / (cur - prev);
   const float theta = fminf(y / (float)h, 1.0f) * kPi;
   const float* row = P.env_pphi + (size_t)t * w;
   const float u2 = r2;
   r2 *= row[w - 1];
-  const int q = guided_lower_bound(row, r2, u2, P.env_gphi + (size_t)t * (PT_ENV_GUIDE + 1), PT_ENV_GUIDE, prev, cur);
+  const int q = record_lower_bound(row, r2, u2, P.env_rphi + (size_t)t * PT_ENV_GUIDE, PT_ENV_GUIDE, prev, cur);
   const float x = (float)q + (r2 - prev) / (cur - prev);
   const float phi = fminf(x / (float)w, 1.0f) * (2.0f * kPi);
   float st, ct, sp, cp;

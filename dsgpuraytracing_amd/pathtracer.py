@@ -106,10 +106,20 @@ class Device:
         flags = _flags(stats)
         check(self._lib.pt_render_tiles(self.handle, arr, len(keep), out.ctypes.data, flags))
 
-    def render_tiles_device(self, tiles, out_ptr: int, stream: int = 0, stats: bool = False, packed: bool = False):
+    def render_tiles_device(self, tiles, out_ptr: int, stream: int = 0, stats: bool = False, packed: bool = False,
+                            out_floats: Optional[int] = None):
         """packed=True: out_ptr holds len(tiles)*32*32*3 floats, tile i's pixel
-        (x, y) at [(i*1024 + (y-ty)*32 + (x-tx))*3] (PT_FLAG_PACKED)."""
+        (x, y) at [(i*1024 + (y-ty)*32 + (x-tx))*3] (PT_FLAG_PACKED); else a
+        whole H x W x 3 frame.  out_floats: the buffer's size in floats, checked
+        against what the layout writes (the library sees only a pointer)."""
         keep, arr = self._tiles(tiles)
+        if out_floats is not None:
+            if getattr(self, "_frame", None) is None:
+                raise ValueError("render_tiles_device: set_params first")
+            need = len(keep) * 1024 * 3 if packed else self._frame[0] * self._frame[1] * 3
+            if out_floats < need:
+                raise ValueError(f"render_tiles_device: output holds {out_floats} floats, the "
+                                 f"{'packed' if packed else 'frame'} layout writes {need}")
         flags = _flags(stats) | (native.PT_FLAG_PACKED if packed else 0)
         check(self._lib.pt_render_tiles_device(self.handle, arr, len(keep), ctypes.c_void_p(out_ptr),
                                                ctypes.c_void_p(stream or None), flags))
