@@ -1090,7 +1090,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     int v = std::atoi(lw);
     if (v >= 1) P.leaf_weight = v;
   }
-  P.census = std::getenv("PT_CENSUS") && !stats ? 1 : 0;  // diagnostics (tools/wave_trace.py --census)
+  P.census = PT_CENSUS && std::getenv("PT_CENSUS") && !stats ? 1 : 0;  // diagnostics (tools/wave_trace.py --census)
   P.drain_div = 0;
   if (const char* dd = std::getenv("PT_DRAIN_DIV")) {  // tuning knob
     int v = std::atoi(dd);
@@ -1605,7 +1605,7 @@ int pt_get_launch_times(pt_ctx* c, float* kernel_ms, float* resolve_ms, int32_t 
 int pt_get_wave_trace(pt_ctx* c, int64_t* out, int64_t cap, int64_t* n_waves) {
   if (!c || !n_waves) return fail(PT_E_INVALID, "pt_get_wave_trace: NULL argument");
   if (!c->last.counters_valid && !c->census_valid)
-    return fail(PT_E_INVALID, "pt_get_wave_trace: the last launch had no counters (or census)");
+    return fail(PT_E_INVALID, "pt_get_wave_trace: the last launch had no counters (nor a census: a -DPT_CENSUS=1 build with PT_CENSUS set)");
   const int64_t n = c->last.grid_blocks;
   *n_waves = n;
   if (!out) return PT_OK;

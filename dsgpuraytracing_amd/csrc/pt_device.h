@@ -58,6 +58,13 @@ struct alignas(32) EnvRec {
   int lo, hi;
   float wm, w0, w1, w2, w3, w4;
 };
+// The residency / drain census of plain launches (tools/wave_trace.py
+// --census) is compiled in only with -DPT_CENSUS=1 (PT_HIPCC_FLAGS): its
+// bookkeeping in the persistent loop cost C3 2% even when off
+// (profiles/r4/census_drain.txt).
+#ifndef PT_CENSUS
+#define PT_CENSUS 0
+#endif
 #ifndef PT_ENV_GUIDE
 #define PT_ENV_GUIDE 1024  // buckets of the environment-CDF guide tables (with the window compare: C5 +10% over 64, profiles/r3/ab_env_window_search.txt)
 #endif
@@ -167,7 +174,7 @@ struct KParams {
   int shade_batch;            // leave the traversal phase once this many lanes finished their ray
   int leaf_weight;            // leaf steps run when leaf_weight * leaf lanes >= 16 * node lanes
   int drain_div;              // queue drained: shade once alive/drain_div lanes are ready (0: 3/4 rule)
-  int census;                 // plain build: record each wave's start / end / CU in the trace area (PT_CENSUS)
+  int census;                 // plain build: record each wave's start / end / CU / drain in the trace area (PT_CENSUS)
   float root_lo[3], root_hi[3];  // scene bounds (root box, rounded outward)
   int cull_x0, cull_y0, cull_x1, cull_y1;  // pixels outside [x0,x1]x[y0,y1] see no geometry
 };

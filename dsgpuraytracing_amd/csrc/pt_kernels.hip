@@ -752,13 +752,14 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // Residency census of the plain build (PT_CENSUS=1, diagnostics): when
   // each wave started and ended, and where it ran -- which waves of the grid
   // were resident from the start.
-  unsigned long long* const census = (!STATS && P.census) ? P.stats + PT_STATS_SLOTS + PT_WAVE_TRACE * (size_t)wave_id : nullptr;
+  unsigned long long* const census = (PT_CENSUS && !STATS && P.census) ? P.stats + PT_STATS_SLOTS + PT_WAVE_TRACE * (size_t)wave_id : nullptr;
   if (census && lane == 0) {
     census[0] = wall_clock64();
     census[3] = ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32) |
                 (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
   }
   unsigned long long w_empty = 0ull;  // when this wave first found the queue empty
+  int census_alive = -1, census_rounds = 0;  // (census: lanes alive at the drain's first round, rounds since)
   unsigned long long slot_t0 = 0ull, slot_lat_sum = 0ull, slot_lat_max = 0ull;  // work-slot latency (wall ticks)
   // per ray: traversal iterations it stepped in / sat out, traversal phases it spanned
   uint32_t r_steps = 0, r_idle = 0, r_rounds = 0, ray_steps_max = 0, ray_idle_max = 0, ray_rounds_max = 0;
@@ -1166,7 +1167,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           uint32_t slot = rank < avail ? chunk_next + rank : nbase + (rank - avail);
           if (slot >= total_slots) {
             mode = shadow ? M_TRAV : M_DONE;  // (a pending shadow ray is traced first)
-            if (STATS && w_empty == 0ull) w_empty = wall_clock64();
+            if ((STATS || census) && w_empty == 0ull) w_empty = wall_clock64();
           } else {
             // Blocks are <= 8x8 pixel rectangles of the tiles, clipped to the
             // scene's screen footprint (pixels outside are written 0 by
@@ -1278,6 +1279,10 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     // lanes still working are ready, not when `batch` of 64 are, or the tail
     // would wait for the slowest ray of the wave at every bounce.
     const int alive = __popcll(__ballot(mode != M_DONE));
+    if (census && seen >= total_slots) {  // (diagnostics: the wave's drain)
+      if (census_alive < 0) census_alive = alive;
+      ++census_rounds;
+    }
     int round_batch = min(batch, (3 * alive + 3) / 4);
     if (P.drain_div > 0 && seen >= total_slots)  // the queue is drained: latency, not throughput
       round_batch = max(1, alive / P.drain_div);
@@ -1333,7 +1338,21 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     PT_STAMP(S_TRAV);
   }
 
-  if (census && lane == 0) census[2] = wall_clock64();
+  if (census) {
+    // first time a lane of the wave found the queue empty, its lanes alive
+    // then, the wave's rounds from then on
+    unsigned long long e = w_empty ? w_empty : ~0ull;
+    for (int off = 32; off > 0; off >>= 1) {
+      const unsigned long long o = __shfl_xor(e, off);
+      e = o < e ? o : e;
+    }
+    if (lane == 0) {
+      census[1] = e;
+      census[2] = wall_clock64();
+      census[4] = (unsigned long long)census_alive;
+      census[5] = (unsigned long long)census_rounds;
+    }
+  }
   if (STATS) {
     PT_STAMP(S_OTHER);
     unsigned long long v[11] = {n_cam, n_bounce, n_shadow, ct.nodes, ct.tris, ct.spheres, n_hits,

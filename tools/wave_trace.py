@@ -31,7 +31,9 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--share", type=int, default=0, help="N: rank 0's share of an N-GPU split (packed output)")
     ap.add_argument("--census", action="store_true",
-                    help="the PLAIN build's residency instead (PT_CENSUS=1): wave starts/ends per CU, no counters")
+                    help="the PLAIN build's residency and drain instead: wave starts / first empty queue / ends "
+                         "per CU, lanes alive and rounds in the drain; needs a library built with "
+                         "PT_HIPCC_FLAGS=-DPT_CENSUS=1 (tools/variants.sh)")
     args = ap.parse_args()
     import torch
 
@@ -77,9 +79,15 @@ def main():
         early = start < 100.0
         per_cu = np.bincount(np.unique(cu_key[early], return_inverse=True)[1])
         q = [0, 0.01, 0.1, 0.5, 0.9, 0.99, 1.0]
+        emp = np.where(tr[:, 1] != -1, (tr[:, 1] - t0) * 0.01, np.nan)  # (-1: never saw it empty)
         print(json.dumps({"census": True, "waves": len(tr), "kernel_ms": dev.launch_times(1)[0][0].item(),
                           "start_us_quantiles": [round(float(np.quantile(start, x)), 1) for x in q],
                           "end_us_quantiles": [round(float(np.quantile(end, x)), 1) for x in q],
+                          "empty_us_quantiles": [round(float(np.nanquantile(emp, x)), 1) for x in q],
+                          "drain_us_quantiles": [round(float(np.nanquantile(end - emp, x)), 1) for x in q],
+                          "alive_at_empty_quantiles": [int(np.quantile(tr[:, 4], x)) for x in q],
+                          "drain_rounds_quantiles": [int(np.quantile(tr[:, 5], x)) for x in q],
+                          "alive_at_empty_hist8": np.bincount(np.clip(tr[:, 4], 0, 64) // 8, minlength=9).tolist(),
                           "late_starts": int((~early).sum()), "cus_seen": int(len(np.unique(cu_key))),
                           "early_waves_per_cu_min_max": [int(per_cu.min()), int(per_cu.max())],
                           "early_waves_per_cu_hist": np.bincount(per_cu).tolist()}))
