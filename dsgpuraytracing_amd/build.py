@@ -66,13 +66,19 @@ def build(force: bool = False, verbose: bool = False) -> str:
             # cost more VALU slots and VGPRs than the pairing saves here
             # (render_kernel 103 -> 99 VGPRs; C3 +3.5%)
             cmd.insert(1, "-fno-slp-vectorize")
-        sched = os.environ.get("PT_KERNEL_SCHED", "ilp")  # experiments: "default" drops the ILP scheduler
-        env_sched = os.environ.get("PT_ENV_SCHED", "ilp")  # experiments: "default"
-        if (base == "pt_kernels.hip" and sched == "ilp") or (base == "pt_kernels_env.hip" and env_sched == "ilp"):
-            # iterative-ILP machine scheduling: C3 +1.7%, framed C3 +1.8%; the
-            # ENV kernels (their own translation unit) measured -2.9% with it in
-            # round 2 and +0.8% on C5 with the round-3 follow-up rays
-            cmd[1:1] = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
+        # machine scheduler per kernel translation unit (experiments: "default"
+        # drops the flag, any other value is passed as the strategy name)
+        sched = os.environ.get("PT_KERNEL_SCHED", "max-ilp")
+        env_sched = os.environ.get("PT_ENV_SCHED", "iterative-ilp")
+        strategy = {"pt_kernels.hip": sched, "pt_kernels_env.hip": env_sched}.get(base, "default")
+        if strategy == "ilp":
+            strategy = "iterative-ilp"
+        if strategy != "default":
+            # common build: iterative-ILP scheduling measured C3 +1.7% in round 2,
+            # max-ILP +1.0-1.5% over it in round 4 (profiles/r4/ab_sched_strategy.txt,
+            # ab_env_uv_groups.txt); the ENV build stays iterative-ILP (C5 +0.8%
+            # with the round-3 follow-up rays; max-ILP neutral)
+            cmd[1:1] = ["-mllvm", f"-amdgpu-sched-strategy={strategy}"]
         if src.endswith(".cpp") and "pt_api" not in src:
             cmd.insert(1, "-xc++")  # host-only translation units
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))

@@ -968,19 +968,34 @@ static void screen_footprint(const pt_ctx* c, KParams& P) {
   P.cull_y1 = r[3];
 }
 
+// Pixels whose camera rays can reach the scene: the footprint's area inside
+// the frame, or the whole frame with an environment light (misses see the
+// map) or no footprint.  A property of the frame -- PT_NO_FOOTPRINT_CULL
+// leaves it alone -- for the sample-group size.
+static int64_t traced_px(const pt_ctx* c, int W, int H) {
+  int r[4];
+  if (c->env_w > 0 || !footprint_rect(c, W, H, r)) return (int64_t)W * H;
+  const int64_t w = std::min(W - 1, r[2]) - std::max(0, r[0]) + 1, h = std::min(H - 1, r[3]) - std::max(0, r[1]) + 1;
+  return std::max<int64_t>(0, w) * std::max<int64_t>(0, h);
+}
+
 // Sample groups of a pixel (KParams: n_groups groups of group_spp samples,
 // the last one possibly short).  The grouping decides the float summation
-// order of a pixel, so it is a function of the FRAME -- its size and spp --
-// and the device's resident grid only, never of the launch's tile set or of
-// a stats build: any split of a frame into tile launches (raytrace_tile
-// calls, the multi-GPU shards) sums every pixel in the same order as the
-// whole frame.  group_spp: 4 (C3 +3.3% over 2; 8 or more lose), halved for
-// small frames until there are >= 16 work slots per resident lane (C1, C2: 1).
-// (A tail of one-sample groups handed out last, to end the launch on short
-// work slots, measured -2% pipelined for +2% on a lone frame: DESIGN.md §4.)
-static int group_size(int64_t frame_px, int spp, int64_t lanes, int64_t frame_blocks) {
-  int gs = PT_GROUP_SPP;
-  while (gs > 1 && frame_px * ((spp + gs - 1) / gs) < lanes * 16) gs /= 2;
+// order of a pixel, so it is a function of the FRAME -- its size, spp, the
+// pixels its camera rays can reach, the environment light -- and the
+// device's resident grid only, never of the launch's tile set or of a stats
+// build: any split of a frame into tile launches (raytrace_tile calls, the
+// multi-GPU shards) sums every pixel in the same order as the whole frame.
+//  * group_spp: 4 (C4 +4%, framed C3 +2% over 2), 2 with an environment
+//    light (C5 +2.3%, c5big +2.1%), halved until the traced samples make >= 24
+//    work slots per resident lane: C3's footprint-culled frame gets 2 (+1.5%
+//    pipelined, its lone launch 1.70 -> 1.44 ms: half the work in flight when
+//    the queue runs dry), C1 / C2 get 1 (profiles/r4/ab_group_size.txt);
+//  * (a tail of one-sample groups handed out last, to end the launch on short
+//    work slots, measured -2% pipelined for +2% on a lone frame: DESIGN.md §4).
+static int group_size(int64_t traced, bool env, int spp, int64_t lanes, int64_t frame_blocks) {
+  int gs = env ? PT_GROUP_SPP_ENV : PT_GROUP_SPP;
+  while (gs > 1 && traced * ((spp + gs - 1) / gs) < lanes * PT_GROUP_MIN_SLOTS) gs /= 2;
   if (const char* g = std::getenv("PT_SAMPLE_GROUP")) {  // tuning knob
     int v = std::atoi(g);
     if (v > 0) gs = v;
@@ -988,10 +1003,13 @@ static int group_size(int64_t frame_px, int spp, int64_t lanes, int64_t frame_bl
   gs = std::max(1, std::min(gs, spp));
   for (;;) {
     // 32-bit slot indices (they may overshoot by a static and a claimed
-    // chunk per wave) and a group-sum budget of 4 GiB per render slot, for the
-    // whole frame's blocks (so every tile split gets the same layout)
+    // chunk per wave) and a group-sum budget of PT_GROUP_SUM_GIB per render
+    // slot, for the whole frame's blocks (so every tile split gets the same
+    // layout)
     const int64_t slots = frame_blocks * 64 * ((spp + gs - 1) / gs);
-    if ((slots + 2 * (lanes / 64) * PT_CHUNK_MAX < (int64_t)INT32_MAX && slots * 12 <= (4ll << 30)) || gs >= spp) break;
+    if ((slots + 2 * (lanes / 64) * PT_CHUNK_MAX < (int64_t)INT32_MAX && slots * 12 <= ((int64_t)PT_GROUP_SUM_GIB << 30)) ||
+        gs >= spp)
+      break;
     gs = std::min(spp, gs * 2);
   }
   return gs;
@@ -1090,7 +1108,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     int v = std::atoi(lw);
     if (v >= 1) P.leaf_weight = v;
   }
-  P.census = PT_CENSUS && std::getenv("PT_CENSUS") && !stats ? 1 : 0;  // diagnostics (tools/wave_trace.py --census)
+  P.census = std::getenv("PT_CENSUS") && !stats ? 1 : 0;  // diagnostics (tools/wave_trace.py --census)
   P.drain_div = 0;
   if (const char* dd = std::getenv("PT_DRAIN_DIV")) {  // tuning knob
     int v = std::atoi(dd);
@@ -1152,10 +1170,9 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     int w = std::atoi(g);
     if (w > 0) want = (int64_t)w * c->n_cu;
   }
-  const int64_t frame_px = (int64_t)P.W * P.H;
   const int64_t want_plain = std::getenv("PT_WAVES_PER_CU") ? want : c->grid_plain;
   const int64_t frame_blocks = (int64_t)((P.W + 7) / 8) * ((P.H + 7) / 8);
-  P.group_spp = group_size(frame_px, P.spp, want_plain * PT_BLOCK, frame_blocks);
+  P.group_spp = group_size(traced_px(c, P.W, P.H), c->env_w > 0, P.spp, want_plain * PT_BLOCK, frame_blocks);
   P.n_groups = (P.spp + P.group_spp - 1) / P.group_spp;
   const int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
   // (slot indices reach past the end by up to a static chunk plus a claimed one per wave)
@@ -1178,6 +1195,8 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   if ((stats || P.census) && (size_t)grid * PT_WAVE_TRACE + PT_STATS_SLOTS > c->stats.n)
     grid = (int)((c->stats.n - PT_STATS_SLOTS) / PT_WAVE_TRACE);
   grid = std::max(1, grid);
+  if (P.census)  // (a build without -DPT_CENSUS=1 leaves the drain fields 0)
+    HIPCHK(hipMemsetAsync(c->stats.p + PT_STATS_SLOTS, 0, (size_t)grid * PT_WAVE_TRACE * 8, rs));
   P.stack_spill = nullptr;
   if (c->bvh_stack > PT_STACK) {  // worst-case depth beyond the LDS stack
     HIPCHK(c->spill[slot].reserve((size_t)(c->bvh_stack - PT_STACK) * grid * PT_BLOCK));
@@ -1605,7 +1624,7 @@ int pt_get_launch_times(pt_ctx* c, float* kernel_ms, float* resolve_ms, int32_t 
 int pt_get_wave_trace(pt_ctx* c, int64_t* out, int64_t cap, int64_t* n_waves) {
   if (!c || !n_waves) return fail(PT_E_INVALID, "pt_get_wave_trace: NULL argument");
   if (!c->last.counters_valid && !c->census_valid)
-    return fail(PT_E_INVALID, "pt_get_wave_trace: the last launch had no counters (nor a census: a -DPT_CENSUS=1 build with PT_CENSUS set)");
+    return fail(PT_E_INVALID, "pt_get_wave_trace: the last launch had no counters (or census)");
   const int64_t n = c->last.grid_blocks;
   *n_waves = n;
   if (!out) return PT_OK;

@@ -19,7 +19,16 @@
 static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand");
 #define PT_QUEUE_WORDS 32  // the work-queue head, alone in its 128-B line
 #ifndef PT_GROUP_SPP
-#define PT_GROUP_SPP 4  // default samples per work slot (C3 +3.3% over 2; 8 or more: C3 -4%, C5 -10%)
+#define PT_GROUP_SPP 4  // default samples per work slot (pt_api.cpp group_size; 8 or more: C3 -4%, C5 -10%)
+#endif
+#ifndef PT_GROUP_SPP_ENV
+#define PT_GROUP_SPP_ENV 2  // with an environment light
+#endif
+#ifndef PT_GROUP_MIN_SLOTS
+#define PT_GROUP_MIN_SLOTS 24  // groups are halved until the traced samples make this many slots per lane
+#endif
+#ifndef PT_GROUP_SUM_GIB
+#define PT_GROUP_SUM_GIB 8  // group-sum budget per render slot (GiB): a group size that needs more doubles
 #endif
 // Leave traversal when this many lanes finished their ray (shade them
 // together).  Scenes with an environment light shade longer per round (map
@@ -58,8 +67,8 @@ struct alignas(32) EnvRec {
   int lo, hi;
   float wm, w0, w1, w2, w3, w4;
 };
-// The residency / drain census of plain launches (tools/wave_trace.py
-// --census) is compiled in only with -DPT_CENSUS=1 (PT_HIPCC_FLAGS): its
+// The drain fields of the census of plain launches (tools/wave_trace.py
+// --census) are compiled in only with -DPT_CENSUS=1 (PT_HIPCC_FLAGS): their
 // bookkeeping in the persistent loop cost C3 2% even when off
 // (profiles/r4/census_drain.txt).
 #ifndef PT_CENSUS

@@ -495,18 +495,11 @@ __device__ __forceinline__ bool box_hit(const Trav& tr, const T* lo, const T* hi
 }
 
 // ---- EnvironmentLight (src/static_scene/environment_light.cpp), fp32.
-// sample_dir (130-199): lat-long bilinear lookup, wrapping in both directions
-// exactly as the reference does.
+// sample_dir (130-199): lat-long bilinear lookup at texel coordinates (tu,
+// tv), wrapping in both directions exactly as the reference does.
 template <class KP>
-__device__ __forceinline__ float3 env_dir(const KP& P, float3 d) {
-  const float kPi = 3.14159265358979323f;
+__device__ __forceinline__ float3 env_uv(const KP& P, float tu, float tv) {
   const int w = P.env_w, h = P.env_h;
-  const float theta = acosf(fminf(fmaxf(d.y, -1.0f), 1.0f));
-  const float sin_theta = fsqrt(fmaxf(0.0f, 1.0f - d.y * d.y));
-  float phi = sin_theta == 0.0f ? kPi : acosf(fminf(fmaxf(d.z / sin_theta, -1.0f), 1.0f));
-  if (d.x > 0.0f) phi = 2.0f * kPi - phi;
-  const float tu = phi * (0.15915494309189535f * (float)w) - 0.5f;
-  const float tv = theta * (0.31830988618379067f * (float)h) - 0.5f;
   const int su = (int)tu, sv = (int)tv;
   float a, b;
   int px1, px2, py1, py2;
@@ -529,6 +522,20 @@ __device__ __forceinline__ float3 env_dir(const KP& P, float3 d) {
   const float3 zy1 = f3(z11.x, z11.y, z11.z) * (1.0f - a) + f3(z21.x, z21.y, z21.z) * a;
   const float3 zy2 = f3(z12.x, z12.y, z12.z) * (1.0f - a) + f3(z22.x, z22.y, z22.z) * a;
   return zy1 * (1.0f - b) + zy2 * b;
+}
+
+// sample_dir of a direction: (theta, phi) from the direction, then the lookup
+template <class KP>
+__device__ __forceinline__ float3 env_dir(const KP& P, float3 d) {
+  const float kPi = 3.14159265358979323f;
+  const int w = P.env_w, h = P.env_h;
+  const float theta = acosf(fminf(fmaxf(d.y, -1.0f), 1.0f));
+  const float sin_theta = fsqrt(fmaxf(0.0f, 1.0f - d.y * d.y));
+  float phi = sin_theta == 0.0f ? kPi : acosf(fminf(fmaxf(d.z / sin_theta, -1.0f), 1.0f));
+  if (d.x > 0.0f) phi = 2.0f * kPi - phi;
+  const float tu = phi * (0.15915494309189535f * (float)w) - 0.5f;
+  const float tv = theta * (0.31830988618379067f * (float)h) - 0.5f;
+  return env_uv(P, tu, tv);
 }
 
 // lower_bound of v = r * a[n-1] accelerated by a guide table g[0..G] with
@@ -574,8 +581,17 @@ __device__ __forceinline__ int record_lower_bound(const float* __restrict__ a, f
 
 // importanceSampling (69-115): inverse CDF over rows (pTheta), then within the
 // row (pPhiGivenTheta), linear inside the texel; pdf per solid angle.
+// The sampled direction's radiance (sample_L returns sample_dir(wi)) is
+// looked up at the texel coordinates the sample was drawn at, (x - 0.5,
+// y - 0.5) -- what sample_dir's acos round trip of wi yields up to float
+// rounding (~1e-5 texel), without its two acosf and a division on the
+// NEE's dependent chain: returned in (tu, tv) for env_uv.
+#ifndef PT_ENV_DIRECT_UV
+#define PT_ENV_DIRECT_UV 1
+#endif
 template <class KP>
-__device__ __forceinline__ void env_sample(const KP& P, float r1, float r2, float3& wi, float& pdf) {
+__device__ __forceinline__ void env_sample(const KP& P, float r1, float r2, float3& wi, float& pdf, float& tu,
+                                           float& tv) {
   const float kPi = 3.14159265358979323f;
   const int w = P.env_w, h = P.env_h;
   const float u1 = r1;
@@ -583,12 +599,14 @@ __device__ __forceinline__ void env_sample(const KP& P, float r1, float r2, floa
   float prev, cur;
   const int t = record_lower_bound(P.env_ptheta, r1, u1, P.env_rtheta, PT_ENV_GUIDE, prev, cur);
   const float y = (float)t + (r1 - prev) / (cur - prev);
+  tv = fminf(y, (float)h) - 0.5f;
   const float theta = fminf(y / (float)h, 1.0f) * kPi;
   const float* row = P.env_pphi + (size_t)t * w;
   const float u2 = r2;
   r2 *= row[w - 1];
   const int q = record_lower_bound(row, r2, u2, P.env_rphi + (size_t)t * PT_ENV_GUIDE, PT_ENV_GUIDE, prev, cur);
   const float x = (float)q + (r2 - prev) / (cur - prev);
+  tu = fminf(x, (float)w) - 0.5f;
   const float phi = fminf(x / (float)w, 1.0f) * (2.0f * kPi);
   float st, ct, sp, cp;
   __sincosf(theta, &st, &ct);
@@ -749,17 +767,19 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   uint32_t seen = 0;                       // queue head after this wave's last claim
   bool first_claim = true;                 // the first chunk is the wave's own (no atomic)
   const unsigned long long w_start = STATS ? wall_clock64() : 0ull;
-  // Residency census of the plain build (PT_CENSUS=1, diagnostics): when
+  // Residency census of the plain build (PT_CENSUS set, diagnostics): when
   // each wave started and ended, and where it ran -- which waves of the grid
-  // were resident from the start.
-  unsigned long long* const census = (PT_CENSUS && !STATS && P.census) ? P.stats + PT_STATS_SLOTS + PT_WAVE_TRACE * (size_t)wave_id : nullptr;
+  // were resident from the start; with a -DPT_CENSUS=1 build also its drain.
+  unsigned long long* const census = (!STATS && P.census) ? P.stats + PT_STATS_SLOTS + PT_WAVE_TRACE * (size_t)wave_id : nullptr;
   if (census && lane == 0) {
     census[0] = wall_clock64();
     census[3] = ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32) |
                 (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
   }
   unsigned long long w_empty = 0ull;  // when this wave first found the queue empty
+#if PT_CENSUS
   int census_alive = -1, census_rounds = 0;  // (census: lanes alive at the drain's first round, rounds since)
+#endif
   unsigned long long slot_t0 = 0ull, slot_lat_sum = 0ull, slot_lat_max = 0ull;  // work-slot latency (wall ticks)
   // per ray: traversal iterations it stepped in / sat out, traversal phases it spanned
   uint32_t r_steps = 0, r_idle = 0, r_rounds = 0, ray_steps_max = 0, ray_idle_max = 0, ray_rounds_max = 0;
@@ -911,11 +931,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           }
           float3 wi;
           float dist, pdf;
+          float etu = 0.0f, etv = 0.0f;  // (environment light: the sample's texel coordinates)
           bool lit = true;
           if (ENV && ltype == 4) {  // EnvironmentLight::sample_L (environment_light.cpp:117-128)
             float r1 = PT_DRAW();
             float r2 = PT_DRAW();
-            env_sample(P, r1, r2, wi, pdf);
+            env_sample(P, r1, r2, wi, pdf, etu, etv);
             dist = 3.0e38f;
           } else if (ltype == 3) {  // AreaLight::sample_L (light.cpp:80-92); grid sampler draws y first
             float u0 = PT_DRAW();
@@ -953,7 +974,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           float cos_t = fmaxf(0.0f, fr.to_local(wi).z);
           if (!(cos_t > 0.0f)) continue;
           float3 f = PT_BSDF3(bsdf, a) * 0.31830988618379067f;
-          const float3 Le = (ENV && ltype == 4) ? env_dir(P, wi) : PT_LIGHT3(li, rad);
+          const float3 Le = (ENV && ltype == 4) ? (PT_ENV_DIRECT_UV ? env_uv(P, etu, etv) : env_dir(P, wi))
+                                                : PT_LIGHT3(li, rad);
           pend = mul(mul(T, Le * (cos_t * rcp(pdf))), f) * scale;
           // shadow ray (pathtracer.cpp:497-504): delta lights offset EPS_N along n
           float3 so = delta ? hp + ns * 5e-3f : offset_ray(hp, dot(wi, ng) >= 0.0f ? ng : f3(0, 0, 0) - ng);
@@ -1167,7 +1189,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           uint32_t slot = rank < avail ? chunk_next + rank : nbase + (rank - avail);
           if (slot >= total_slots) {
             mode = shadow ? M_TRAV : M_DONE;  // (a pending shadow ray is traced first)
-            if ((STATS || census) && w_empty == 0ull) w_empty = wall_clock64();
+            if ((STATS || (PT_CENSUS && census)) && w_empty == 0ull) w_empty = wall_clock64();
           } else {
             // Blocks are <= 8x8 pixel rectangles of the tiles, clipped to the
             // scene's screen footprint (pixels outside are written 0 by
@@ -1279,10 +1301,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     // lanes still working are ready, not when `batch` of 64 are, or the tail
     // would wait for the slowest ray of the wave at every bounce.
     const int alive = __popcll(__ballot(mode != M_DONE));
+#if PT_CENSUS
     if (census && seen >= total_slots) {  // (diagnostics: the wave's drain)
       if (census_alive < 0) census_alive = alive;
       ++census_rounds;
     }
+#endif
     int round_batch = min(batch, (3 * alive + 3) / 4);
     if (P.drain_div > 0 && seen >= total_slots)  // the queue is drained: latency, not throughput
       round_batch = max(1, alive / P.drain_div);
@@ -1338,6 +1362,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     PT_STAMP(S_TRAV);
   }
 
+  if (census && lane == 0) census[2] = wall_clock64();
+#if PT_CENSUS
   if (census) {
     // first time a lane of the wave found the queue empty, its lanes alive
     // then, the wave's rounds from then on
@@ -1348,11 +1374,11 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     }
     if (lane == 0) {
       census[1] = e;
-      census[2] = wall_clock64();
       census[4] = (unsigned long long)census_alive;
       census[5] = (unsigned long long)census_rounds;
     }
   }
+#endif
   if (STATS) {
     PT_STAMP(S_OTHER);
     unsigned long long v[11] = {n_cam, n_bounce, n_shadow, ct.nodes, ct.tris, ct.spheres, n_hits,

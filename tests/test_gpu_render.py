@@ -753,6 +753,34 @@ def test_hip_tile_finish_drains_after_a_failed_launch(monkeypatch):
     assert np.array_equal(hdr, whole)
 
 
+def test_render_tiles_device_checks_the_output_size():
+    """render_tiles_device takes a raw device pointer: with out_floats it
+    refuses a buffer smaller than the layout it asked for (a whole frame, or
+    len(tiles) packed 32x32 tiles) BEFORE anything is launched -- round 4's
+    strong companion once wrote a frame-layout render into a packed buffer."""
+    import torch
+    from dsgpuraytracing_amd.pathtracer import Device
+    sc = Scene.from_dump(golden("c1_default_64x64.scene.ptd"))
+    w = h = 64
+    dev = Device(0)
+    dev.upload_scene(sc)
+    dev.set_camera(sc.camera)
+    dev.set_params(w, h, 4, 4, 1, 9)
+    tiles = np.asarray(tile_fifo(w, h), np.int32)[:2]
+    packed = torch.zeros(2 * 1024 * 3, dtype=torch.float32, device="cuda:0")
+    with pytest.raises(ValueError, match="frame layout writes"):
+        dev.render_tiles_device(tiles, packed.data_ptr(), out_floats=packed.numel())
+    dev.render_tiles_device(tiles, packed.data_ptr(), packed=True, out_floats=packed.numel())
+    torch.cuda.synchronize()
+    frame = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda:0")
+    dev.render_tiles_device(tiles, frame.data_ptr(), out_floats=frame.numel())
+    torch.cuda.synchronize()
+    got = packed.view(2, 32, 32, 3).cpu().numpy()
+    ref = frame.cpu().numpy()
+    for i, (x, y, tw, th) in enumerate(tiles):
+        assert np.array_equal(got[i, :th, :tw], ref[y:y + th, x:x + tw])
+
+
 @pytest.mark.parametrize("w,h,threads", [(256, 192, 8), (200, 136, 3)])
 def test_native_seam_bench_bit_identical(w, h, threads):
     """tools/seam_bench.cpp -- C++ std::thread workers calling the one-tile
