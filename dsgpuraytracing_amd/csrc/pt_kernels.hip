@@ -73,6 +73,22 @@ __device__ __forceinline__ void store3(float* p, float3 v) {
   p[1] = v.y;
   p[2] = v.z;
 }
+// A group sum: written once, read once by the resolve.  Non-temporal stores
+// (PT_NT_SUMS=1: no L2 allocation) trade FETCH_SIZE for WRITE_SIZE -- C3
+// -27% / +27%, C5 -6% / +6% -- at throughput within noise (C5 +0.2%, C3 ±0,
+// C4 +0.3%, c5big +0.9%: profiles/r4/ab_nt_sums.txt); left off.
+#ifndef PT_NT_SUMS
+#define PT_NT_SUMS 0
+#endif
+__device__ __forceinline__ void store_sum(float* p, float3 v) {
+#if PT_NT_SUMS
+  __builtin_nontemporal_store(v.x, p);
+  __builtin_nontemporal_store(v.y, p + 1);
+  __builtin_nontemporal_store(v.z, p + 2);
+#else
+  store3(p, v);
+#endif
+}
 // Pixel q (0..1023) of a tile in 8x8 blocks (4 blocks per row); (-1,-1) when
 // it lies outside a ragged tile.
 __device__ __forceinline__ int2 tile_pixel(int4 tile, uint32_t q) {
@@ -834,7 +850,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if (shadow == SH_FOLLOW) {
           if (!tr.found) acc = acc + pend;
         } else {  // the finished group's one store: its total with the light sample if the shadow ray is clear
-          store3(P.partial + 3 * (size_t)oslot, tr.found ? acc : pend);
+          store_sum(P.partial + 3 * (size_t)oslot, tr.found ? acc : pend);
           acc = ng;  // the new group's sum so far (environment seen by its camera rays that missed)
         }
         if (shadow == SH_STORE) {
@@ -1100,7 +1116,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         }
       }
       if (group_end) {
-        store3(P.partial + 3 * (size_t)myslot, acc);
+        store_sum(P.partial + 3 * (size_t)myslot, acc);
         PT_SLOT_DONE();
         mode = M_FETCH;
       }
@@ -1263,7 +1279,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             ng = f3(0, 0, 0);  // (the next group's sum while the store is pending)
             shadow = SH_STORE;
           } else {  // SH_STORE: this group's sum is in ng (acc holds the last group's)
-            store3(P.partial + 3 * (size_t)myslot, shadow ? ng : acc);
+            store_sum(P.partial + 3 * (size_t)myslot, shadow ? ng : acc);
           }
           PT_SLOT_DONE();
           mode = M_FETCH;
