@@ -79,6 +79,8 @@ def main():
         early = start < 100.0
         per_cu = np.bincount(np.unique(cu_key[early], return_inverse=True)[1])
         q = [0, 0.01, 0.1, 0.5, 0.9, 0.99, 1.0]
+        if not tr[:, 1].any():
+            sys.exit("the library has no drain census: build it with PT_HIPCC_FLAGS=-DPT_CENSUS=1")
         emp = np.where(tr[:, 1] != -1, (tr[:, 1] - t0) * 0.01, np.nan)  # (-1: never saw it empty)
         print(json.dumps({"census": True, "waves": len(tr), "kernel_ms": dev.launch_times(1)[0][0].item(),
                           "start_us_quantiles": [round(float(np.quantile(start, x)), 1) for x in q],
