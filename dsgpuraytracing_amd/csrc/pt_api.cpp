@@ -1178,7 +1178,14 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   // (slot indices reach past the end by up to a static chunk plus a claimed one per wave)
   if (slots + 2 * want * PT_CHUNK_MAX >= (int64_t)INT32_MAX) return fail(PT_E_INVALID, "frame too large for one launch");
   pt_fastdiv_init((uint32_t)P.n_groups, &P.grp_m, &P.grp_sh);
-  P.sblocks = P.n_groups % 2 == 0 ? 1 : 0;
+  // queue claims: bigger for frames with many slots per lane (fewer atomics
+  // on the one head; a lone small frame's drain prefers the smaller claim)
+  P.chunk = slots >= (int64_t)PT_CHUNK_BIG_SLOTS * want_plain * PT_BLOCK ? PT_CHUNK_MAX : PT_CHUNK;
+  if (const char* cs = std::getenv("PT_CHUNK_SLOTS")) {  // tuning knob (64..PT_CHUNK_MAX, a multiple of 64)
+    const int v = std::atoi(cs);
+    if (v >= 64 && v <= PT_CHUNK_MAX && v % 64 == 0) P.chunk = v;
+  }
+  P.sblocks = (64 * P.n_groups) % P.chunk == 0 ? 1 : 0;  // every (aligned) chunk inside one block
   // group sums: 12 B per work slot of THIS launch (a rank's share of a split
   // frame holds only its own blocks' sums)
   HIPCHK(c->partial[slot].reserve((size_t)std::max<int64_t>(slots, 1) * 3));

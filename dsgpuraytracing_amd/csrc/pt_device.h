@@ -8,13 +8,13 @@
 #define PT_BLOCK 64  // one wave64 per workgroup: the persistent queue is per wave
 #endif
 #ifndef PT_CHUNK
-#define PT_CHUNK 128  // smallest claim of work slots a wave takes from the queue per atomic
+#define PT_CHUNK 128  // work slots a wave claims from the queue per atomic (KParams.chunk)
 #endif
 #ifndef PT_CHUNK_MAX
-#define PT_CHUNK_MAX 128  // largest claim (guided self-scheduling, see the refill in pt_kernels.hip)
+#define PT_CHUNK_MAX 256  // the claim for frames with >= PT_CHUNK_BIG_SLOTS slots per resident lane
 #endif
-#ifndef PT_CHUNK_DIV
-#define PT_CHUNK_DIV 8u  // a claim is ~1/(PT_CHUNK_DIV * waves) of the slots still unclaimed
+#ifndef PT_CHUNK_BIG_SLOTS
+#define PT_CHUNK_BIG_SLOTS 128  // C4 (184 slots per lane) +1.5%, C5 (1,620) +6.6%; C3 (26), framed C3 (51): their lone launches lose
 #endif
 static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand");
 #define PT_QUEUE_WORDS 32  // the work-queue head, alone in its 128-B line
@@ -155,7 +155,8 @@ struct KParams {
   // j): (b * 64 + q) * n_groups + j -- a pixel's groups are consecutive, so a
   // wave's lanes hold a few pixels' groups (coherent camera rays).
   uint32_t grp_m, grp_sh;           // fastdiv by n_groups (pt_fastdiv)
-  int sblocks;                      // a 128-slot chunk lies in one block (n_groups even): scalar block loads
+  int sblocks;                      // every chunk lies in one block (64 * n_groups a multiple of chunk): scalar block loads
+  int chunk;                        // slots per queue claim (PT_CHUNK or PT_CHUNK_MAX), a multiple of 64
   const int* tile_block0;           // first block of each tile (n_tiles + 1 entries), for the resolve
   const DNode* nodes;
   const DNode2* nodes2;  // the binary tree (reference-count launch only)

@@ -1131,13 +1131,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       bool need = mode == M_FETCH;
       unsigned long long m = __ballot(need);
       if (m != 0ull) {
-        // Lanes are served from the wave's private chunk of consecutive slots;
-        // one atomic refills it.  Guided self-scheduling: a chunk is about
-        // 1/(PT_CHUNK_DIV * waves) of the slots still unclaimed (as last seen), between
-        // PT_CHUNK and PT_CHUNK_MAX, so early chunks are large (few atomics on
-        // the one queue head, which sits memory-side since the XCD L2s are
-        // not coherent) and the tail is handed out 64 slots at a time.
-        // (One queue per XCD over bands of the frame measured C3 -9%.)
+        // Lanes are served from the wave's private chunk of P.chunk
+        // consecutive slots; one atomic on the one queue head (memory-side,
+        // since the XCD L2s are not coherent) refills it.  128 slots, 256 for
+        // launches with >= 128 slots per lane (half the atomics: C5 +6.6%, C4
+        // +1.5%), chosen on the host (profiles/r4/ab_chunk_claims.txt).  (One queue per XCD
+        // over bands of the frame measured C3 -9%.)
         uint32_t cnt = (uint32_t)__popcll(m);
         uint32_t avail = chunk_end - chunk_next;
         uint32_t nbase = 0, csize = 0;
@@ -1154,16 +1153,15 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             // the launch's start every wave would otherwise queue on the one
             // head at once (memory-side atomics, serialised), and the last
             // ones would wait for thousands of others before their first ray.
-            csize = PT_CHUNK_MAX;
-            nbase = wave_id * (uint32_t)PT_CHUNK_MAX;
+            csize = (uint32_t)P.chunk;
+            nbase = wave_id * csize;
             seen = nbase + csize;
             first_claim = false;
           } else {
-            const uint32_t left = total_slots - seen;
-            csize = min((uint32_t)PT_CHUNK_MAX, max((uint32_t)PT_CHUNK, left / (PT_CHUNK_DIV * n_waves))) & ~63u;
+            csize = (uint32_t)P.chunk;
             if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
             // (the head counts the chunks after the statically dealt ones)
-            nbase = __builtin_amdgcn_readfirstlane(__shfl(nbase, 0)) + (PT_STATIC_FIRST ? n_waves * (uint32_t)PT_CHUNK_MAX : 0u);
+            nbase = __builtin_amdgcn_readfirstlane(__shfl(nbase, 0)) + (PT_STATIC_FIRST ? n_waves * csize : 0u);
             seen = nbase + csize;
             if (STATS) n_atomics += lane == 0;
           }
