@@ -275,7 +275,7 @@ int pt_create(int device, pt_ctx** out) {
     HIPCHK(hipStreamCreateWithFlags(&c->rstream[k], hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
     HIPCHK(hipEventRecord(c->ev_free[k], c->stream));
-    HIPCHK(c->counter[k].reserve(PT_QUEUE_WORDS));  // work-queue heads, one 128-B line each
+    HIPCHK(c->counter[k].reserve(PT_QUEUE_WORDS * PT_QUEUE_HEADS));  // work-queue heads, one 128-B line each
   }
   for (auto& tri : c->ev)
     for (auto& e : tri) HIPCHK(hipEventCreate(&e));
@@ -1035,7 +1035,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     HIPCHK(c->tiles[slot].reserve(tl.size()));
     HIPCHK(hipMemcpyAsync(c->tiles[slot].p, th.data(), th.size() * sizeof(int4), hipMemcpyHostToDevice, rs));
   }
-  HIPCHK(hipMemsetAsync(c->counter[slot].p, 0, PT_QUEUE_WORDS * sizeof(uint32_t), rs));
+  HIPCHK(hipMemsetAsync(c->counter[slot].p, 0, PT_QUEUE_WORDS * PT_QUEUE_HEADS * sizeof(uint32_t), rs));
   if (stats) {
     unsigned long long init[PT_STATS_SLOTS] = {0};
     init[21] = init[23] = init[25] = ~0ull;  // atomicMin slots

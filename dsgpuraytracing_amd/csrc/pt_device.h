@@ -17,7 +17,10 @@
 #define PT_CHUNK_BIG_SLOTS 128  // C4 (184 slots per lane) +1.5%, C5 (1,620) +6.6%; C3 (26), framed C3 (51): their lone launches lose
 #endif
 static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand");
-#define PT_QUEUE_WORDS 32  // the work-queue head, alone in its 128-B line
+#define PT_QUEUE_WORDS 32  // a work-queue head, alone in its 128-B line
+#ifndef PT_QUEUE_HEADS
+#define PT_QUEUE_HEADS 1  // queue heads, interleaved chunk by chunk (8, one per XCD: C5 +2%, C3 / C4 / framed C3 -0.5..-1%; off)
+#endif
 #ifndef PT_GROUP_SPP
 #define PT_GROUP_SPP 4  // default samples per work slot (pt_api.cpp group_size; 8 or more: C3 -4%, C5 -10%)
 #endif

@@ -782,6 +782,10 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   uint32_t chunk_next = 0, chunk_end = 0;  // the wave's private range of work slots
   uint32_t seen = 0;                       // queue head after this wave's last claim
   bool first_claim = true;                 // the first chunk is the wave's own (no atomic)
+#if PT_QUEUE_HEADS > 1
+  // the queue head this wave claims from: its XCD's (HW_REG_XCC_ID), until that one runs dry
+  uint32_t qh = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) % PT_QUEUE_HEADS;
+#endif
   const unsigned long long w_start = STATS ? wall_clock64() : 0ull;
   // Residency census of the plain build (PT_CENSUS set, diagnostics): when
   // each wave started and ended, and where it ran -- which waves of the grid
@@ -1159,9 +1163,30 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             first_claim = false;
           } else {
             csize = (uint32_t)P.chunk;
+#if PT_QUEUE_HEADS > 1
+            const uint32_t base0 = PT_STATIC_FIRST ? n_waves * csize : 0u;  // (after the statically dealt chunks)
+            // PT_QUEUE_HEADS heads, one per XCD, each in its own 128-B line:
+            // head h deals chunks h, h + H, h + 2H, ... -- the same interleaved
+            // sweep of the frame as one head, with 1/H of the atomics on each
+            // line.  A wave whose head ran dry moves on to the next one.
+            nbase = total_slots;
+            for (int t = 0; t < PT_QUEUE_HEADS; ++t) {  // (wave-uniform; one pass but at the very end)
+              uint32_t r = 0;
+              if (lane == 0) r = atomicAdd(P.work_counter + qh * PT_QUEUE_WORDS, 1u);
+              r = __builtin_amdgcn_readfirstlane(__shfl(r, 0));
+              const uint64_t cand = (uint64_t)base0 + ((uint64_t)r * PT_QUEUE_HEADS + qh) * csize;
+              if (cand < (uint64_t)total_slots) {
+                nbase = (uint32_t)cand;
+                break;
+              }
+              qh = (qh + 1u) % PT_QUEUE_HEADS;
+            }
+            if (nbase >= total_slots) csize = 0;  // every head ran dry: drained
+#else
             if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
             // (the head counts the chunks after the statically dealt ones)
             nbase = __builtin_amdgcn_readfirstlane(__shfl(nbase, 0)) + (PT_STATIC_FIRST ? n_waves * csize : 0u);
+#endif
             seen = nbase + csize;
             if (STATS) n_atomics += lane == 0;
           }
