@@ -201,6 +201,25 @@ def test_hip_deterministic_and_tile_assignment_independent():
     assert (one[:64] == 0).all()
 
 
+@pytest.mark.parametrize("scene,w,h", [("c1_default_128x128", 128, 128), ("c1env_64x64", 64, 64)])
+def test_hip_queue_claim_size_never_changes_values(monkeypatch, scene, w, h):
+    """The queue's claim size (PT_CHUNK_SLOTS; 128, or 256 for launches with
+    many slots per lane) decides only which wave renders which slots: images
+    are bit-identical for every claim size, also with the launch split into
+    tile shards."""
+    ref, _ = gpu_render(scene, w, h, 16, seed=13)
+    tiles = tile_fifo(w, h)
+    for c in ("64", "128", "256"):
+        monkeypatch.setenv("PT_CHUNK_SLOTS", c)
+        img, _ = gpu_render(scene, w, h, 16, seed=13)
+        assert np.array_equal(img, ref), c
+        parts = np.zeros_like(ref)
+        for shard in range(2):
+            p, _ = gpu_render(scene, w, h, 16, seed=13, tiles=tiles[shard::2])
+            parts += p
+        assert np.array_equal(parts, ref), c
+
+
 @pytest.mark.parametrize("scene,w,h", [("c1_default_128x128", 128, 128), ("c1_sphcam_96x64", 96, 64),
                                        ("CBspheres_64x64", 64, 64)])
 def test_screen_footprint_culling_is_exact(monkeypatch, scene, w, h):
