@@ -51,11 +51,13 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #define PT_LDS_LIGHTS 8
 #endif
 // leaf steps when leaf lanes >= node lanes * 16 / leaf weight; with 32-lane
-// shading rounds 10 beats 16 (C3 +1.9%, framed C3 +1.8%, C4 +1.4%); C5 (the
+// shading rounds 10 beat 16 (C3 +1.9%, framed C3 +1.8%, C4 +1.4%); C5 (the
 // environment-light build) is flat between 10 and 16 and keeps 16
-// (profiles/r3/ab_leaf_weight.txt)
+// (profiles/r3/ab_leaf_weight.txt).  Round 4, with two-sample groups on C3:
+// 12 over 10, C3 +0.8% and its lone launch -0.9%, C4 / framed C3 flat
+// (profiles/r4/ab_knobs_batch_leaf.txt)
 #ifndef PT_LEAF_WEIGHT
-#define PT_LEAF_WEIGHT 10
+#define PT_LEAF_WEIGHT 12
 #endif
 #ifndef PT_LEAF_WEIGHT_ENV
 #define PT_LEAF_WEIGHT_ENV 16
