@@ -167,7 +167,9 @@ struct pt_ctx {
   bool census_valid = false;  // the last launch was a PT_CENSUS plain launch (its trace area holds start/end/CU)
   bool times_pending = false;  // c->last's times belong to a launch not yet synchronised
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;  // the current launch's triple
-  DevBuf<DNode> nodes;
+  DevBuf<DNode> nodes;    // the render tree, PT_NODE_WIDTH 4
+  DevBuf<DNode8> nodes8;  // the render tree, PT_NODE_WIDTH 8 (+ children 4..7's references)
+  DevBuf<int4> nodes8_hi;
   DevBuf<DNode2> nodes2;  // binary tree for PT_FLAG_REF_COUNTS
   DevBuf<int> prim_map;   // own BVH order (SAH or GPU-built) -> uploaded primitive index (else empty)
   // primitives in the caller's (reference BVH) order, for the reference-count
@@ -245,7 +247,7 @@ struct pt_ctx {
   DevBuf<int32_t> q_i;
   int n_lights = 0, n_bsdfs = 0;
   int bvh_stack = 0;  // worst-case traversal stack entries of the uploaded BVH
-  size_t n_nodes4 = 0;
+  size_t n_render_nodes = 0;
   int64_t n_prims = 0;
   float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
   double root_lo_d[3] = {0, 0, 0}, root_hi_d[3] = {0, 0, 0};
@@ -309,6 +311,8 @@ int pt_destroy(pt_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();  // no render of this context may still be running
   c->nodes.release();
+  c->nodes8.release();
+  c->nodes8_hi.release();
   c->nodes2.release();
   c->prim_map.release();
   c->env_tex.release();
@@ -588,6 +592,19 @@ static int build_host_bvh(const pt_scene* s, std::vector<DNode>& dn, std::vector
   return PT_OK;
 }
 
+// The 8-wide render tree from a binary tree already on the device
+// (ptk_build_wide): replaces c->nodes8 / c->nodes8_hi; the worst-case
+// traversal stack goes to *max_stack.
+static int build_wide(pt_ctx* c, const DNode2* bin_dev, int n_bin, int* max_stack) {
+  WideOut w{};
+  HIPCHK(ptk_build_wide(bin_dev, n_bin, &w, c->stream));
+  c->nodes8.adopt(w.nodes, (size_t)std::max(1, w.n));
+  c->nodes8_hi.adopt(w.hi, (size_t)std::max(1, w.n));
+  c->n_render_nodes = (size_t)w.n;
+  *max_stack = w.max_stack;
+  return PT_OK;
+}
+
 // GPU linear-BVH build over the primitives already in c->prims / c->norms
 // (CUDAPathTracer::buildBVH, cuda_src/setup.cu:478-686; kernels in lbvh.hip).
 static int build_gpu_bvh(pt_ctx* c, const pt_scene* s) {
@@ -619,11 +636,16 @@ static int build_gpu_bvh(pt_ctx* c, const pt_scene* s) {
   c->prim_map.adopt(out.prim_map, (size_t)in.n);
   c->nodes.adopt(out.nodes4, (size_t)out.n4);
   c->nodes2.adopt(out.nodes2, (size_t)std::max(1, out.n2));
+  c->n_render_nodes = (size_t)out.n4;
+#if PT_NODE_WIDTH == 8
+  // (the BVH4 emission still numbers the primitives in depth-first leaf order,
+  // which the binary nodes' leaf cursors refer to)
+  if (int rc = build_wide(c, out.nodes2, std::max(1, out.n2), &out.max_stack)) return rc;
+#endif
   if (out.max_stack > PT_STACK_MAX)
     return fail(PT_E_INVALID, "pt_upload_scene_lbvh: BVH needs a deeper traversal stack (" +
                                   std::to_string(out.max_stack) + " > " + std::to_string(PT_STACK_MAX) + ")");
   c->bvh_stack = out.max_stack;
-  c->n_nodes4 = (size_t)out.n4;
   for (int k = 0; k < 3; ++k) {
     c->root_lo[k] = out.root_lo[k];
     c->root_hi[k] = out.root_hi[k];
@@ -810,6 +832,19 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
     int max_stack = 0;
     int rc = build_host_bvh(s, dn, d2, max_stack);
     if (rc) return rc;
+#if PT_NODE_WIDTH == 8
+    {  // the 8-wide render tree from the host tree's binary nodes, collapsed on the device
+      DevBuf<DNode2> bin;
+      HIPCHK(bin.reserve(d2.size()));
+      HIPCHK(hipMemcpy(bin.p, d2.data(), d2.size() * sizeof(DNode2), hipMemcpyHostToDevice));
+      rc = build_wide(c, bin.p, (int)d2.size(), &max_stack);
+      bin.release();
+      if (rc) return rc;
+      if (max_stack > PT_STACK_MAX)
+        return fail(PT_E_INVALID, "pt_upload_scene: BVH needs a deeper traversal stack (" + std::to_string(max_stack) +
+                                      " > " + std::to_string(PT_STACK_MAX) + ")");
+    }
+#endif
     if (s != s0) {  // the reference-count launch walks the caller's (reference) tree
       std::vector<DNode> dn0;
       int ms0 = 0;
@@ -827,7 +862,9 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
       HIPCHK(hipMemcpy(c->prim_map.p, pm.data(), pm.size() * sizeof(int), hipMemcpyHostToDevice));
     }
     c->bvh_stack = max_stack;
-    c->n_nodes4 = dn.size();
+#if PT_NODE_WIDTH == 4
+    c->n_render_nodes = dn.size();
+#endif
     const pt_bvh_node* N = s->nodes;
     for (int k = 0; k < 3; ++k) {
       c->root_lo[k] = round_down(N[0].bb_min[k]);
@@ -1066,6 +1103,8 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.n_bsdfs = c->n_bsdfs;
   P.n_tiles = (int)tl.size();
   P.nodes = c->nodes.p;
+  P.nodes8 = c->nodes8.p;
+  P.nodes8_hi = c->nodes8_hi.p;
   P.nodes2 = c->nodes2.p;
   P.prims = c->prims.p;
   P.norms = c->norms.p;
@@ -1231,7 +1270,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   for (const int4& t : tl) px += (int64_t)t.z * t.w;
   c->last.pixels = px;
   c->last.bvh_stack = c->bvh_stack;
-  c->last.bvh_nodes = (int64_t)c->n_nodes4;
+  c->last.bvh_nodes = (int64_t)c->n_render_nodes;
   c->last.samples = px * c->params.spp;
   return PT_OK;
 }
@@ -1584,7 +1623,8 @@ int pt_intersect(pt_ctx* c, int64_t n, const double* o, const double* d, const d
     HIPCHK(c->q_spill.reserve((size_t)(c->bvh_stack - PT_STACK) * (size_t)((n + PT_BLOCK - 1) / PT_BLOCK * PT_BLOCK)));
     spill = c->q_spill.p;
   }
-  HIPCHK(ptk_launch_intersect(c->nodes.p, c->prims.p, c->q_f.p, c->q_f.p + 3 * n, c->q_f.p + 6 * n, n, dh, dt, dp, da,
+  const void* rnodes = PT_NODE_WIDTH == 8 ? (const void*)c->nodes8.p : (const void*)c->nodes.p;
+  HIPCHK(ptk_launch_intersect(rnodes, c->nodes8_hi.p, c->prims.p, c->q_f.p, c->q_f.p + 3 * n, c->q_f.p + 6 * n, n, dh, dt, dp, da,
                               spill, c->prim_map.p, c->stream));
   std::vector<int32_t> ib((size_t)n * 3);
   std::vector<float> tb((size_t)n);
@@ -1598,6 +1638,37 @@ int pt_intersect(pt_ctx* c, int64_t n, const double* o, const double* d, const d
     if (t) t[i] = tb[(size_t)i];
   }
   return PT_OK;
+}
+
+// Host replay of the environment light's inverse-CDF searches (the kernel's
+// record_lower_bound over the tables build_env_tables makes) against
+// std::lower_bound, for n query pairs (u1, u2) in [0, 1): the row search over
+// pTheta, then the column search over that row of pPhiGivenTheta, each checked
+// for the index and the interpolation pair (prev, cur) the sampler reads.
+int64_t pt_env_search_check(const float* rgb, int32_t width, int32_t height, int64_t n, const float* u1,
+                            const float* u2, int64_t* long_windows) {
+  if (!rgb || width <= 0 || height <= 0 || n < 0 || (n > 0 && (!u1 || !u2)))
+    return fail(PT_E_INVALID, "pt_env_search_check: bad arguments");
+  EnvTables t;
+  build_env_tables(rgb, width, height, t);
+  int64_t bad = 0, longw = 0;
+  auto check = [&](const float* a, int len, const EnvRec* rec, float u) -> int {
+    const float v = u * a[len - 1];
+    const int k = std::min(PT_ENV_GUIDE - 1, std::max(0, (int)(u * (float)PT_ENV_GUIDE)));
+    longw += rec[k].hi - rec[k].lo > 4;
+    float prev = 0.f, cur = 0.f;
+    const int got = record_lower_bound(a, v, u, rec, PT_ENV_GUIDE, prev, cur);
+    const int want = (int)(std::lower_bound(a, a + len, v) - a);
+    const float wcur = a[std::min(want, len - 1)], wprev = want > 0 ? a[want - 1] : 0.0f;
+    if (got != want || std::memcmp(&cur, &wcur, 4) != 0 || std::memcmp(&prev, &wprev, 4) != 0) ++bad;
+    return std::min(got, len - 1);
+  };
+  for (int64_t i = 0; i < n; ++i) {
+    const int row = check(t.p_theta.data(), height, t.r_theta.data(), u1[i]);
+    check(&t.p_phi[(size_t)row * width], width, &t.r_phi[(size_t)row * PT_ENV_GUIDE], u2[i]);
+  }
+  if (long_windows) *long_windows = longw;
+  return bad;
 }
 
 int pt_get_stats(pt_ctx* c, pt_stats* out) {

@@ -67,11 +67,63 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 // memory round trip: the window [lo, hi] = [g[k-1], g[k+2]] of the guide
 // table g, and the window's values w_i = a[min(lo + i, hi)] (i < 4), w4 =
 // a[hi], wm = a[lo - 1] (0 at lo = 0).  Windows longer than four entries
-// (hi - lo > 4) are halved on the array itself.
+// (hi - lo > 4) are halved on the array itself (record_lower_bound).
 struct alignas(32) EnvRec {
   int lo, hi;
   float wm, w0, w1, w2, w3, w4;
 };
+
+// lower_bound of v = r * a[n-1] accelerated by a guide table g[0..G] with
+// g[k] = lower_bound(a, k/G * a[n-1]) (built on the host, clamped to n-1): the
+// answer lies in [g[k-1], g[k+2]] for k = floor(r*G), one bucket of slack
+// either side for rounding, and a[g[k+2]] >= v; the result is exactly
+// std::lower_bound's.  With PT_ENV_GUIDE buckets the window is a few entries
+// where the CDF carries mass (where samples land).  Bucket k's record (EnvRec)
+// holds the window and its values, so the usual short window (<= 4 entries)
+// costs ONE memory round trip -- two 16-B loads of one 32-B record -- and
+// lower_bound = lo + #{entries < v} (the array is sorted); the caller's
+// interpolation pair (prev = a[t-1] or 0, cur = a[t]) comes from the same
+// registers.  A longer window -- where the CDF is nearly flat (dim regions of
+// a peaky map) or the map is wider than the guide table (w > PT_ENV_GUIDE:
+// several entries per bucket) -- is halved on the array down to <= 4 entries
+// (answer in [lo, lo + n]) and its five values re-read.  (Guide table, then
+// window: two dependent round trips, C5 -1.9%: profiles/r4/ab_env_records.txt.)
+// Host and device: pt_env_search_check (pt_api.cpp) replays it against
+// std::lower_bound on the host (tests/test_env_search.py).
+__host__ __device__ inline int record_lower_bound(const float* __restrict__ a, float v, float r,
+                                                  const EnvRec* __restrict__ rec, int G, float& prev, float& cur) {
+  int k = (int)(r * (float)G);
+  k = k < 0 ? 0 : k > G - 1 ? G - 1 : k;
+  // one 32-B copy of the record (two 16-B loads on the device).  (Reading it as
+  // two float4 and bit-casting the int fields out of their elements misread
+  // the window in host code -- clang's __builtin_bit_cast of a vector element
+  // returns element 0 there -- which the host replay caught.)
+  EnvRec e;
+  __builtin_memcpy(&e, rec + k, sizeof(EnvRec));
+  int lo = e.lo;
+  const int hi = e.hi;
+  float wm = e.wm, w0 = e.w0, w1 = e.w1, w2 = e.w2, w3 = e.w3, w4 = e.w4;
+  int n = hi - lo;
+  if (n > 4) {
+    while (n > 4) {
+      const int half = n >> 1;
+      if (a[lo + half] < v) {
+        lo += half + 1;
+        n -= half + 1;
+      } else {
+        n = half;
+      }
+    }
+    auto at = [&](int i) { return a[i < hi ? i : hi]; };
+    wm = lo > 0 ? a[lo - 1] : 0.0f;
+    w0 = at(lo), w1 = at(lo + 1), w2 = at(lo + 2), w3 = at(lo + 3);
+    w4 = at(lo + 4);  // (the record's w4 is a[hi] of the WHOLE window: ADVICE r4)
+  }
+  const int c = (int)(w0 < v) + (int)(w1 < v) + (int)(w2 < v) + (int)(w3 < v);
+  cur = c == 0 ? w0 : c == 1 ? w1 : c == 2 ? w2 : c == 3 ? w3 : w4;
+  prev = c == 0 ? wm : c == 1 ? w0 : c == 2 ? w1 : c == 3 ? w2 : w3;
+  return lo + c;
+}
 // The drain fields of the census of plain launches (tools/wave_trace.py
 // --census) are compiled in only with -DPT_CENSUS=1 (PT_HIPCC_FLAGS): their
 // bookkeeping in the persistent loop cost C3 2% even when off
@@ -88,7 +140,7 @@ struct alignas(32) EnvRec {
 #define PT_STACK 24  // traversal stack entries per lane in LDS (lane-contiguous)
 #endif
 #ifndef PT_STACK_MAX
-#define PT_STACK_MAX 128  // deepest worst-case stack accepted (entries past PT_STACK spill to global memory)
+#define PT_STACK_MAX 256  // deepest worst-case stack accepted (entries past PT_STACK spill to global memory; 8-wide nodes push up to 7 per level)
 #endif
 
 // BVH4 node, 128 B (one L2 line): four child boxes in SoA form, component k
@@ -101,6 +153,31 @@ struct alignas(16) DNode {
   int4 ref;
   int4 pad;
 };
+
+// Node width of the render tree: 8 (DNode8, round 5) or 4 (DNode, rounds 1-4;
+// kept as the A/B arm, -DPT_NODE_WIDTH=4).
+#ifndef PT_NODE_WIDTH
+#define PT_NODE_WIDTH 4
+#endif
+static_assert(PT_NODE_WIDTH == 4 || PT_NODE_WIDTH == 8, "PT_NODE_WIDTH is 4 or 8");
+
+// BVH8 node, 128 B (one L2 line): eight child boxes quantised to fp16 offsets
+// from the node's origin (Ylitie et al. 2017 style, with fp16 instead of 8-bit
+// codes so that a plane decodes with ONE v_fma_mix_f32 and no conversion):
+//   plane = origin[a] + q * 2^e[a], q an fp16 (lox..hiz component k = child k),
+// lo planes rounded down and hi planes rounded up (the quantised box contains
+// the child's float box); then the references of children 0..3.  Children
+// 4..7's references live in a side array (one int4 per node, KParams.nodes8_hi), so a node
+// step is 9 16-B loads over 1.125 lines.  References as DNode.ref (node index
+// or leaf cursor); empty slots hold the inverted box (lo = +inf, hi = -inf),
+// which no ray enters.
+struct alignas(16) DNode8 {
+  float ox, oy, oz;  // origin: the lower corner of the union of the child boxes
+  uint32_t ex;       // per-axis scale exponents, signed bytes 0 (x), 1 (y), 2 (z)
+  uint4 lox, hix, loy, hiy, loz, hiz;  // 8 fp16 each
+  int4 ref;          // children 0..3
+};
+static_assert(sizeof(DNode8) == 128, "DNode8 is one 128-B line");
 
 // Binary node of the reference topology, 64 B: both child boxes + child
 // references (as DNode.ref).  Only traversed by the reference-count launch
@@ -151,7 +228,7 @@ struct KParams {
   int n_bsdfs;
   int n_tiles;     // 32x32 (or smaller) tiles: 1024 pixels each
   // Sample groups (work slots) of a pixel, a function of the frame only
-  // (launch(): pt_api.cpp group_layout): group j holds samples
+  // (launch(): pt_api.cpp group_size): group j holds samples
   // [j * group_spp, min((j + 1) * group_spp, spp)).
   int group_spp;   // samples per work slot
   int group_shift;   // log2(group_spp) when a power of two, else -1 (shifts instead of divisions)
@@ -163,7 +240,9 @@ struct KParams {
   int sblocks;                      // every chunk lies in one block (64 * n_groups a multiple of chunk): scalar block loads
   int chunk;                        // slots per queue claim (PT_CHUNK or PT_CHUNK_MAX), a multiple of 64
   const int* tile_block0;           // first block of each tile (n_tiles + 1 entries), for the resolve
-  const DNode* nodes;
+  const DNode* nodes;     // the render tree, PT_NODE_WIDTH 4
+  const DNode8* nodes8;   // the render tree, PT_NODE_WIDTH 8
+  const int4* nodes8_hi;  // its children 4..7's references
   const DNode2* nodes2;  // the binary tree (reference-count launch only)
   const DPrim* prims;
   const float* norms;  // 9 floats per primitive (vertex normals n1,n2,n3)
@@ -236,9 +315,22 @@ struct LbvhOut {
 };
 extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t s);
 
+// 8-wide render tree (DNode8) collapsed on the device from a binary tree in
+// DNode2 form (bin[0] the root; child references >= 0 index bin, < 0 are leaf
+// cursors), opening the largest-area internal child until eight children.
+// Outputs hipMalloc'd (the caller owns them).
+struct WideOut {
+  DNode8* nodes;
+  int4* hi;       // children 4..7's references, one int4 per node
+  int n;
+  int max_stack;  // worst-case traversal stack
+};
+extern "C" hipError_t ptk_build_wide(const DNode2* bin, int n_bin, WideOut* out, hipStream_t s);
+
 extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, bool ref_counts, hipStream_t s);
 extern "C" hipError_t ptk_launch_resolve(const KParams* P, hipStream_t s);
-extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prims, const float* o, const float* d,
+// nodes: DNode (PT_NODE_WIDTH 4) or DNode8 (8, with nodes_hi)
+extern "C" hipError_t ptk_launch_intersect(const void* nodes, const int4* nodes_hi, const DPrim* prims, const float* o, const float* d,
                                            const float* maxt, int64_t n, int32_t* hit, float* t, int32_t* prim,
                                            int32_t* anyhit, int* spill, const int* prim_map, hipStream_t s);
 extern "C" hipError_t ptk_render_occupancy(int* waves_per_cu, bool stats, bool env, bool gtab);

@@ -162,20 +162,26 @@ struct Counters {
 // The closest hit is (tmax, prim): the shading round rebuilds the barycentrics
 // and reads the material from the primitive record, so no more of the hit is
 // carried through traversal (every persistent value costs a VGPR in all waves).
+// The ray keeps its reciprocal direction only: the direction is re-derived
+// where a primitive test or the shading round needs it (tdir, three v_rcp_f32),
+// which frees three VGPRs in every wave (round 5: the 8-wide node step's nine
+// loads and per-node coefficients would otherwise spill).  Every consumer
+// derives it the same way, so the hit record's barycentrics still equal the
+// traversal test's bit for bit.
 struct Trav {
-  float3 o, d, inv;
+  float3 o, inv;
   float tmax;
   int node, sp;
   int prim;
   bool any, found;
 };
+__device__ __forceinline__ float3 tdir(const Trav& t) { return f3(rcp(t.inv.x), rcp(t.inv.y), rcp(t.inv.z)); }
 
 __device__ __forceinline__ void trav_init(Trav& tr, float3 o, float3 d, float tmax, bool any) {
   const float kTiny = 1e-20f;
   float3 dd = f3(fabsf(d.x) < kTiny ? copysignf(kTiny, d.x) : d.x, fabsf(d.y) < kTiny ? copysignf(kTiny, d.y) : d.y,
                  fabsf(d.z) < kTiny ? copysignf(kTiny, d.z) : d.z);
   tr.o = o;
-  tr.d = d;
   tr.inv = f3(rcp(dd.x), rcp(dd.y), rcp(dd.z));
   tr.tmax = tmax;
   tr.node = 0;
@@ -206,7 +212,7 @@ __device__ __forceinline__ float mt_terms(float3 o, float3 d, float3 V0, float3 
 template <bool STATS>
 __device__ __forceinline__ bool prim_test(const float4 v0, const float4 e1, const float4 e2, int pi, Trav& tr,
                                           Counters& ct) {
-  const float3 o = tr.o, d = tr.d;
+  const float3 o = tr.o, d = tdir(tr);
   const int meta = __float_as_int(v0.w);
   float t, u = 0.0f, v = 0.0f;
   if (meta & 1) {  // triangle: Moller-Trumbore; u,v >= 0, u+v <= 1, 0 < t < tmax
@@ -411,6 +417,114 @@ __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, const
   return node_order(stk, tr, d, rf);
 }
 
+// 8-wide node step (DNode8, round 5; Ylitie et al. 2017 style, fp16 planes).
+// A plane decodes as t = q * (2^e * inv) + (origin - o) * inv: per node the
+// three scales a = ldexp(inv, e) and offsets b, per plane ONE v_fma_mix_f32
+// (the fp16 operand is read from its half of the dword by op_sel, no
+// conversion).  Near
+// and far planes are picked by the ray's direction signs through the load
+// addresses, as in node_step.  Child order: continue with the NEAREST entered
+// child, push the other entered ones in slot order (lowest slot on top) --
+// the traversal census of the C3 ray mix (tools/wide_sim.cpp)
+// gives the same node and leaf steps per ray as a full distance sort (4.97 vs
+// 4.96 camera, 5.57 vs 5.53 bounce, 4.43 vs 4.44 shadow) for a third of its
+// VALU: rays enter 1.03 children per node on average.  Nine 16-B loads: the
+// header, six plane vectors (8 halves each), two reference vectors.
+typedef _Float16 pt_h8 __attribute__((ext_vector_type(8)));
+template <bool STATS, bool ROOT = false>
+__device__ __forceinline__ bool node_step8(const DNode8* __restrict__ nodes, const int4* __restrict__ nodes_hi,
+                                           const Stack& stk, Trav& tr, Counters& ct, lds_cchar* root = nullptr) {
+  const float kRobust = PT_ROBUST;
+  const float3 o = tr.o, inv = tr.inv;
+  const uint32_t sx = (__float_as_uint(inv.x) >> 27) & 16u, sy = (__float_as_uint(inv.y) >> 27) & 16u,
+                 sz = (__float_as_uint(inv.z) >> 27) & 16u;
+  pt_v4i hd, nx, fx, ny, fy, nz, fz, r0, r1;
+  if constexpr (ROOT) {
+    typedef __attribute__((address_space(3))) const pt_v4i lds_v4i;
+    hd = *(lds_v4i*)root;
+    nx = *(lds_v4i*)(root + (16u + sx));
+    fx = *(lds_v4i*)(root + (16u + (sx ^ 16u)));
+    ny = *(lds_v4i*)(root + (48u + sy));
+    fy = *(lds_v4i*)(root + (48u + (sy ^ 16u)));
+    nz = *(lds_v4i*)(root + (80u + sz));
+    fz = *(lds_v4i*)(root + (80u + (sz ^ 16u)));
+    r0 = *(lds_v4i*)(root + 112u);
+    r1 = *(lds_v4i*)(root + 128u);
+  } else {
+    const char* nb = (const char*)nodes;
+    const uint32_t base = (uint32_t)tr.node << 7;
+    hd = *(const pt_v4i*)(nb + base);
+    nx = *(const pt_v4i*)(nb + (base + 16u + sx));
+    fx = *(const pt_v4i*)(nb + (base + 16u + (sx ^ 16u)));
+    ny = *(const pt_v4i*)(nb + (base + 48u + sy));
+    fy = *(const pt_v4i*)(nb + (base + 48u + (sy ^ 16u)));
+    nz = *(const pt_v4i*)(nb + (base + 80u + sz));
+    fz = *(const pt_v4i*)(nb + (base + 80u + (sz ^ 16u)));
+    r0 = *(const pt_v4i*)(nb + (base + 112u));
+    r1 = *(const pt_v4i*)((const char*)nodes_hi + ((uint32_t)tr.node << 4));
+    asm volatile("" : "+v"(fz), "+v"(r0), "+v"(r1));
+  }
+  if (STATS) ct.nodes++;
+  const uint32_t ew = (uint32_t)hd.w;
+  const float ax = __builtin_amdgcn_ldexpf(inv.x, (int)(int8_t)(ew & 0xffu));
+  const float ay = __builtin_amdgcn_ldexpf(inv.y, (int)(int8_t)((ew >> 8) & 0xffu));
+  const float az = __builtin_amdgcn_ldexpf(inv.z, (int)(int8_t)((ew >> 16) & 0xffu));
+  const float bx = (__int_as_float(hd.x) - o.x) * inv.x;
+  const float by = (__int_as_float(hd.y) - o.y) * inv.y;
+  const float bz = (__int_as_float(hd.z) - o.z) * inv.z;
+  const pt_h8 NX = __builtin_bit_cast(pt_h8, nx), FX = __builtin_bit_cast(pt_h8, fx);
+  const pt_h8 NY = __builtin_bit_cast(pt_h8, ny), FY = __builtin_bit_cast(pt_h8, fy);
+  const pt_h8 NZ = __builtin_bit_cast(pt_h8, nz), FZ = __builtin_bit_cast(pt_h8, fz);
+  const int ref[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+  bool hit[8];
+  float dmin = __builtin_inff();
+  int rn = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float tn = fmaxf(fmaxf(fmaf((float)NX[k], ax, bx), fmaf((float)NY[k], ay, by)),
+                           fmaxf(fmaf((float)NZ[k], az, bz), 0.0f));
+    const float tf = fminf(fminf(fmaf((float)FX[k], ax, bx), fmaf((float)FY[k], ay, by)),
+                           fminf(fmaf((float)FZ[k], az, bz), tr.tmax)) * kRobust;
+    hit[k] = tn <= tf;
+    const bool nearer = hit[k] && tn < dmin;
+    dmin = nearer ? tn : dmin;
+    rn = nearer ? ref[k] : rn;
+  }
+  if (dmin == __builtin_inff()) return trav_pop(stk, tr);
+  // push the other entered children, slot 7 first (lowest slot on top); with
+  // room for eight entries every candidate is written and the top advances
+  // only past pushed ones (no branches)
+  int sp = tr.sp;
+  if (sp + 8 <= PT_STACK) {
+#pragma unroll
+    for (int k = 7; k >= 0; --k) {
+      stk.lds[sp * PT_BLOCK] = ref[k];
+      sp += hit[k] && ref[k] != rn;
+    }
+  } else {
+#pragma unroll
+    for (int k = 7; k >= 0; --k)
+      if (hit[k] && ref[k] != rn) stk.put(sp++, ref[k]);
+  }
+  tr.sp = sp;
+  tr.node = rn;
+  return false;
+}
+
+// The render tree's node step: 8-wide (DNode8 + nodes_hi) or 4-wide (DNode).
+template <bool STATS, bool ROOT = false>
+__device__ __forceinline__ bool node_stepw(const void* __restrict__ nodes, const int4* __restrict__ nodes_hi,
+                                           const Stack& stk, Trav& tr, Counters& ct, lds_cchar* root = nullptr) {
+#if PT_NODE_WIDTH == 8
+  return node_step8<STATS, ROOT>((const DNode8*)nodes, nodes_hi, stk, tr, ct, root);
+#else
+  (void)nodes_hi;
+  return node_step<STATS, ROOT>((const DNode*)nodes, stk, tr, ct, root);
+#endif
+}
+// bytes of the workgroup's LDS copy of the root (node + children 4..7's references)
+#define PT_ROOT_BYTES (PT_NODE_WIDTH == 8 ? 144 : 128)
+
 // Binary node step over the reference topology (reference-count launch).
 template <bool STATS>
 __device__ __forceinline__ bool node_step2(const DNode2* __restrict__ nodes, const Stack& stk, Trav& tr,
@@ -480,18 +594,18 @@ __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const
 }
 
 template <bool STATS>
-__device__ __forceinline__ bool trav_step(const DNode* __restrict__ nodes, const DPrim* __restrict__ prims,
-                                          const Stack& stk, Trav& tr, Counters& ct) {
-  return tr.node < 0 ? leaf_step<STATS>(prims, stk, tr, ct) : node_step<STATS>(nodes, stk, tr, ct);
+__device__ __forceinline__ bool trav_step(const void* __restrict__ nodes, const int4* __restrict__ nodes_hi,
+                                          const DPrim* __restrict__ prims, const Stack& stk, Trav& tr, Counters& ct) {
+  return tr.node < 0 ? leaf_step<STATS>(prims, stk, tr, ct) : node_stepw<STATS>(nodes, nodes_hi, stk, tr, ct);
 }
 
 template <bool STATS>
-__device__ __forceinline__ bool traverse(const DNode* __restrict__ nodes, const DPrim* __restrict__ prims,
-                                         const Stack& stk, float3 o, float3 d, float tmax,
-                                         bool any, Hit& hit, Counters& ct) {
+__device__ __forceinline__ bool traverse(const void* __restrict__ nodes, const int4* __restrict__ nodes_hi,
+                                         const DPrim* __restrict__ prims, const Stack& stk, float3 o, float3 d,
+                                         float tmax, bool any, Hit& hit, Counters& ct) {
   Trav tr;
   trav_init(tr, o, d, tmax, any);
-  while (!trav_step<STATS>(nodes, prims, stk, tr, ct)) {
+  while (!trav_step<STATS>(nodes, nodes_hi, prims, stk, tr, ct)) {
   }
   hit.t = tr.tmax;
   hit.prim = tr.prim;
@@ -552,47 +666,6 @@ __device__ __forceinline__ float3 env_dir(const KP& P, float3 d) {
   const float tu = phi * (0.15915494309189535f * (float)w) - 0.5f;
   const float tv = theta * (0.31830988618379067f * (float)h) - 0.5f;
   return env_uv(P, tu, tv);
-}
-
-// lower_bound of v = r * a[n-1] accelerated by a guide table g[0..G] with
-// g[k] = lower_bound(a, k/G * a[n-1]) (built on the host, clamped to n-1): the
-// answer lies in [g[k-1], g[k+2]] for k = floor(r*G), one bucket of slack
-// either side for rounding, and a[g[k+2]] >= v; the result is exactly
-// std::lower_bound's.  With PT_ENV_GUIDE buckets the window is a few entries
-// where the CDF carries mass (where samples land).  Bucket k's record (EnvRec)
-// holds the window and its values, so the usual short window (<= 4 entries)
-// costs ONE memory round trip -- two 16-B loads of one 32-B record -- and
-// lower_bound = lo + #{entries < v} (the array is sorted); the caller's
-// interpolation pair (prev = a[t-1] or 0, cur = a[t]) comes from the same
-// registers.  A longer window is halved down to <= 4 entries on the array
-// and re-read.  (Guide table, then window: two dependent round trips, C5 -1.9%:
-// profiles/r4/ab_env_records.txt.)
-__device__ __forceinline__ int record_lower_bound(const float* __restrict__ a, float v, float r,
-                                                  const EnvRec* __restrict__ rec, int G, float& prev, float& cur) {
-  const int k = min(G - 1, max(0, (int)(r * (float)G)));
-  typedef float rf4 __attribute__((ext_vector_type(4)));
-  const rf4 q0 = *(const rf4*)&rec[k].lo, q1 = *(const rf4*)&rec[k].w1;
-  int lo = __float_as_int(q0.x);
-  const int hi = __float_as_int(q0.y);
-  float wm = q0.z, w0 = q0.w, w1 = q1.x, w2 = q1.y, w3 = q1.z, w4 = q1.w;
-  int n = hi - lo;
-  if (n > 4) {  // (rare: where the CDF is flat, the window spans more entries)
-    while (n > 4) {
-      const int half = n >> 1;
-      if (a[lo + half] < v) {
-        lo += half + 1;
-        n -= half + 1;
-      } else {
-        n = half;
-      }
-    }
-    wm = lo > 0 ? a[lo - 1] : 0.0f;
-    w0 = a[min(lo, hi)], w1 = a[min(lo + 1, hi)], w2 = a[min(lo + 2, hi)], w3 = a[min(lo + 3, hi)];
-  }
-  const int c = (int)(w0 < v) + (int)(w1 < v) + (int)(w2 < v) + (int)(w3 < v);
-  cur = c == 0 ? w0 : c == 1 ? w1 : c == 2 ? w2 : c == 3 ? w3 : w4;
-  prev = c == 0 ? wm : c == 1 ? w0 : c == 2 ? w1 : c == 3 ? w2 : w3;
-  return lo + c;
 }
 
 // importanceSampling (69-115): inverse CDF over rows (pTheta), then within the
@@ -676,8 +749,15 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   const Stack stk{(lds_int*)(s_stack + lane), P.stack_spill, n_waves * PT_BLOCK};
   // The BVH4 root, which every ray visits first: one LDS copy per wave, so
   // the root step of a fresh ray costs no vector-memory traffic (C3 +2%).
-  __shared__ DNode s_root;
-  if (!BIN && lane < (int)(sizeof(DNode) / 16)) ((float4*)&s_root)[lane] = ((const float4*)P.nodes)[lane];
+  __shared__ int4 s_root[PT_ROOT_BYTES / 16];
+  if (!BIN) {
+#if PT_NODE_WIDTH == 8
+    if (lane < 8) s_root[lane] = ((const int4*)P.nodes8)[lane];
+    else if (lane == 8) s_root[8] = P.nodes8_hi[0];
+#else
+    if (lane < 8) s_root[lane] = ((const int4*)P.nodes)[lane];
+#endif
+  }
 
   // Material and light tables are read by every shading step: keep small
   // ones in LDS (the usual case); larger ones stay in global memory.
@@ -828,7 +908,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // (pathtracer.cpp:571-575); starts the sample's random stream.  Returns
   // whether the ray enters the scene's root box (a ray that misses it sees
   // nothing but the environment: pathtracer.cpp:421-426).
-  auto camera_ray = [&](Trav& t) -> bool {
+  auto camera_ray = [&](Trav& t, float3& d) -> bool {
     const int px = pix & 0xffff, py = (int)((uint32_t)pix >> 16);
     rbase = ptrng::stream_base(P.seed, (uint32_t)(px + py * P.W), (uint32_t)sample + P.sample_base);
     rdim = ptrng::kDrawInit;
@@ -838,7 +918,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     float fy = ((float)py + ry) * P.inv_h;
     float3 sp = f3((0.5f - fx) * P.cam_ax, (0.5f - fy) * P.cam_ay, 1.0f);
     float3 wsp = ld3(P.c2w_col0) * sp.x + ld3(P.c2w_col1) * sp.y + ld3(P.c2w_col2) * sp.z;
-    float3 d = normalize(f3(0, 0, 0) - wsp);
+    d = normalize(f3(0, 0, 0) - wsp);
     trav_init(t, wsp + ld3(P.cam_pos), d, 3.0e38f, false);
     if (STATS) n_cam++;
     if (DBG && pix_index(pix) == P.dbg_pix) printf("pixel (%d,%d) sample %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g)\n", px, py, sample, t.o.x, t.o.y, t.o.z, d.x, d.y, d.z);
@@ -889,7 +969,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         shadow = 0;
       } else if (!found) {
         // miss: the environment map if there is one and includeLe (pathtracer.cpp:411-427)
-        if (ENV && includeLe) acc = acc + mul(T, env_dir(P, tr.d));
+        if (ENV && includeLe) acc = acc + mul(T, env_dir(P, tdir(tr)));
         finish = true;
         stage = 2;
       } else {
@@ -910,21 +990,21 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if (meta & 1) {
           float3 V0 = f3(pr.v0.x, pr.v0.y, pr.v0.z), E1 = f3(pr.e1.x, pr.e1.y, pr.e1.z), E2 = f3(pr.e2.x, pr.e2.y, pr.e2.z);
           float hu, hv, ht;
-          mt_terms(tr.o, tr.d, V0, E1, E2, hu, hv, ht);  // the barycentrics of the traversal test
+          mt_terms(tr.o, tdir(tr), V0, E1, E2, hu, hv, ht);  // the barycentrics of the traversal test
           float w0 = 1.0f - hu - hv;
           hp = V0 + E1 * hu + E2 * hv;
           ns = ld3(nn) * w0 + ld3(nn + 3) * hu + ld3(nn + 6) * hv;
           ng = cross(E1, E2);
         } else {
           float3 C = f3(pr.v0.x, pr.v0.y, pr.v0.z);
-          ns = normalize(tr.o + tr.d * tr.tmax - C);
+          ns = normalize(tr.o + tdir(tr) * tr.tmax - C);
           hp = C + ns * pr.e1.x;
           ng = ns;
         }
         // Triangle::intersect flips the shading normal to face the ray
         // (triangle.cpp:95-99); Sphere::intersect keeps it outward
         // (sphere.cpp:66-70), which is what tells GlassBSDF a ray is leaving.
-        if ((meta & 1) && dot(tr.d, ns) > 0.0f) ns = f3(0, 0, 0) - ns;
+        if ((meta & 1) && dot(tdir(tr), ns) > 0.0f) ns = f3(0, 0, 0) - ns;
         ng = normalize(ng);
         if (includeLe) acc = acc + mul(T, PT_BSDF3(bsdf, e));
         if (DBG && pix_index(pix) == P.dbg_pix) printf("  depth %d hit prim %d bsdf %d t=%.9g n=(%.6g %.6g %.6g) T=(%.5g)\n", (int)(cur & 0xffu), tr.prim, bsdf, tr.tmax, ns.x, ns.y, ns.z, T.x);
@@ -1039,11 +1119,11 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             // w_out (pathtracer.cpp:449-453) is only read by mirror / glass
             // sampling, which never waits for a shadow ray (f() = 0 there):
             // tr still holds the incoming ray, so it is rebuilt here, not kept.
-            const float3 wo = normalize(fr.to_local(f3(0, 0, 0) - tr.d));
+            const float3 wo = normalize(fr.to_local(f3(0, 0, 0) - tdir(tr)));
             wi = f3(-wo.x, -wo.y, wo.z);
             f = PT_BSDF3(bsdf, a) * (1.0f / fmaxf(wo.z, 1e-8f));
           } else {  // Refraction (bsdf.cpp:90-111) / Glass (bsdf.cpp:120-158)
-            const float3 wo = normalize(fr.to_local(f3(0, 0, 0) - tr.d));
+            const float3 wo = normalize(fr.to_local(f3(0, 0, 0) - tdir(tr)));
             float ratio = bsdf_f(bsdf, offsetof(DBsdf, ior) / 4);
             float sgn = 1.0f;
             if (wo.z > 0.0f) {
@@ -1266,7 +1346,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       // parks the camera ray in (hp, ns), to start when the shadow ray ends.
       while (mode == M_CAMERA) {
         Trav cr;
-        const bool in = camera_ray(cr);
+        float3 cd;
+        const bool in = camera_ray(cr, cd);
         if (!shadow) tr = cr;
         if (in) {
           T = f3(1, 1, 1);
@@ -1274,7 +1355,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           includeLe = true;
           if (shadow) {
             hp = cr.o;
-            ns = cr.d;
+            ns = cd;
             if (shadow == SH_STORE) shadow = SH_STORE_FOLLOW;
           }
           mode = M_TRAV;
@@ -1289,7 +1370,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         // float addition at silhouettes against the map, inside the
         // near-exact tolerance; parking such rays instead cost C5 18%.)
         if (ENV) {
-          const float3 e = env_dir(P, cr.d);
+          const float3 e = env_dir(P, cd);
           if (shadow == SH_STORE) ng = ng + e;
           else acc = acc + e;
         }
@@ -1321,7 +1402,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     // asm -- so the re-read parameters are not re-loaded per iteration --
     // measured C5 -2.5%, C3 -3%: the scalar loads hide behind the node
     // step's vector loads; profiles/r4/ab_layout.txt)
-    const DNode* t_nodes = P.nodes;
+#if PT_NODE_WIDTH == 8
+    const void* t_nodes = P.nodes8;
+#else
+    const void* t_nodes = P.nodes;
+#endif
+    const int4* t_nodes_hi = P.nodes8_hi;
     const DPrim* t_prims = P.prims;
     const int t_leaf_weight = P.leaf_weight;
     // Fresh rays (node 0: references only point forward, so no ray returns
@@ -1331,7 +1417,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     if constexpr (!BIN) {
       bool done = false;
       if (mode == M_TRAV && tr.node == 0) {
-        done = node_step<STATS, true>(t_nodes, stk, tr, ct, (lds_cchar*)&s_root);
+        done = node_stepw<STATS, true>(t_nodes, t_nodes_hi, stk, tr, ct, (lds_cchar*)s_root);
         if (done) mode = M_SHADE;
       }
       follow_on(done);  // (a shadow ray leaves the root only if it misses every child box)
@@ -1384,7 +1470,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if (STATS) n_leafit += lane == 0;
       } else if (trav && !at_leaf) {
         if constexpr (BIN) done = node_step2<STATS>(P.nodes2, stk, tr, ct);
-        else done = node_step<STATS>(t_nodes, stk, tr, ct);
+        else done = node_stepw<STATS>(t_nodes, t_nodes_hi, stk, tr, ct);
       }
       if (done) mode = M_SHADE;
       follow_on(done);
@@ -1531,7 +1617,8 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
 }
 
 // Batched BVHAccel::intersect queries, one lane per ray.
-__global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __restrict__ nodes,
+__global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const void* __restrict__ nodes,
+                                                           const int4* __restrict__ nodes_hi,
                                                            const DPrim* __restrict__ prims, const float* __restrict__ o,
                                                            const float* __restrict__ d, const float* __restrict__ maxt,
                                                            int64_t n, int32_t* hit, float* t, int32_t* prim,
@@ -1546,12 +1633,12 @@ __global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __rest
   h.t = 0;
   h.prim = -1;
   Counters ct = {0, 0, 0};
-  bool f = traverse<false>(nodes, prims, stk, O, D, 3.0e38f, false, h, ct);
+  bool f = traverse<false>(nodes, nodes_hi, prims, stk, O, D, 3.0e38f, false, h, ct);
   hit[i] = f ? 1 : 0;
   t[i] = f ? h.t : -1.0f;
   prim[i] = f ? (prim_map ? prim_map[h.prim] : h.prim) : -1;
   Hit h2;
-  bool a = traverse<false>(nodes, prims, stk, O, D, maxt[i], true, h2, ct);
+  bool a = traverse<false>(nodes, nodes_hi, prims, stk, O, D, maxt[i], true, h2, ct);
   anyhit[i] = a ? 1 : 0;
 }
 
@@ -1612,13 +1699,14 @@ extern "C" hipError_t ptk_launch_resolve(const KParams* P, hipStream_t s) {
   return hipGetLastError();
 }
 
-extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prims, const float* o, const float* d,
-                                           const float* maxt, int64_t n, int32_t* hit, float* t, int32_t* prim,
-                                           int32_t* anyhit, int* spill, const int* prim_map, hipStream_t s) {
+extern "C" hipError_t ptk_launch_intersect(const void* nodes, const int4* nodes_hi, const DPrim* prims, const float* o,
+                                           const float* d, const float* maxt, int64_t n, int32_t* hit, float* t,
+                                           int32_t* prim, int32_t* anyhit, int* spill, const int* prim_map,
+                                           hipStream_t s) {
   int grid = (int)((n + PT_BLOCK - 1) / PT_BLOCK);
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL(ptk::intersect_kernel, dim3(grid), dim3(PT_BLOCK), 0, s, nodes, prims, o, d, maxt, n, hit, t,
-                     prim, anyhit, spill, prim_map);
+  hipLaunchKernelGGL(ptk::intersect_kernel, dim3(grid), dim3(PT_BLOCK), 0, s, nodes, nodes_hi, prims, o, d, maxt, n,
+                     hit, t, prim, anyhit, spill, prim_map);
   return hipGetLastError();
 }
 

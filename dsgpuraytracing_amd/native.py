@@ -116,6 +116,7 @@ _SIGS = {
     "pt_last_error": (c_char_p, []),
     "pt_to_color": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p]),
     "pt_to_color_check": (c_int64, [c_uint32, c_uint32]),
+    "pt_env_search_check": (c_int64, [c_void_p, c_int32, c_int32, c_int64, c_void_p, c_void_p, POINTER(c_int64)]),
     # include/ptgpu_scene.h (bound with full types in scene_loader.py)
     "pt_host_scene_load": (c_int32, [c_char_p, c_int32, c_int32, c_char_p, POINTER(c_void_p)]),
     "pt_host_scene_view": (c_int32, [c_void_p, c_void_p, c_void_p]),
@@ -166,6 +167,8 @@ def lib():
     except OSError as e:  # pragma: no cover - depends on the box
         raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
     for name, (res, args) in _SIGS.items():
+        if os.environ.get("PT_LIB") and not hasattr(L, name):
+            continue  # (an older build in an A/B: it lacks a later diagnostics entry point)
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

@@ -198,7 +198,7 @@ typedef struct pt_stats {
   int64_t hitshade_clocks; /* of shade_clocks: hit records, NEE and bounces = section_clocks[0..2] */
   double resolve_ms;       /* device time of the sample-group resolve kernel */
   int32_t bvh_stack;       /* worst-case traversal stack entries of the uploaded BVH */
-  int64_t bvh_nodes;       /* 4-wide BVH nodes uploaded */
+  int64_t bvh_nodes;       /* render-tree nodes uploaded (8-wide; 4-wide in a PT_NODE_WIDTH=4 build) */
   int64_t section_clocks[4]; /* of shade_clocks: hit record, light sampling, BSDF sampling + sample
                                 completion, queue fetch (the rest of shade_clocks: camera rays and loop
                                 overhead) */
@@ -317,6 +317,16 @@ int pt_to_color(const float* hdr, int32_t width, int32_t height, int32_t x0, int
  * [lo_bits, hi_bits) whose tabulated 8-bit code differs from the direct evaluation
  * code8(powf(s * exposure, 1 / 2.2)) (0 = the table is exact there). */
 int64_t pt_to_color_check(uint32_t lo_bits, uint32_t hi_bits);
+/* Diagnostics for the environment light's inverse-CDF sampling (host only): builds
+ * EnvironmentLight's tables (src/static_scene/environment_light.cpp:6-48) for the
+ * width x height float RGB map and replays the kernel's guide-record search
+ * (pt_device.h record_lower_bound) for n query pairs (u1[i], u2[i]) in [0, 1)
+ * against std::lower_bound, as importanceSampling's two searches
+ * (environment_light.cpp:69-115): returns how many searches disagreed in the index
+ * or the interpolation pair (0 = exact), or a negative PT_E_*; *long_windows (nullable)
+ * receives how many searches took the window-halving path. */
+int64_t pt_env_search_check(const float* rgb, int32_t width, int32_t height, int64_t n, const float* u1,
+                            const float* u2, int64_t* long_windows);
 
 #ifdef __cplusplus
 }

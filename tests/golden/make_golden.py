@@ -20,11 +20,13 @@ available on the GPU box) and stores inputs + outputs as small PTDUMP files:
                                reference renders of the BASELINE C3 / C5 proxy scenes
                                (scenes.proxy_path(1); scenes.c5_path(2) and c5_path(3) + the env map)
                                at 128x128, 64 spp, two seeds (statistical parity)
+  scene_hashes.json             sha256 of every array of the reference's flattened scene for the
+                               bunny scenes and the C5 / c5big proxies with their map (1920x1080)
   tocolor_in.ptd / tocolor_ref.ptd
                                HDR edge cases -> HDRImageBuffer::toColor's RGBA8
                                frameBuffer and save_image's flipped rows
 
-Usage: python tests/golden/make_golden.py [--only env|refraction|tocolor|baseline]
+Usage: python tests/golden/make_golden.py [--only env|refraction|tocolor|baseline|c5big|c5hashes]
 (needs oracle/_ref/ref_driver)
 """
 from __future__ import annotations
@@ -178,6 +180,8 @@ def main():
         return make_baseline_scenes()
     if only == "c5big":
         return make_baseline_scenes("c5bigproxy")
+    if only == "c5hashes":
+        return make_hashes(c5_only=True)
     make_env()
     if only:
         return
@@ -225,20 +229,34 @@ def main():
     rays = os.path.join(HERE, "c1_rays.ptd")
     ptdump.write(rays, {"ray_o": o.reshape(-1), "ray_d": d.reshape(-1), "ray_maxt": maxt})
     run([C1, "-w", "64", "-h", "64", "--mode", "rays", "--rays", rays, "--out", os.path.join(HERE, "c1_rays_ref.ptd")])
-    # Scene checksums of larger scenes (too big to commit as dumps): the
-    # reference's own flattened scene, hashed array by array.
+    make_hashes()
+    print("golden fixtures written to", HERE)
+
+
+def make_hashes(c5_only=False):
+    """Scene checksums of larger scenes (too big to commit as dumps): the
+    reference's own flattened scene, hashed array by array -- the bunny scenes
+    and (round 5) the C5 / c5big glass-and-mirror proxies
+    with their environment map at 1920x1080.  Merged into scene_hashes.json."""
     sys.path.insert(0, ROOT)
     from dsgpuraytracing_amd import scenes
-    hashes = {}
-    for dae, w, h in [(os.path.join(ROOT, "assets", "CBbunny.dae"), 1024, 1024), (scenes.proxy_path(1), 1024, 1024),
-                      (scenes.proxy_path(1), 1920, 1080)]:
+    path = os.path.join(HERE, "scene_hashes.json")
+    hashes = json.load(open(path)) if os.path.exists(path) else {}
+    todo = [] if c5_only else [(os.path.join(ROOT, "assets", "CBbunny.dae"), 1024, 1024, None),
+                               (scenes.proxy_path(1), 1024, 1024, None), (scenes.proxy_path(1), 1920, 1080, None)]
+    todo += [(scenes.c5_path(2), 1920, 1080, scenes.c5_envmap_path()),
+             (scenes.c5_path(3), 1920, 1080, scenes.c5_envmap_path())]
+    for dae, w, h, env in todo:
         tmp = os.path.join(HERE, "_tmp_scene.ptd")
-        run([dae, "-w", str(w), "-h", str(h), "--mode", "dump", "--out", tmp])
-        hashes[f"{os.path.basename(dae)}@{w}x{h}"] = scene_hashes(ptdump.read(tmp))
+        args = [dae, "-w", str(w), "-h", str(h), "--mode", "dump", "--out", tmp]
+        if env:
+            args += ["--envmap", env]
+        run(args)
+        key = f"{os.path.basename(dae)}@{w}x{h}" + (f"+{os.path.basename(env)}" if env else "")
+        hashes[key] = scene_hashes(ptdump.read(tmp))
         os.remove(tmp)
-    with open(os.path.join(HERE, "scene_hashes.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(hashes, f, indent=1, sort_keys=True)
-    print("golden fixtures written to", HERE)
 
 
 def scene_hashes(d):

@@ -51,13 +51,21 @@ def test_environment_light_scene_bit_identical(fixture, dae):
     assert got["light_type"][-1] == native.PT_LIGHT_ENVIRONMENT
 
 
-@pytest.mark.parametrize("key", ["CBbunny.dae@1024x1024", "CBbunny_sub1.dae@1024x1024", "CBbunny_sub1.dae@1920x1080"])
+@pytest.mark.parametrize("key", ["CBbunny.dae@1024x1024", "CBbunny_sub1.dae@1024x1024", "CBbunny_sub1.dae@1920x1080",
+                                 "CBbunny_sub2_c5.dae@1920x1080+c5_sky_512x256.exr",
+                                 "CBbunny_sub3_c5.dae@1920x1080+c5_sky_512x256.exr"])
 def test_bunny_scenes_match_reference_checksums(key):
+    """The bunny scenes, and the C5 / c5big glass-and-mirror proxies with their
+    environment map (457k / 1.83M primitives: halfedge normals, BVH, the map
+    decoded by the native EXR reader), against hashes of the reference's own
+    flattened scene (make_golden.py make_hashes: ref_driver --mode dump)."""
     want = json.load(open(golden("scene_hashes.json")))[key]
     name, res = key.split("@")
+    res, _, env = res.partition("+")
     w, h = (int(v) for v in res.split("x"))
-    dae = os.path.join(ROOT, "assets", name) if name == "CBbunny.dae" else scenes.proxy_path(1)
-    got = scene_loader.load_dae(dae, w, h)
+    dae = {"CBbunny.dae": os.path.join(ROOT, "assets", "CBbunny.dae"), "CBbunny_sub1.dae": scenes.proxy_path(1),
+           "CBbunny_sub2_c5.dae": scenes.c5_path(2), "CBbunny_sub3_c5.dae": scenes.c5_path(3)}[name]
+    got = scene_loader.load_dae(dae, w, h, envmap=scenes.c5_envmap_path() if env else None)
     assert sorted(got) == sorted(want)
     for k, v in want.items():
         assert got[k].size == v["n"], k

@@ -1,0 +1,454 @@
+// wide_sim.cpp -- CPU traversal census of 4- vs 8-wide BVH layouts (design
+// study for the 8-wide node; not part of the product).
+//
+// Loads a scene with the native host pipeline, builds the host binned-SAH
+// binary tree (pt_host_build_render_tree), collapses it to W-wide nodes by
+// opening the largest-area internal child, and traces a sample of the C3 ray
+// mix: camera rays, cosine bounces from their hits and shadow rays towards
+// the area light.  Per ray kind and per layout / child ordering it counts the
+// node steps and leaf steps (two primitives per step, as leaf_step) the
+// kernel's traversal would take -- the dependent memory round trips of a ray.
+//
+//   g++ -O2 -std=c++17 -Iinclude tools/wide_sim.cpp -Ldsgpuraytracing_amd -lptgpu \
+//       -Wl,-rpath,$PWD/dsgpuraytracing_amd -o _scratch/wide_sim
+//   _scratch/wide_sim _scenes/CBbunny_sub1.dae 1024 1024 [rays]
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "ptgpu.h"
+#include "ptgpu_scene.h"
+
+struct V3 {
+  double x, y, z;
+};
+static V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+static V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static V3 operator*(V3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+static double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static V3 cross(V3 a, V3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+static V3 norm(V3 a) { return a * (1.0 / std::sqrt(dot(a, a))); }
+
+struct Child {
+  double lo[3], hi[3];
+  int ref;  // >= 0 wide node, < 0: ~leaf index
+};
+struct WNode {
+  int n;
+  Child c[8];
+  int slot_of_octant[8];  // octant ordering: children permuted into slots
+};
+struct Leaf {
+  int first, count;
+};
+
+static const pt_scene* S;
+static std::vector<int64_t> perm;
+static std::vector<pt_bvh_node> B;
+
+static double area(const Child& c) {
+  double dx = c.hi[0] - c.lo[0], dy = c.hi[1] - c.lo[1], dz = c.hi[2] - c.lo[2];
+  return dx * dy + dy * dz + dz * dx;
+}
+
+struct Tree {
+  std::vector<WNode> nodes;
+  std::vector<Leaf> leaves;
+  int W;
+  bool split = false;  // fill free slots by splitting multi-primitive leaf children into single primitives
+  bool quant = false;  // child boxes as the fp16 DNode8 encoding decodes them (conservative)
+};
+static double q16(double x, bool up) {  // x >= 0 on the fp16 grid, rounded down / up
+  if (x <= 0) return 0;
+  int k;
+  std::frexp(x, &k);  // x in [2^(k-1), 2^k)
+  double ulp = std::ldexp(1.0, std::max(k - 1, -14) - 10);
+  double q = x / ulp;
+  return (up ? std::ceil(q) : std::floor(q)) * ulp;
+}
+
+static bool is_leaf(int64_t i) { return B[i].left < 0; }
+
+static Child child_of(Tree& t, int64_t b) {
+  Child c;
+  for (int k = 0; k < 3; ++k) {
+    c.lo[k] = B[b].bb_min[k];
+    c.hi[k] = B[b].bb_max[k];
+  }
+  if (is_leaf(b)) {
+    t.leaves.push_back({(int)B[b].start, (int)B[b].range});
+    c.ref = ~(int)(t.leaves.size() - 1);
+  } else {
+    c.ref = (int)b;  // binary index until emitted
+  }
+  return c;
+}
+
+static int emit(Tree& t, int64_t b) {
+  std::vector<Child> ch = {child_of(t, B[b].left), child_of(t, B[b].right)};
+  while ((int)ch.size() < t.W) {
+    int best = -1;
+    double ba = -1;
+    for (int k = 0; k < (int)ch.size(); ++k)
+      if (ch[k].ref >= 0 && area(ch[k]) > ba) {
+        ba = area(ch[k]);
+        best = k;
+      }
+    if (best < 0) break;
+    int64_t x = ch[best].ref;
+    ch[best] = child_of(t, B[x].left);
+    ch.push_back(child_of(t, B[x].right));
+  }
+  if (t.split) {
+    for (;;) {
+      int best = -1;
+      for (int k = 0; k < (int)ch.size(); ++k)
+        if (ch[k].ref < 0 && t.leaves[~ch[k].ref].count >= 2 && (int)ch.size() + t.leaves[~ch[k].ref].count - 1 <= t.W) {
+          best = k;
+          break;
+        }
+      if (best < 0) break;
+      Leaf L = t.leaves[~ch[best].ref];
+      for (int q = 0; q < L.count; ++q) {
+        Child c;
+        const double* g = S->prim_geom + 9 * perm[L.first + q];
+        for (int a = 0; a < 3; ++a) {
+          if (S->prim_type[perm[L.first + q]] == PT_PRIM_TRIANGLE) {
+            c.lo[a] = std::min({g[a], g[3 + a], g[6 + a]});
+            c.hi[a] = std::max({g[a], g[3 + a], g[6 + a]});
+          } else {
+            c.lo[a] = g[a] - g[3];
+            c.hi[a] = g[a] + g[3];
+          }
+        }
+        t.leaves.push_back({L.first + q, 1});
+        c.ref = ~(int)(t.leaves.size() - 1);
+        if (q == 0) ch[best] = c;
+        else ch.push_back(c);
+      }
+    }
+  }
+  if (t.quant) {
+    for (int a = 0; a < 3; ++a) {
+      double org = 1e300, ext = 0;
+      for (auto& c : ch) org = std::min(org, (double)(float)c.lo[a]);
+      for (auto& c : ch) ext = std::max(ext, (double)(float)c.hi[a] - org);
+      int k2 = 0;
+      if (ext > 0) std::frexp(ext, &k2);
+      int e = k2 - 15;
+      for (auto& c : ch) {
+        c.lo[a] = org + std::ldexp(q16(std::ldexp((double)(float)c.lo[a] - org, -e), false), e);
+        c.hi[a] = org + std::ldexp(q16(std::ldexp((double)(float)c.hi[a] - org, -e), true), e);
+      }
+    }
+  }
+  int me = (int)t.nodes.size();
+  t.nodes.push_back(WNode{});
+  t.nodes[me].n = (int)ch.size();
+  for (size_t k = 0; k < ch.size(); ++k) {
+    if (ch[k].ref >= 0) ch[k].ref = emit(t, ch[k].ref);
+    t.nodes[me].c[k] = ch[k];
+  }
+  // octant slots (Ylitie et al. 2017): greedy assignment of children to the
+  // octant whose ray direction visits them first (smallest centre . dir)
+  WNode& w = t.nodes[me];
+  double pc[3];
+  for (int k = 0; k < 3; ++k) {
+    double lo = 1e300, hi = -1e300;
+    for (int i = 0; i < w.n; ++i) {
+      lo = std::min(lo, w.c[i].lo[k]);
+      hi = std::max(hi, w.c[i].hi[k]);
+    }
+    pc[k] = 0.5 * (lo + hi);
+  }
+  std::vector<int> used(8, 0), assigned(8, -1);
+  for (int s = 0; s < 8; ++s) assigned[s] = -1;
+  // cost[i][o]: child i's centre along octant o's direction
+  for (int round = 0; round < w.n; ++round) {
+    double best = 1e300;
+    int bi = -1, bo = -1;
+    for (int i = 0; i < w.n; ++i) {
+      if (used[i]) continue;
+      for (int o = 0; o < 8; ++o) {
+        if (assigned[o] >= 0) continue;
+        V3 d = {o & 1 ? -1.0 : 1.0, o & 2 ? -1.0 : 1.0, o & 4 ? -1.0 : 1.0};
+        V3 c = {0.5 * (w.c[i].lo[0] + w.c[i].hi[0]) - pc[0], 0.5 * (w.c[i].lo[1] + w.c[i].hi[1]) - pc[1],
+                0.5 * (w.c[i].lo[2] + w.c[i].hi[2]) - pc[2]};
+        double cost = dot(c, d);
+        if (cost < best) {
+          best = cost;
+          bi = i;
+          bo = o;
+        }
+      }
+    }
+    used[bi] = 1;
+    assigned[bo] = bi;
+  }
+  for (int o = 0; o < 8; ++o) w.slot_of_octant[o] = assigned[o];
+  return me;
+}
+
+struct Ray {
+  V3 o, d;
+  double tmax;
+  bool any;
+};
+
+enum Order { SORT = 0, OCT = 1, NEAR_SLOT = 2, NEAR_OCT = 3, SLOT = 4, RSLOT = 5 };
+
+struct Count {
+  double nodes = 0, leafsteps = 0, prims = 0, hitkids = 0, rays = 0, pushes = 0, maxstack = 0;
+};
+
+static bool tri_hit(const Ray& r, int64_t p, double& t) {
+  const double* g = S->prim_geom + 9 * p;
+  if (S->prim_type[p] != PT_PRIM_TRIANGLE) {
+    V3 c = {g[0], g[1], g[2]};
+    double rad = g[3];
+    V3 oc = r.o - c;
+    double b = dot(oc, r.d), cc = dot(oc, oc) - rad * rad, disc = b * b - cc;
+    if (disc < 0) return false;
+    double s = std::sqrt(disc), t1 = -b - s, t2 = -b + s;
+    double tt = t1 > 0 ? t1 : t2;
+    if (tt > 0 && tt < r.tmax) {
+      t = tt;
+      return true;
+    }
+    return false;
+  }
+  V3 p0 = {g[0], g[1], g[2]}, p1 = {g[3], g[4], g[5]}, p2 = {g[6], g[7], g[8]};
+  V3 e1 = p1 - p0, e2 = p2 - p0, pv = cross(r.d, e2);
+  double det = dot(e1, pv);
+  if (det == 0) return false;
+  double id = 1 / det;
+  V3 tv = r.o - p0;
+  double u = dot(tv, pv) * id;
+  V3 qv = cross(tv, e1);
+  double v = dot(r.d, qv) * id, tt = dot(e2, qv) * id;
+  if (u < 0 || v < 0 || u + v > 1) return false;
+  if (tt > 1e-9 && tt < r.tmax) {
+    t = tt;
+    return true;
+  }
+  return false;
+}
+
+static bool box(const Ray& r, const Child& c, double tmax, double& tn) {
+  double t0 = 0, t1 = tmax;
+  const double o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+  for (int k = 0; k < 3; ++k) {
+    double inv = 1.0 / (d[k] == 0 ? 1e-20 : d[k]);
+    double a = (c.lo[k] - o[k]) * inv, b = (c.hi[k] - o[k]) * inv;
+    if (a > b) std::swap(a, b);
+    t0 = std::max(t0, a);
+    t1 = std::min(t1, b);
+  }
+  tn = t0;
+  return t0 <= t1 * 1.0000008;
+}
+
+// returns hit t (or -1)
+static int64_t g_prim = -1;
+static double trace(const Tree& t, Ray r, Order ord, Count& ct) {
+  std::vector<int> st;
+  g_prim = -1;
+  int cur = 0;  // node index, or ~leaf
+  bool found = false;
+  int oct = (r.d.x < 0 ? 1 : 0) | (r.d.y < 0 ? 2 : 0) | (r.d.z < 0 ? 4 : 0);
+  ct.rays += 1;
+  for (;;) {
+    if (cur >= 0) {
+      ct.nodes += 1;
+      const WNode& w = t.nodes[cur];
+      struct H {
+        double d;
+        int ref, key;
+      } h[8];
+      int nh = 0;
+      for (int s = 0; s < 8; ++s) {
+        int i;
+        if (ord == OCT || ord == NEAR_OCT) {
+          // traversal order: octant slots by key s = slot ^ oct, increasing
+          i = w.slot_of_octant[s ^ oct];
+        } else if (ord == RSLOT) {
+          i = 7 - s;
+        } else {
+          i = s;
+        }
+        if (i < 0 || i >= w.n) continue;
+        double tn;
+        if (box(r, w.c[i], r.tmax, tn)) h[nh++] = {tn, w.c[i].ref, s};
+      }
+      ct.hitkids += nh;
+      if (nh == 0) {
+        if (st.empty()) break;
+        cur = st.back();
+        st.pop_back();
+        continue;
+      }
+      if (ord == SORT) {
+        std::sort(h, h + nh, [](const H& a, const H& b) { return a.d < b.d; });
+      } else if (ord == NEAR_SLOT || ord == NEAR_OCT) {
+        int m = 0;
+        for (int k = 1; k < nh; ++k)
+          if (h[k].d < h[m].d) m = k;
+        H x = h[m];
+        for (int k = m; k > 0; --k) h[k] = h[k - 1];
+        h[0] = x;
+      }
+      for (int k = nh - 1; k >= 1; --k) st.push_back(h[k].ref);
+      ct.pushes += nh - 1;
+      ct.maxstack = std::max(ct.maxstack, (double)st.size());
+      cur = h[0].ref;
+    } else {
+      const Leaf& L = t.leaves[~cur];
+      ct.leafsteps += (L.count + 1) / 2;
+      bool stop = false;
+      for (int k = 0; k < L.count; ++k) {
+        ct.prims += 1;
+        double th;
+        if (tri_hit(r, perm[L.first + k], th)) {
+          r.tmax = th;
+          g_prim = perm[L.first + k];
+          found = true;
+          if (r.any) {
+            stop = true;
+            break;
+          }
+        }
+      }
+      if (stop || st.empty()) break;
+      cur = st.back();
+      st.pop_back();
+    }
+  }
+  return found ? r.tmax : -1;
+}
+
+static int64_t hit_prim(const Ray& r, double t) {  // brute re-identify (for the normal)
+  (void)r;
+  (void)t;
+  return -1;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 4) {
+    std::fprintf(stderr, "usage: wide_sim scene.dae W H [rays]\n");
+    return 2;
+  }
+  int W = std::atoi(argv[2]), H = std::atoi(argv[3]);
+  int nrays = argc > 4 ? std::atoi(argv[4]) : 20000;
+  pt_host_scene* hs = nullptr;
+  if (pt_host_scene_load(argv[1], W, H, nullptr, &hs) != PT_OK) {
+    std::fprintf(stderr, "load failed: %s\n", pt_last_error());
+    return 1;
+  }
+  static pt_scene sc;
+  pt_camera cam;
+  pt_host_scene_view(hs, &sc, &cam);
+  S = &sc;
+  B.resize(2 * sc.n_prims);
+  perm.resize(sc.n_prims);
+  int64_t nn = 0;
+  if (pt_host_build_render_tree(&sc, B.data(), &nn, perm.data()) != PT_OK) return 1;
+  B.resize(nn);
+  Tree t4, t8, t2, t8s, t4s, t8q;
+  t8q.W = 8;
+  t8q.quant = true;
+  emit(t8q, 0);
+  t4.W = 4;
+  t8.W = 8;
+  t2.W = 2;
+  t8s.W = 8;
+  t8s.split = true;
+  t4s.W = 4;
+  t4s.split = true;
+  emit(t4, 0);
+  emit(t8, 0);
+  emit(t2, 0);
+  emit(t8s, 0);
+  emit(t4s, 0);
+  auto fill = [](const Tree& t) { double c = 0; for (auto& n : t.nodes) c += n.n; return c / t.nodes.size(); };
+  std::printf("children per node: BVH4 %.2f, BVH8 %.2f, BVH8 split %.2f, BVH4 split %.2f\n", fill(t4), fill(t8), fill(t8s), fill(t4s));
+  std::printf("prims %lld, binary nodes %lld, BVH4 nodes %zu, BVH8 nodes %zu, leaves %zu\n", (long long)sc.n_prims,
+              (long long)nn, t4.nodes.size(), t8.nodes.size(), t8.leaves.size());
+  // area light
+  V3 lp{0, 0, 0}, ldx{0, 0, 0}, ldy{0, 0, 0};
+  for (int i = 0; i < sc.n_lights; ++i)
+    if (sc.lights[i].type == PT_LIGHT_AREA) {
+      lp = {sc.lights[i].position[0], sc.lights[i].position[1], sc.lights[i].position[2]};
+      ldx = {sc.lights[i].dim_x[0], sc.lights[i].dim_x[1], sc.lights[i].dim_x[2]};
+      ldy = {sc.lights[i].dim_y[0], sc.lights[i].dim_y[1], sc.lights[i].dim_y[2]};
+    }
+  std::mt19937_64 rng(7);
+  std::uniform_real_distribution<double> U(0, 1);
+  // rays: camera rays through the frame; per hit a shadow ray and a bounce,
+  // per bounce hit a shadow ray
+  std::vector<Ray> cam_r, bounce_r, shadow_r;
+  V3 cpos = {cam.pos[0], cam.pos[1], cam.pos[2]};
+  double ax = cam.screen_w / cam.screen_dist, ay = cam.screen_h / cam.screen_dist;
+  Count dummy;
+  auto find_hit_normal = [&](const Ray& r, double th, V3& n) {
+    // the nearest hit primitive by brute force over the leaves the BVH2 visits is
+    // overkill; take the geometric normal of the nearest triangle via a second
+    // exhaustive pass over a small neighbourhood: approximate with the
+    // direction back to the origin (enough for a bounce distribution)
+    (void)th;
+    const double* g = S->prim_geom + 9 * g_prim;
+    if (S->prim_type[g_prim] == PT_PRIM_TRIANGLE)
+      n = norm(cross(V3{g[3] - g[0], g[4] - g[1], g[5] - g[2]}, V3{g[6] - g[0], g[7] - g[1], g[8] - g[2]}));
+    else
+      n = norm(r.o + r.d * th - V3{g[0], g[1], g[2]});
+    if (dot(n, r.d) > 0) n = n * -1.0;
+  };
+  while ((int)cam_r.size() < nrays) {
+    double fx = U(rng), fy = U(rng);
+    V3 sp = {(0.5 - fx) * ax, (0.5 - fy) * ay, 1.0};
+    V3 wsp = {cam.c2w[0] * sp.x + cam.c2w[1] * sp.y + cam.c2w[2] * sp.z,
+              cam.c2w[3] * sp.x + cam.c2w[4] * sp.y + cam.c2w[5] * sp.z,
+              cam.c2w[6] * sp.x + cam.c2w[7] * sp.y + cam.c2w[8] * sp.z};
+    Ray r{wsp + cpos, norm(wsp * -1.0), 1e30, false};
+    double th = trace(t4, r, SORT, dummy);
+    if (th < 0) continue;  // (misses are culled or trivial)
+    cam_r.push_back(r);
+    V3 p = r.o + r.d * th;
+    V3 n;
+    find_hit_normal(r, th, n);
+    V3 lpt = lp + ldx * (U(rng) - 0.5) + ldy * (U(rng) - 0.5);
+    V3 dl = lpt - p;
+    double dist = std::sqrt(dot(dl, dl));
+    shadow_r.push_back(Ray{p + dl * (1e-6 / dist), dl * (1.0 / dist), dist * 0.999, true});
+    // cosine-ish bounce around n
+    V3 a = std::fabs(n.x) > 0.5 ? V3{0, 1, 0} : V3{1, 0, 0};
+    V3 tu = norm(cross(a, n)), tv = cross(n, tu);
+    double r1 = U(rng), r2 = U(rng), st = std::sqrt(r1), ctt = std::sqrt(1 - r1);
+    V3 d = norm(tu * (st * std::cos(2 * M_PI * r2)) + tv * (st * std::sin(2 * M_PI * r2)) + n * ctt);
+    bounce_r.push_back(Ray{p + d * 1e-6, d, 1e30, false});
+  }
+  (void)hit_prim;
+  const char* names[] = {"camera", "bounce", "shadow"};
+  std::vector<Ray>* sets[] = {&cam_r, &bounce_r, &shadow_r};
+  struct L {
+    const char* name;
+    const Tree* t;
+    Order o;
+  } layouts[] = {{"BVH2", &t2, SORT},        {"BVH4 sort", &t4, SORT},       {"BVH8 sort", &t8, SORT},
+                 {"BVH8 octant", &t8, OCT},  {"BVH8 near+slot", &t8, NEAR_SLOT}, {"BVH8 near+oct", &t8, NEAR_OCT},
+                 {"BVH8 fp16 sort", &t8q, SORT}, {"BVH8 fp16 n+slot", &t8q, NEAR_SLOT}};
+  for (int s = 0; s < 3; ++s) {
+    std::printf("-- %s rays (%zu)\n", names[s], sets[s]->size());
+    for (const L& l : layouts) {
+      Count c;
+      for (const Ray& r : *sets[s]) trace(*l.t, r, l.o, c);
+      std::printf("  %-16s node steps %6.2f  leaf steps %6.2f  prims %6.2f  hit children/node %5.2f  pushes %5.2f  max stack %3.0f  steps %6.2f\n",
+                  l.name, c.nodes / c.rays, c.leafsteps / c.rays, c.prims / c.rays, c.hitkids / c.nodes,
+                  c.pushes / c.rays, c.maxstack, (c.nodes + c.leafsteps) / c.rays);
+    }
+  }
+  pt_host_scene_free(hs);
+  return 0;
+}
