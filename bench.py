@@ -224,15 +224,17 @@ def _coprime(k, ntx):
     return k
 
 
-def cpu_baseline_reference(dae: str, envmap, budget_s: float = 15.0) -> dict:
+def cpu_baseline_reference(dae: str, envmap, budget_s: float = 15.0, threads: int = 1) -> dict:
     """The reference's OWN CPU path (oracle/_ref/ref_driver, compiled from
     /root/reference/src by oracle/ref/Makefile; it travels to the GPU box with
     the tree) timed on this host: PathTracer::raytrace_tile (pathtracer.cpp:
-    585-611) on every k-th 32x32 tile of the frame's FIFO, on one thread with
-    glibc rand() as shipped (== its -t 1 setting, its fastest: the shared rand()
-    lock makes it anti-scale with threads), k sized from a calibration run so
-    the sample takes about budget_s.  Scene load and BVH build are excluded,
-    as in the reference's own timer."""
+    585-611) on every k-th 32x32 tile of the frame's FIFO, k sized from a
+    calibration run so the sample takes about budget_s.  threads = 1: one
+    thread with glibc rand() as shipped (== its -t 1 setting); threads = T:
+    T threads popping the sample's tiles from one shared queue as its
+    worker_thread does (pathtracer.cpp:613-637) -- readme.txt:1 publishes
+    -t 8, where the shared rand() lock keeps it near the -t 1 rate.  Scene
+    load and BVH build are excluded, as in the reference's own timer."""
     import subprocess
 
     ntx = (W + 31) // 32
@@ -240,7 +242,8 @@ def cpu_baseline_reference(dae: str, envmap, budget_s: float = 15.0) -> dict:
 
     def run(begin, stride):
         cmd = [REF_DRIVER, dae, "--mode", "tiles", "-w", str(W), "-h", str(H), "-s", str(SPP), "-m", str(DEPTH),
-               "-l", str(NSL), "--seed", str(SEED), "--tile-begin", str(begin), "--tile-stride", str(stride)]
+               "-l", str(NSL), "--seed", str(SEED), "--tile-begin", str(begin), "--tile-stride", str(stride),
+               "-t", str(threads)]
         if envmap:
             cmd += ["--envmap", envmap]
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True, timeout=600, check=True)
@@ -251,11 +254,13 @@ def cpu_baseline_reference(dae: str, envmap, budget_s: float = 15.0) -> dict:
     per_tile = max(c["render_s"], 1e-4) / max(1, c["tiles"])
     step = _coprime(max(1, int(round(ntiles * per_tile / budget_s))), ntx)
     m = run(step // 2, step)
-    return {"value": m["pixels"] * SPP / m["render_s"] / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "reference",
+    how = ("one thread, glibc rand() as shipped (its -t 1)" if threads == 1 else
+           f"{threads} threads on one shared tile queue as its worker_thread, glibc rand() as shipped (its -t {threads}, "
+           f"readme.txt:1's published setting)")
+    return {"value": m["pixels"] * SPP / m["render_s"] / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "reference",
             "sample": f"every {step}th 32x32 tile of the {W}x{H} frame ({m['pixels']} px, uniform) at {SPP} spp, "
                       f"-m {DEPTH} -l {NSL}: the reference's PathTracer::raytrace_tile built from its own sources "
-                      f"(oracle/_ref/ref_driver --mode tiles), one thread, glibc rand() as shipped (its -t 1), "
-                      f"{m['render_s']:.1f} s of rendering"}
+                      f"(oracle/_ref/ref_driver --mode tiles), {how}, {m['render_s']:.1f} s of rendering"}
 
 
 def _tiles_px(begin, stride):
@@ -558,7 +563,14 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
                        "parallelism": (f"samples{world}" if weak else f"tiles{world}") if world > 1 else "single",
                        "exchange_bytes_per_rank": (int(band[0].numel() * 4) if weak else
                                                    (int(ex.packed.numel() * 4) if ex is not None else 0)),
-                       "render_time_s": round(elapsed / frames, 7), "scene_load_s": round(t_load, 3),
+                       # BASELINE's "wall-clock render time": ONE frame start to image,
+                       # synchronised on both sides (the reference's timer spans one
+                       # render, application.cpp:776-780); the pipelined frame
+                       # interval is ms_per_step
+                       "render_time_s": round((single_ms if single_ms is not None else elapsed / frames * 1e3) / 1e3, 7),
+                       "wall_clock_frame_ms": None if single_ms is None else round(single_ms, 3),
+                       "pipelined_frame_interval_ms": round(elapsed / frames * 1e3, 4),
+                       "scene_load_s": round(t_load, 3),
                        "single_frame_ms": None if single_ms is None else round(single_ms, 3),
                        "bvh": bvh_desc(args.lbvh),
                        "upload_s": round(t_up, 4),
@@ -604,6 +616,8 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
                     scene_loader.dump_dae(dae, W, H, dp, cam_info=cam, envmap=envmap)
                 if dae is not None and os.access(REF_DRIVER, os.X_OK) and cam is None:
                     out["cpu_baseline"] = cpu_baseline_reference(dae, envmap)
+                    # the reference at its published setting (readme.txt:1: -t 8)
+                    out["cpu_baseline_published"] = cpu_baseline_reference(dae, envmap, budget_s=10.0, threads=8)
                 else:  # the bit-identical restatement when the reference build is absent
                     out["cpu_baseline"] = cpu_baseline_port(dp)
                 out["cpu_baseline_fair"] = cpu_baseline_port(dp, budget_s=10.0, rng_mode=1, threads=host_threads())
@@ -641,6 +655,26 @@ def strong_companions(local, rank, world, backend, StepGuard, TileExchange, fram
         mine = np.asarray(ex.mine, dtype=np.int32).reshape(-1, 4)
         guard = StepGuard()
         xev = []
+        # the 1-GPU point of the curve, in this process: every rank renders the
+        # WHOLE frame alone (no exchange), same clock; efficiency = rate_N /
+        # (N * rate_1)
+        whole = np.asarray(tile_fifo(w, h), dtype=np.int32).reshape(-1, 4)
+        for _ in range(warmup):
+            guard.run(dev.render_tiles_device, whole, frame.data_ptr(), stream)
+        guard.check()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(frames):
+            guard.run(dev.render_tiles_device, whole, frame.data_ptr(), stream)
+        dist.barrier()
+        torch.cuda.synchronize()
+        el1 = time.perf_counter() - t1
+        guard.check()
+        t = torch.tensor([el1], dtype=torch.float64, device="cpu" if backend == "gloo" else f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        rate1 = w * h * spp * frames / float(t.item()) / 1e6
+        frame.zero_()
 
         def step(timed=False):
             guard.run(dev.render_tiles_device, mine, ex.packed.data_ptr(), stream, packed=True,
@@ -684,6 +718,8 @@ def strong_companions(local, rank, world, backend, StepGuard, TileExchange, fram
         res[f"{name}_strong"] = {
             "workload": wl["desc"] + f", one frame's tiles over {world} GPUs + one gather (strong)",
             "value": round(w * h * spp * frames / el / 1e6, 1), "unit": "Mrays/s",
+            "single_gpu_value": round(rate1, 1),
+            "efficiency": round(w * h * spp * frames / el / 1e6 / (world * rate1), 4),
             "ms_per_frame": round(el / frames * 1e3, 3), "frames": frames, "scaling": "strong",
             "gather_bytes_per_rank": int(ex.packed.numel() * 4),
             "kernel_ms_slowest_over_mean": round(max(kms) / max(1e-9, float(np.mean(kms))), 4),

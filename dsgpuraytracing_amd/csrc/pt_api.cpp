@@ -1030,7 +1030,10 @@ static int64_t traced_px(const pt_ctx* c, int W, int H) {
 //    the queue runs dry), C1 / C2 get 1 (profiles/r4/ab_group_size.txt);
 //  * (a tail of one-sample groups handed out last, to end the launch on short
 //    work slots, measured -2% pipelined for +2% on a lone frame: DESIGN.md §4).
-static int group_size(int64_t traced, bool env, int spp, int64_t lanes, int64_t frame_blocks) {
+//  * `budget_waves` bounds the 32-bit slot indices: the largest grid any
+//    launch of the frame may use (plain or stats build), so a frame that fits
+//    one build fits the other.
+static int group_size(int64_t traced, bool env, int spp, int64_t lanes, int64_t frame_blocks, int64_t budget_waves) {
   int gs = env ? PT_GROUP_SPP_ENV : PT_GROUP_SPP;
   while (gs > 1 && traced * ((spp + gs - 1) / gs) < lanes * PT_GROUP_MIN_SLOTS) gs /= 2;
   if (const char* g = std::getenv("PT_SAMPLE_GROUP")) {  // tuning knob
@@ -1044,7 +1047,7 @@ static int group_size(int64_t traced, bool env, int spp, int64_t lanes, int64_t 
     // slot, for the whole frame's blocks (so every tile split gets the same
     // layout)
     const int64_t slots = frame_blocks * 64 * ((spp + gs - 1) / gs);
-    if ((slots + 2 * (lanes / 64) * PT_CHUNK_MAX < (int64_t)INT32_MAX && slots * 12 <= ((int64_t)PT_GROUP_SUM_GIB << 30)) ||
+    if ((slots + 2 * budget_waves * PT_CHUNK_MAX < (int64_t)INT32_MAX && slots * 4 * PT_SUM_WORDS <= ((int64_t)PT_GROUP_SUM_GIB << 30)) ||
         gs >= spp)
       break;
     gs = std::min(spp, gs * 2);
@@ -1059,10 +1062,13 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   std::memset(&c->last, 0, sizeof(c->last));
   c->times_pending = false;
   if (tl.empty()) return PT_OK;
-  // PT_PIPELINE=0: every render on the caller's stream, one slot (A/B)
-  static const bool pipeline = !std::getenv("PT_PIPELINE") || std::atoi(std::getenv("PT_PIPELINE")) != 0;
-  const int slot = pipeline ? (int)(c->n_launches % pt_ctx::kSlots) : 0;
-  hipStream_t rs = pipeline ? c->rstream[slot] : s;
+  // PT_PIPELINE=0: every render on the caller's stream, one slot (A/B).  A
+  // census launch (PT_CENSUS) writes its per-wave records into the one shared
+  // trace area, so it never overlaps another launch: it runs unpipelined too.
+  static const bool pipeline = (!std::getenv("PT_PIPELINE") || std::atoi(std::getenv("PT_PIPELINE")) != 0);
+  const bool census_launch = std::getenv("PT_CENSUS") && !stats;
+  const int slot = pipeline && !census_launch ? (int)(c->n_launches % pt_ctx::kSlots) : 0;
+  hipStream_t rs = pipeline && !census_launch ? c->rstream[slot] : s;
   // the slot's device state is free once the previous resolve that read it ran
   HIPCHK(hipStreamWaitEvent(rs, c->ev_free[slot], 0));
   // the tile list rarely changes between frames: upload it only when it does
@@ -1147,7 +1153,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     int v = std::atoi(lw);
     if (v >= 1) P.leaf_weight = v;
   }
-  P.census = std::getenv("PT_CENSUS") && !stats ? 1 : 0;  // diagnostics (tools/wave_trace.py --census)
+  P.census = census_launch ? 1 : 0;  // diagnostics (tools/wave_trace.py --census)
   P.drain_div = 0;
   if (const char* dd = std::getenv("PT_DRAIN_DIV")) {  // tuning knob
     int v = std::atoi(dd);
@@ -1211,7 +1217,8 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   }
   const int64_t want_plain = std::getenv("PT_WAVES_PER_CU") ? want : c->grid_plain;
   const int64_t frame_blocks = (int64_t)((P.W + 7) / 8) * ((P.H + 7) / 8);
-  P.group_spp = group_size(traced_px(c, P.W, P.H), c->env_w > 0, P.spp, want_plain * PT_BLOCK, frame_blocks);
+  const int64_t budget_waves = std::max({want, want_plain, (int64_t)c->grid_stats});
+  P.group_spp = group_size(traced_px(c, P.W, P.H), c->env_w > 0, P.spp, want_plain * PT_BLOCK, frame_blocks, budget_waves);
   P.n_groups = (P.spp + P.group_spp - 1) / P.group_spp;
   const int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
   // (slot indices reach past the end by up to a static chunk plus a claimed one per wave)
@@ -1227,9 +1234,9 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.sblocks = (64 * P.n_groups) % P.chunk == 0 ? 1 : 0;  // every (aligned) chunk inside one block
   // group sums: 12 B per work slot of THIS launch (a rank's share of a split
   // frame holds only its own blocks' sums)
-  HIPCHK(c->partial[slot].reserve((size_t)std::max<int64_t>(slots, 1) * 3));
+  HIPCHK(c->partial[slot].reserve((size_t)std::max<int64_t>(slots, 1) * PT_SUM_WORDS));
   P.partial = c->partial[slot].p;
-  c->last.partial_bytes = slots * 12;
+  c->last.partial_bytes = slots * 4 * PT_SUM_WORDS;
   auto log2_exact = [](int v) {  // log2(v) for a power of two, else -1
     int k = 0;
     while ((1 << k) < v && k < 30) ++k;

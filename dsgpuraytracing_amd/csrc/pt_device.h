@@ -30,6 +30,13 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #ifndef PT_GROUP_MIN_SLOTS
 #define PT_GROUP_MIN_SLOTS 24  // groups are halved until the traced samples make this many slots per lane
 #endif
+// Floats per group sum in memory: 3 (packed float3, 12 B) or 4 (float4, 16 B:
+// every record inside one 16-B aligned chunk -- the write-back experiment of
+// round 5).
+#ifndef PT_SUM_WORDS
+#define PT_SUM_WORDS 3
+#endif
+static_assert(PT_SUM_WORDS == 3 || PT_SUM_WORDS == 4, "PT_SUM_WORDS is 3 or 4");
 #ifndef PT_GROUP_SUM_GIB
 #define PT_GROUP_SUM_GIB 8  // group-sum budget per render slot (GiB): a group size that needs more doubles
 #endif

@@ -81,6 +81,10 @@ __device__ __forceinline__ void store3(float* p, float3 v) {
 #define PT_NT_SUMS 0
 #endif
 __device__ __forceinline__ void store_sum(float* p, float3 v) {
+#if PT_SUM_WORDS == 4
+  *(float4*)p = make_float4(v.x, v.y, v.z, 0.0f);
+  return;
+#endif
 #if PT_NT_SUMS
   __builtin_nontemporal_store(v.x, p);
   __builtin_nontemporal_store(v.y, p + 1);
@@ -162,26 +166,43 @@ struct Counters {
 // The closest hit is (tmax, prim): the shading round rebuilds the barycentrics
 // and reads the material from the primitive record, so no more of the hit is
 // carried through traversal (every persistent value costs a VGPR in all waves).
-// The ray keeps its reciprocal direction only: the direction is re-derived
-// where a primitive test or the shading round needs it (tdir, three v_rcp_f32),
-// which frees three VGPRs in every wave (round 5: the 8-wide node step's nine
-// loads and per-node coefficients would otherwise spill).  Every consumer
-// derives it the same way, so the hit record's barycentrics still equal the
-// traversal test's bit for bit.
+// PT_TRAV_DIR 0: the ray keeps its reciprocal direction only and re-derives
+// the direction where a primitive test or the shading round needs it (tdir,
+// three v_rcp_f32) -- three VGPRs fewer in every wave, which the 8-wide node
+// step needs to stay spill-free; every consumer derives it the same way, so
+// the hit record's barycentrics still equal the traversal test's bit for bit.
+// With 4-wide nodes the direction is kept (the re-derivation measured C3
+// -1.1%, framed C3 -0.5%, C5 -2.1%: profiles/r5/ab_dfree_*.txt).
+#ifndef PT_TRAV_DIR
+#define PT_TRAV_DIR (PT_NODE_WIDTH == 4)
+#endif
 struct Trav {
+#if PT_TRAV_DIR
+  float3 o, d, inv;
+#else
   float3 o, inv;
+#endif
   float tmax;
   int node, sp;
   int prim;
   bool any, found;
 };
-__device__ __forceinline__ float3 tdir(const Trav& t) { return f3(rcp(t.inv.x), rcp(t.inv.y), rcp(t.inv.z)); }
+__device__ __forceinline__ float3 tdir(const Trav& t) {
+#if PT_TRAV_DIR
+  return t.d;
+#else
+  return f3(rcp(t.inv.x), rcp(t.inv.y), rcp(t.inv.z));
+#endif
+}
 
 __device__ __forceinline__ void trav_init(Trav& tr, float3 o, float3 d, float tmax, bool any) {
   const float kTiny = 1e-20f;
   float3 dd = f3(fabsf(d.x) < kTiny ? copysignf(kTiny, d.x) : d.x, fabsf(d.y) < kTiny ? copysignf(kTiny, d.y) : d.y,
                  fabsf(d.z) < kTiny ? copysignf(kTiny, d.z) : d.z);
   tr.o = o;
+#if PT_TRAV_DIR
+  tr.d = d;
+#endif
   tr.inv = f3(rcp(dd.x), rcp(dd.y), rcp(dd.z));
   tr.tmax = tmax;
   tr.node = 0;
@@ -313,11 +334,52 @@ __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb) {
   ra = tr;
 }
 
+// Child order of a node step (PT_NODE_ORDER): 1 = continue with the NEAREST
+// entered child and push the other entered ones in slot order (slot 3 first,
+// the lowest slot on top); 0 = the round-1..4 full sort (5-exchange network,
+// farthest pushed first).  Rays enter 1.02 children per node on average, so
+// the order of the pushed ones hardly matters: the CPU traversal census of
+// the C3 ray mix (tools/wide_sim.cpp) gives the same node and leaf steps per
+// ray for both (camera 6.40 / 6.40, bounce 7.17 / 7.13, shadow 6.00 / 6.00),
+// and the nearest-only selection is a third of the network's VALU.
+#ifndef PT_NODE_ORDER
+#define PT_NODE_ORDER 1
+#endif
+
 // Second half of a node step: entry distances d (kMiss = not entered) and
 // references rf of the four children -> continue with the nearest, push the
-// other hits farthest first.
+// other hits.
 __device__ __forceinline__ bool node_order(const Stack& stk, Trav& tr, const float* d, const int4 rf) {
   const float kMiss = 3.0e38f;
+#if PT_NODE_ORDER == 1
+  {
+    const int r[4] = {rf.x, rf.y, rf.z, rf.w};
+    float dmin = d[0];
+    int rn = r[0];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const bool nearer = d[k] < dmin;
+      dmin = fminf(dmin, d[k]);
+      rn = nearer ? r[k] : rn;
+    }
+    if (dmin == kMiss) return trav_pop(stk, tr);
+    int sp = tr.sp;
+    if (sp + 4 <= PT_STACK) {
+#pragma unroll
+      for (int k = 3; k >= 0; --k) {
+        stk.lds[sp * PT_BLOCK] = r[k];
+        sp += d[k] != kMiss && r[k] != rn;
+      }
+    } else {
+#pragma unroll
+      for (int k = 3; k >= 0; --k)
+        if (d[k] != kMiss && r[k] != rn) stk.put(sp++, r[k]);
+    }
+    tr.sp = sp;
+    tr.node = rn;
+    return false;
+  }
+#endif
   int r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
   float d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3];
   // near-first order: 5-exchange sorting network on the entry distances
@@ -719,6 +781,9 @@ enum : int { SH_RESUME = 1, SH_FOLLOW = 2, SH_STORE = 3, SH_STORE_FOLLOW = 4 };
 #ifndef PT_STATIC_FIRST
 #define PT_STATIC_FIRST 1
 #endif
+#ifndef PT_BALLOT_SPLIT
+#define PT_BALLOT_SPLIT 1
+#endif
 
 // Wave-clock sections of the STATS build: every shader clock of a wave's
 // lifetime falls in exactly one (pt_stats.shade_clocks + trav_clocks = the
@@ -929,12 +994,16 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // light sample (or store the group's total with it) and go on with the
   // next extension ray -- or retire -- without a shading round.
   auto follow_on = [&](bool done) {
+#if PT_BALLOT_SPLIT
+    {  // (the divergent branch alone skips itself when no lane takes it)
+#else
     if (__ballot(done && shadow >= SH_FOLLOW) != 0ull) {
+#endif
       if (done && shadow >= SH_FOLLOW) {
         if (shadow == SH_FOLLOW) {
           if (!tr.found) acc = acc + pend;
         } else {  // the finished group's one store: its total with the light sample if the shadow ray is clear
-          store_sum(P.partial + 3 * (size_t)oslot, tr.found ? acc : pend);
+          store_sum(P.partial + PT_SUM_WORDS * (size_t)oslot, tr.found ? acc : pend);
           acc = ng;  // the new group's sum so far (environment seen by its camera rays that missed)
         }
         if (shadow == SH_STORE) {
@@ -1200,7 +1269,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         }
       }
       if (group_end) {
-        store_sum(P.partial + 3 * (size_t)myslot, acc);
+        store_sum(P.partial + PT_SUM_WORDS * (size_t)myslot, acc);
         PT_SLOT_DONE();
         mode = M_FETCH;
       }
@@ -1383,7 +1452,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             ng = f3(0, 0, 0);  // (the next group's sum while the store is pending)
             shadow = SH_STORE;
           } else {  // SH_STORE: this group's sum is in ng (acc holds the last group's)
-            store_sum(P.partial + 3 * (size_t)myslot, shadow ? ng : acc);
+            store_sum(P.partial + PT_SUM_WORDS * (size_t)myslot, shadow ? ng : acc);
           }
           PT_SLOT_DONE();
           mode = M_FETCH;
@@ -1445,8 +1514,17 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       // a leaf (or nothing else is left), node steps otherwise
       const bool trav = mode == M_TRAV;
       const bool at_leaf = trav && tr.node < 0;
+#if PT_BALLOT_SPLIT
+      // ballots of single compares, combined in SGPRs: a ballot of a combined
+      // condition is re-materialised through a VGPR (v_cndmask + v_cmp) by the
+      // compiler, twice per iteration
+      const unsigned long long b_trav = __ballot(mode == M_TRAV), b_leaf = __ballot(tr.node < 0);
+      const int n_leaf = __popcll(b_trav & b_leaf);
+      const int n_node = __popcll(b_trav & ~b_leaf);
+#else
       const int n_leaf = __popcll(__ballot(at_leaf));
       const int n_node = __popcll(__ballot(trav && !at_leaf));
+#endif
       bool done = false;
       const bool leaf_iter = n_leaf > 0 && (n_node == 0 || n_leaf * t_leaf_weight >= n_node * 16);
       if (STATS && trav) {
@@ -1609,9 +1687,9 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
     const int4 b = P.blocks[k];
     if (qx >= b.z || qy >= b.w) continue;
     float3 acc = f3(0, 0, 0);
-    const float* pa = P.partial + 3 * ((size_t)k * 64u + (size_t)q) * (size_t)P.n_groups;
+    const float* pa = P.partial + PT_SUM_WORDS * ((size_t)k * 64u + (size_t)q) * (size_t)P.n_groups;
 #pragma unroll 2
-    for (int j = 0; j < P.n_groups; ++j) acc = acc + ld3(pa + 3 * (size_t)j);
+    for (int j = 0; j < P.n_groups; ++j) acc = acc + ld3(pa + PT_SUM_WORDS * (size_t)j);
     store3(out_at(b.x + qx, b.y + qy), acc * inv_spp);
   }
 }

@@ -14,8 +14,10 @@
 //   render : writes the HDR sampleBuffer (float32 W*H*3, y=0 bottom) to a PTDUMP
 //   tiles  : times PathTracer::raytrace_tile (pathtracer.cpp:585-611) on every
 //            --tile-stride-th 32x32 tile of the FIFO from --tile-begin, on this
-//            one thread (the -t 1 worker's work, glibc rand() as shipped) — the
-//            CPU baseline of bench.py on a bounded sample of a frame
+//            one thread (the -t 1 worker's work, glibc rand() as shipped), or
+//            with -t T on T threads popping those tiles from one shared queue
+//            as the reference's workers do (its published -t 8 setting) — the
+//            CPU baselines of bench.py on a bounded sample of a frame
 //   dump   : writes the flattened scene the GPU seam would receive (PTDUMP)
 //   rays   : answers BVHAccel::intersect nearest/any-hit queries (KATs)
 //   rng    : prints the first rand() draws and the sampler draw order
@@ -48,10 +50,12 @@
 #include "static_scene/sphere.h"
 #include "static_scene/triangle.h"
 
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ptdump.h"
@@ -535,16 +539,32 @@ int main(int argc, char** argv) {
     pt->tile_samples.assign(pt->num_tiles_w * pt->num_tiles_h, 0);
     const size_t ntx = (o.w + 31) / 32, nt = ntx * ((o.h + 31) / 32);
     size_t px = 0, n = 0;
-    std::srand(o.seed);
-    auto t0 = std::chrono::steady_clock::now();
+    std::vector<size_t> sample;
     for (size_t i = o.tile_begin; i < nt; i += o.tile_stride) {
       const size_t tx = (i % ntx) * 32, ty = (i / ntx) * 32;
-      pt->raytrace_tile((int)tx, (int)ty, 32, 32);
+      sample.push_back(i);
       px += (std::min(o.w, tx + 32) - tx) * (std::min(o.h, ty + 32) - ty);
       ++n;
     }
+    std::srand(o.seed);
+    // -t T: T threads popping the sample's tiles from one shared queue and
+    // calling raytrace_tile, as the reference's worker_thread does
+    // (pathtracer.cpp:613-637; rand() stays the one shared glibc stream)
+    std::atomic<size_t> next{0};
+    auto worker = [&]() {
+      for (size_t k; (k = next.fetch_add(1)) < sample.size();) {
+        const size_t i = sample[k];
+        pt->raytrace_tile((int)((i % ntx) * 32), (int)((i / ntx) * 32), 32, 32);
+      }
+    };
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> pool;
+    for (size_t t = 1; t < std::max<size_t>(1, o.threads); ++t) pool.emplace_back(worker);
+    worker();
+    for (auto& th : pool) th.join();
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    std::printf("{\"render_s\": %.6f, \"pixels\": %zu, \"tiles\": %zu, \"spp\": %zu}\n", secs, px, n, o.spp);
+    std::printf("{\"render_s\": %.6f, \"pixels\": %zu, \"tiles\": %zu, \"spp\": %zu, \"threads\": %zu}\n", secs, px, n,
+                o.spp, std::max<size_t>(1, o.threads));
     return 0;
   }
   // render (main.cpp:170-181 with srand moved next to the render)

@@ -438,7 +438,8 @@ int main(int argc, char** argv) {
     Order o;
   } layouts[] = {{"BVH2", &t2, SORT},        {"BVH4 sort", &t4, SORT},       {"BVH8 sort", &t8, SORT},
                  {"BVH8 octant", &t8, OCT},  {"BVH8 near+slot", &t8, NEAR_SLOT}, {"BVH8 near+oct", &t8, NEAR_OCT},
-                 {"BVH8 fp16 sort", &t8q, SORT}, {"BVH8 fp16 n+slot", &t8q, NEAR_SLOT}};
+                 {"BVH8 fp16 sort", &t8q, SORT}, {"BVH8 fp16 n+slot", &t8q, NEAR_SLOT},
+                 {"BVH4 near+slot", &t4, NEAR_SLOT}};
   for (int s = 0; s < 3; ++s) {
     std::printf("-- %s rays (%zu)\n", names[s], sets[s]->size());
     for (const L& l : layouts) {
