@@ -249,6 +249,7 @@ struct pt_ctx {
   int bvh_stack = 0;  // worst-case traversal stack entries of the uploaded BVH
   size_t n_render_nodes = 0;
   int64_t n_prims = 0;
+  bool tri_only = false;  // every primitive a triangle
   float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
   double root_lo_d[3] = {0, 0, 0}, root_hi_d[3] = {0, 0, 0};
   bool have_scene = false, have_cam = false, have_params = false;
@@ -897,6 +898,7 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
   c->n_lights = (int)ls.size();
   c->n_bsdfs = (int)bs.size();
   c->n_prims = s->n_prims;
+  c->tri_only = std::all_of(s->prim_type, s->prim_type + s->n_prims, [](int t) { return t == PT_PRIM_TRIANGLE; });
   c->have_scene = true;
   return PT_OK;
 }
@@ -1154,6 +1156,9 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     if (v >= 1) P.leaf_weight = v;
   }
   P.census = census_launch ? 1 : 0;  // diagnostics (tools/wave_trace.py --census)
+  // triangle-only scenes take the render kernel without the sphere test
+  // (branch-free leaf steps); PT_NO_TRI_ONLY forces the mixed one (A/B, tests)
+  P.tri_only = c->tri_only && !std::getenv("PT_NO_TRI_ONLY") ? 1 : 0;
   P.drain_div = 0;
   if (const char* dd = std::getenv("PT_DRAIN_DIV")) {  // tuning knob
     int v = std::atoi(dd);

@@ -101,15 +101,29 @@ __host__ __device__ inline int record_lower_bound(const float* __restrict__ a, f
                                                   const EnvRec* __restrict__ rec, int G, float& prev, float& cur) {
   int k = (int)(r * (float)G);
   k = k < 0 ? 0 : k > G - 1 ? G - 1 : k;
-  // one 32-B copy of the record (two 16-B loads on the device).  (Reading it as
-  // two float4 and bit-casting the int fields out of their elements misread
-  // the window in host code -- clang's __builtin_bit_cast of a vector element
-  // returns element 0 there -- which the host replay caught.)
+#if defined(__HIP_DEVICE_COMPILE__)
+  // the record as two 16-B vector loads, both issued before the window test:
+  // read through a 32-B struct copy, the compiler loads (lo, hi, wm) first and
+  // sinks the w_i loads behind the branch -- a second dependent round trip
+  // (C5 -1.5%, round 5)
+  typedef float rf4 __attribute__((ext_vector_type(4)));
+  const rf4 q0 = ((const rf4*)(rec + k))[0];
+  rf4 q1 = ((const rf4*)(rec + k))[1];
+  asm volatile("" : "+v"(q1));
+  int lo = __float_as_int(q0.x);
+  const int hi = __float_as_int(q0.y);
+  float wm = q0.z, w0 = q0.w, w1 = q1.x, w2 = q1.y, w3 = q1.z, w4 = q1.w;
+#else
+  // host replay: one 32-B copy of the record.  (Bit-casting the int fields
+  // out of float4 elements misread the window in host code -- clang's
+  // __builtin_bit_cast of a vector element returns element 0 there -- which
+  // the host replay caught.)
   EnvRec e;
   __builtin_memcpy(&e, rec + k, sizeof(EnvRec));
   int lo = e.lo;
   const int hi = e.hi;
   float wm = e.wm, w0 = e.w0, w1 = e.w1, w2 = e.w2, w3 = e.w3, w4 = e.w4;
+#endif
   int n = hi - lo;
   if (n > 4) {
     while (n > 4) {
@@ -275,6 +289,7 @@ struct KParams {
   int shade_batch;            // leave the traversal phase once this many lanes finished their ray
   int leaf_weight;            // leaf steps run when leaf_weight * leaf lanes >= 16 * node lanes
   int drain_div;              // queue drained: shade once alive/drain_div lanes are ready (0: 3/4 rule)
+  int tri_only;               // every primitive is a triangle: the kernel without the sphere test
   int census;                 // plain build: record each wave's start / end / CU / drain in the trace area (PT_CENSUS)
   float root_lo[3], root_hi[3];  // scene bounds (root box, rounded outward)
   int cull_x0, cull_y0, cull_x1, cull_y1;  // pixels outside [x0,x1]x[y0,y1] see no geometry

@@ -341,9 +341,12 @@ __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb) {
 // the order of the pushed ones hardly matters: the CPU traversal census of
 // the C3 ray mix (tools/wide_sim.cpp) gives the same node and leaf steps per
 // ray for both (camera 6.40 / 6.40, bounce 7.17 / 7.13, shadow 6.00 / 6.00),
-// and the nearest-only selection is a third of the network's VALU.
+// and the nearest-only selection is a third of the network's VALU.  On the
+// GPU the network measured faster all the same (same session, 3 rounds: C3
+// +1.3%, lone launch -2.5%; C5 +1.8%: profiles/r5/ab_order_ballot.txt), so it
+// stays the default.
 #ifndef PT_NODE_ORDER
-#define PT_NODE_ORDER 1
+#define PT_NODE_ORDER 0
 #endif
 
 // Second half of a node step: entry distances d (kMiss = not entered) and
@@ -630,7 +633,7 @@ __device__ __forceinline__ bool node_step2(const DNode2* __restrict__ nodes, con
 __device__ __forceinline__ int leaf_first(int cur) { return (~cur) >> 3; }
 __device__ __forceinline__ int leaf_count(int cur) { return ((~cur) & 7) + 1; }
 
-template <bool STATS>
+template <bool STATS, bool TRI = false>
 __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const Stack& stk, Trav& tr,
                                           Counters& ct) {
   const int pa = leaf_first(tr.node);
@@ -646,8 +649,37 @@ __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const
   // triple for one-primitive steps measured -2%: the branch costs more.)
   PT_FENCE4(a2);
   PT_FENCE4(b2);
-  if (prim_test<STATS>(a0, a1, a2, pa, tr, ct)) return true;
-  if (two && prim_test<STATS>(b0, b1, b2, pb, tr, ct)) return true;
+  if constexpr (TRI) {
+    // Triangle-only scene: both Moller-Trumbore tests without branches (the
+    // mixed build's per-primitive type test, det == 0 exit and sphere code
+    // cost exec-mask bookkeeping in every leaf step).  Same predicate and
+    // order as prim_test: the second triangle is tested against the tmax
+    // the first left.  An occlusion ray that the first triangle already
+    // stops may take the second one's (t, prim) as well -- only `found` is
+    // read after an occlusion query.
+    // (all six loads complete at one wait: without the fence the scheduler
+    // waits for the first triple before it issues the second)
+    PT_FENCE4(a0);
+    PT_FENCE4(a1);
+    PT_FENCE4(b0);
+    PT_FENCE4(b1);
+    const float3 o = tr.o, d = tdir(tr);
+    float ua, va, ta, ub, vb, tb;
+    const float da = mt_terms(o, d, f3(a0.x, a0.y, a0.z), f3(a1.x, a1.y, a1.z), f3(a2.x, a2.y, a2.z), ua, va, ta);
+    const float db = mt_terms(o, d, f3(b0.x, b0.y, b0.z), f3(b1.x, b1.y, b1.z), f3(b2.x, b2.y, b2.z), ub, vb, tb);
+    // (bitwise &: no short-circuit exec-mask blocks)
+    const bool ha = (da != 0.0f) & (ua >= 0.0f) & (va >= 0.0f) & (ua + va <= 1.0f) & (ta > 0.0f) & (ta < tr.tmax);
+    const float tm = ha ? ta : tr.tmax;
+    const bool hb = two & (db != 0.0f) & (ub >= 0.0f) & (vb >= 0.0f) & (ub + vb <= 1.0f) & (tb > 0.0f) & (tb < tm);
+    tr.tmax = hb ? tb : tm;
+    tr.prim = hb ? pb : ha ? pa : tr.prim;
+    tr.found = tr.found || ha || hb;
+    if (STATS) ct.tris += two ? 2u : 1u;
+    if (tr.any && (ha || hb)) return true;
+  } else {
+    if (prim_test<STATS>(a0, a1, a2, pa, tr, ct)) return true;
+    if (two && prim_test<STATS>(b0, b1, b2, pb, tr, ct)) return true;
+  }
   if (n > 2) {
     tr.node = ~(((pa + 2) << 3) | (n - 3));
     return false;
@@ -784,6 +816,35 @@ enum : int { SH_RESUME = 1, SH_FOLLOW = 2, SH_STORE = 3, SH_STORE_FOLLOW = 4 };
 #ifndef PT_BALLOT_SPLIT
 #define PT_BALLOT_SPLIT 1
 #endif
+// Instruction-cost probes (diagnostics, 0 = off): N extra independent SALU or
+// VALU instructions per traversal iteration (PT_PROBE_TRAV_*) or per shading
+// round (PT_PROBE_SHADE_*), to price one more instruction of each kind in each
+// phase (tools/ab.sh against the plain build).
+#ifndef PT_PROBE_TRAV_SALU
+#define PT_PROBE_TRAV_SALU 0
+#endif
+#ifndef PT_PROBE_TRAV_VALU
+#define PT_PROBE_TRAV_VALU 0
+#endif
+#ifndef PT_PROBE_SHADE_SALU
+#define PT_PROBE_SHADE_SALU 0
+#endif
+#ifndef PT_PROBE_SHADE_VALU
+#define PT_PROBE_SHADE_VALU 0
+#endif
+template <int NS, int NV>
+__device__ __forceinline__ void probe_insts() {
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    int s;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(s) : "i"(k));
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    int v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "i"(k));
+  }
+}
 
 // Wave-clock sections of the STATS build: every shader clock of a wave's
 // lifetime falls in exactly one (pt_stats.shade_clocks + trav_clocks = the
@@ -804,7 +865,8 @@ enum : int { S_HIT = 0, S_NEE = 1, S_BSDF = 2, S_FETCH = 3, S_CAMERA = 4, S_TRAV
 // GTAB: material/light tables larger than the LDS copies (read from global
 // memory; the common build reads them from LDS through address-space-typed
 // pointers, never through FLAT accesses).
-template <bool STATS, bool DBG, bool BIN, bool ENV, bool GTAB>
+// TRI: every primitive is a triangle (branch-free leaf steps, no sphere test).
+template <bool STATS, bool DBG, bool BIN, bool ENV, bool GTAB, bool TRI = false>
 __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel(KParams P) {
   // the wave's PT_STACK x 64 LDS stack (lane-contiguous rows)
   __shared__ int s_stack[PT_STACK * PT_BLOCK];
@@ -1024,6 +1086,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     // the shading round issues at raised wave priority, traversal at the
     // base one (C4 +0.6%, C5 +0.4%, C3 within noise: profiles/r3/ab_build_options.txt)
     __builtin_amdgcn_s_setprio(2);
+    probe_insts<PT_PROBE_SHADE_SALU, PT_PROBE_SHADE_VALU>();
     // ================= shading phase: lanes whose ray finished =================
     if (mode == M_SHADE) {
       const bool found = tr.found;
@@ -1544,7 +1607,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       // and stepping both kinds once the queue is drained did not win it back:
       // profiles/r4/ab_bisect_2.txt)
       if (leaf_iter) {
-        if (at_leaf) done = leaf_step<STATS>(t_prims, stk, tr, ct);
+        if (at_leaf) done = leaf_step<STATS, TRI>(t_prims, stk, tr, ct);
         if (STATS) n_leafit += lane == 0;
       } else if (trav && !at_leaf) {
         if constexpr (BIN) done = node_step2<STATS>(P.nodes2, stk, tr, ct);
@@ -1552,6 +1615,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       }
       if (done) mode = M_SHADE;
       follow_on(done);
+      probe_insts<PT_PROBE_TRAV_SALU, PT_PROBE_TRAV_VALU>();
       if (STATS && done) {
         ray_steps_max = max(ray_steps_max, r_steps);
         ray_idle_max = max(ray_idle_max, r_idle);
@@ -1733,8 +1797,12 @@ static void launch_render(const KParams* P, int waves, bool stats, bool ref_coun
     hipLaunchKernelGGL((ptk::render_kernel<true, false, true, ENV, GTAB>), dim3(grid), blk, 0, s, *P);
   else if (P->dbg_pix >= 0)
     hipLaunchKernelGGL((ptk::render_kernel<false, true, false, ENV, GTAB>), dim3(grid), blk, 0, s, *P);
+  else if (stats && P->tri_only && !GTAB)
+    hipLaunchKernelGGL((ptk::render_kernel<true, false, false, ENV, GTAB, true>), dim3(grid), blk, 0, s, *P);
   else if (stats)
     hipLaunchKernelGGL((ptk::render_kernel<true, false, false, ENV, GTAB>), dim3(grid), blk, 0, s, *P);
+  else if (P->tri_only && !GTAB)
+    hipLaunchKernelGGL((ptk::render_kernel<false, false, false, ENV, GTAB, true>), dim3(grid), blk, 0, s, *P);
   else
     hipLaunchKernelGGL((ptk::render_kernel<false, false, false, ENV, GTAB>), dim3(grid), blk, 0, s, *P);
 }

@@ -234,6 +234,47 @@ def test_screen_footprint_culling_is_exact(monkeypatch, scene, w, h):
         assert st["culled_samples"] > 0
 
 
+def _render_dae(dae, env, w, h, spp, seed, tiles=None, stats=False):
+    sc = Scene.from_dae(dae, w, h, envmap=env)
+    pt = PathTracer(ns_aa=spp, max_ray_depth=4, ns_area_light=1, seed=seed)
+    pt.set_frame_size(w, h)
+    pt.set_camera(sc.camera)
+    pt.set_scene(sc)
+    if tiles is None:
+        pt.start_raytracing(stats=stats)
+    else:
+        pt.render_tiles(tiles, stats=stats)
+    return pt.sampleBuffer.copy(), pt.last_stats
+
+
+@pytest.mark.parametrize("name", ["CBbunny", "c3proxy", "c5proxy"])
+def test_triangle_only_kernel_is_identical(monkeypatch, name):
+    """Triangle-only scenes run the render kernel whose leaf steps test both
+    triangles without branches and without the sphere test (TRI); the mixed
+    kernel (PT_NO_TRI_ONLY) renders the same bits -- whole frame, tile shards,
+    launch counters on -- with the environment-light build (c5proxy) too."""
+    from dsgpuraytracing_amd import scenes
+    dae, env = {"CBbunny": (os.path.join(ROOT, "assets", "CBbunny.dae"), None),
+                "c3proxy": (scenes.proxy_path(1), None),
+                "c5proxy": (scenes.c5_path(2), scenes.c5_envmap_path())}[name]
+    w = h = 96
+    a, st = _render_dae(dae, env, w, h, 8, 17, stats=True)
+    monkeypatch.setenv("PT_NO_TRI_ONLY", "1")
+    b, st2 = _render_dae(dae, env, w, h, 8, 17, stats=True)
+    assert np.array_equal(a, b)
+    assert st["camera_rays"] == st2["camera_rays"] and st["shadow_rays"] == st2["shadow_rays"]
+    assert st["node_visits"] == st2["node_visits"]
+    monkeypatch.delenv("PT_NO_TRI_ONLY")
+    c, _ = _render_dae(dae, env, w, h, 8, 17)
+    assert np.array_equal(a, c)
+    tiles = tile_fifo(w, h)
+    parts = np.zeros_like(a)
+    for shard in range(2):
+        p, _ = _render_dae(dae, env, w, h, 8, 17, tiles=tiles[shard::2])
+        parts += p
+    assert np.array_equal(parts, a)
+
+
 @pytest.mark.parametrize("scene", ["CBspheres_64x64", "c1env_64x64"])
 def test_global_table_variant_is_identical(monkeypatch, scene):
     """Scenes with more BSDFs/lights than the LDS copies hold use the kernel
