@@ -285,6 +285,9 @@ __device__ __forceinline__ bool prim_test(const float4 v0, const float4 e1, cons
 // compiler merge the LDS / spill paths into FLAT accesses, which occupy the
 // vector-memory (TA/TD) path the node and primitive fetches need.
 typedef __attribute__((address_space(3))) int lds_int;
+#ifndef PT_SPILL_WAIT
+#define PT_SPILL_WAIT 1
+#endif
 
 struct Stack {
   lds_int* lds;   // s_stack + lane, stride PT_BLOCK
@@ -312,6 +315,12 @@ struct Stack {
       v = lds[i * PT_BLOCK];
     } else {
       v = *spill_at(i);
+#if PT_SPILL_WAIT
+      // wait for the (rare) spill load here: otherwise the loop latch and
+      // header wait vmcnt(0) for it on every iteration, and with it for the
+      // group-sum stores the iteration issued
+      asm volatile("" : "+v"(v));
+#endif
     }
     return v;
   }
@@ -322,6 +331,30 @@ __device__ __forceinline__ bool trav_pop(const Stack& stk, Trav& tr) {
   --tr.sp;
   tr.node = stk.get(tr.sp);
   return false;
+}
+
+// Stack fast path (PT_STACK_FAST): when no lane of the wave can touch the
+// global spill area in this step (a wave-uniform ballot), pushes and pops are
+// plain LDS accesses without per-lane branches: the divergent push / pop
+// blocks, each with its own spill test, cost ~20 scalar instructions of
+// exec-mask bookkeeping per traversal iteration, and a scalar instruction in
+// the traversal loop costs more than a vector one (profiles/r5/probes_inst_cost.txt).
+#ifndef PT_STACK_FAST
+#define PT_STACK_FAST 1
+#endif
+#ifndef PT_SEL_SIMPLE
+#define PT_SEL_SIMPLE 1
+#endif
+// Pop for the lanes with `pop` set, every lane's stack top in LDS (sp <=
+// PT_STACK); returns true for a lane whose stack was empty (its traversal is
+// over).  The LDS read is issued for every lane (entry 0 for an empty stack).
+__device__ __forceinline__ bool trav_pop_lds(const Stack& stk, Trav& tr, bool pop) {
+  const int spm = max(tr.sp - 1, 0);
+  const int top = stk.lds[spm * PT_BLOCK];
+  const bool done = pop && tr.sp == 0;
+  tr.node = pop ? top : tr.node;
+  tr.sp = pop ? spm : tr.sp;
+  return done;
 }
 
 __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb) {
@@ -391,6 +424,25 @@ __device__ __forceinline__ bool node_order(const Stack& stk, Trav& tr, const flo
   cswap(d0, r0, d2, r2);
   cswap(d1, r1, d3, r3);
   cswap(d1, r1, d2, r2);
+#if PT_STACK_FAST
+  if (__ballot(tr.sp > PT_STACK - 3) == 0ull) {  // (wave-uniform) three pushes and a pop stay in LDS
+    // the hits are a sorted prefix: all three candidates are written, the top
+    // advances past hits only; a lane that entered no child pushed nothing
+    // and pops
+    int sp = tr.sp;
+    stk.lds[sp * PT_BLOCK] = r3;
+    sp += d3 != kMiss;
+    stk.lds[sp * PT_BLOCK] = r2;
+    sp += d2 != kMiss;
+    stk.lds[sp * PT_BLOCK] = r1;
+    sp += d1 != kMiss;
+    tr.sp = sp;
+    tr.node = r0;
+    const bool miss = d0 == kMiss;
+    if (__ballot(miss) == 0ull) return false;
+    return trav_pop_lds(stk, tr, miss);
+  }
+#endif
   if (d0 == kMiss) return trav_pop(stk, tr);
   // push the farther hits (farthest first), continue with the nearest.  The
   // hits are a sorted prefix, so with room for three entries every candidate
@@ -675,6 +727,16 @@ __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const
     tr.prim = hb ? pb : ha ? pa : tr.prim;
     tr.found = tr.found || ha || hb;
     if (STATS) ct.tris += two ? 2u : 1u;
+#if PT_STACK_FAST
+    if (__ballot(tr.sp > PT_STACK) == 0ull) {  // (wave-uniform) every pop reads LDS
+      const bool stop = tr.any & (ha | hb);   // occlusion found: the ray is done
+      const bool more = n > 2;                // the leaf's next two primitives
+      tr.node = more ? ~(((pa + 2) << 3) | (n - 3)) : tr.node;
+      const bool pop = !stop & !more;
+      if (__ballot(pop) == 0ull) return stop;
+      return stop | trav_pop_lds(stk, tr, pop);
+    }
+#endif
     if (tr.any && (ha || hb)) return true;
   } else {
     if (prim_test<STATS>(a0, a1, a2, pa, tr, ct)) return true;
@@ -1589,7 +1651,14 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       const int n_node = __popcll(__ballot(trav && !at_leaf));
 #endif
       bool done = false;
+#if PT_SEL_SIMPLE
+      // (n_leaf > 0 and n_node == 0 need no tests of their own: some lane
+      // traverses, so n_leaf * w >= n_node * 16 is false for n_leaf == 0 and
+      // true for n_node == 0 -- two scalar compare-and-branches fewer)
+      const bool leaf_iter = n_leaf * t_leaf_weight >= n_node * 16;
+#else
       const bool leaf_iter = n_leaf > 0 && (n_node == 0 || n_leaf * t_leaf_weight >= n_node * 16);
+#endif
       if (STATS && trav) {
         const bool stepped = leaf_iter == at_leaf;
         r_steps += stepped;

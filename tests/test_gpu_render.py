@@ -469,9 +469,20 @@ def test_hip_deep_bvh_stack_spill_vs_restatement(monkeypatch, restate, tmp_path)
     hit, t, prim, anyh = dev.intersect(o, dr, maxt)
     dev.set_camera(sc.camera)
     dev.set_params(64, 64, 2, 4, 1, 1)
-    dev.render_tiles([(0, 0, 64, 64)], np.zeros((64, 64, 3), np.float32))  # the render path with spill on
+    img = np.zeros((64, 64, 3), np.float32)
+    dev.render_tiles([(0, 0, 64, 64)], img)  # the render path with spill on
     st = dev.stats()
     assert st["bvh_stack"] > 32
+    # the render kernel's traversal with stacks past PT_STACK (the LDS fast
+    # path and the spill path side by side in one wave), triangle-only kernel
+    # and mixed kernel, against the restatement
+    ref, _ = restate.render(path, 64, 64, 2, 4, 1, 1, rng_mode=1, threads=2)
+    close = (np.abs(img - ref).max(axis=2) <= 1e-3 * np.maximum(1.0, np.abs(ref).max(axis=2))).mean()
+    assert close >= 0.99, close
+    monkeypatch.setenv("PT_NO_TRI_ONLY", "1")
+    img2 = np.zeros((64, 64, 3), np.float32)
+    dev.render_tiles([(0, 0, 64, 64)], img2)
+    assert np.array_equal(img, img2)
     rh, rt, rp, _, ra = restate.intersect(path, o.reshape(-1), dr.reshape(-1), maxt)
     assert hit.mean() > 0.3 and np.array_equal(hit, rh)
     both = hit == 1

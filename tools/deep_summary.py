@@ -9,10 +9,10 @@ import json
 import os
 import sys
 
-KERNELS = {"c5": "render_kernel<false, false, false, true, false>"}
+KERNELS = {"c5": "render_kernel<false, false, false, true, false"}
 wl, summ = sys.argv[1], sys.argv[2]
 prof = sys.argv[3] if len(sys.argv) > 3 else "gpurun_out/prof"
-K = KERNELS.get(wl, "render_kernel<false, false, false, false, false>")
+K = KERNELS.get(wl, "render_kernel<false, false, false, false, false")
 vals = {}
 for name in ("sq2", "sq3", "tcp", "tcp2", "ta"):
     p = os.path.join(prof, name, f"{name}_counter_collection.csv")

@@ -8,13 +8,13 @@ import json
 import os
 import sys
 
-KERNEL = {"c5": "render_kernel<false, false, false, true, false>",
-          "c5big": "render_kernel<false, false, false, true, false>"}
+KERNEL = {"c5": "render_kernel<false, false, false, true, false",
+          "c5big": "render_kernel<false, false, false, true, false"}
 
 
 def main():
     d, wl = sys.argv[1], sys.argv[2]
-    kern = KERNEL.get(wl, "render_kernel<false, false, false, false, false>")
+    kern = KERNEL.get(wl, "render_kernel<false, false, false, false, false")
     for arm in sorted(os.listdir(d)):
         files = glob.glob(os.path.join(d, arm, "**", "*counter_collection.csv"), recursive=True)
         agg = collections.defaultdict(list)

@@ -26,9 +26,10 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dsgpuraytracing_amd.elfsha import kernel_sha256  # noqa: E402
 
-# render_kernel<STATS, DBG, BIN, ENV, GTAB>: the timed launch of each workload
-KERNELS = {"c5": "render_kernel<false, false, false, true, false>", "c5big": "render_kernel<false, false, false, true, false>"}
-KERNEL = "render_kernel<false, false, false, false, false>"
+# render_kernel<STATS, DBG, BIN, ENV, GTAB[, TRI]>: the timed launch of each workload (prefix:
+# the triangle-only and the mixed instantiation; one bench run launches one of them)
+KERNELS = {"c5": "render_kernel<false, false, false, true, false", "c5big": "render_kernel<false, false, false, true, false"}
+KERNEL = "render_kernel<false, false, false, false, false"
 
 
 def _pmc(path):
