@@ -608,6 +608,72 @@ __device__ void encode8(const float (*lo)[3], const float (*hi)[3], const int* r
   h = make_int4(r[4], r[5], r[6], r[7]);
 }
 
+// Compressed 4-wide node from a DNode: the same quantisation as encode8 over
+// four children (empty slots -- boxes at +inf -- become lo = +inf / hi = -inf
+// halves, never entered).
+__global__ void k_compress4(const DNode* __restrict__ in, int n, DNodeC* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const DNode d = in[i];
+  const float* pl[6] = {&d.lox.x, &d.hix.x, &d.loy.x, &d.hiy.x, &d.loz.x, &d.hiz.x};
+  float lo[4][3], hi[4][3];
+  bool empty[4];
+  float org[3] = {INFINITY, INFINITY, INFINITY};
+  for (int k = 0; k < 4; ++k) {
+    bool e = false;
+    for (int a = 0; a < 3; ++a) {
+      lo[k][a] = pl[2 * a][k];
+      hi[k][a] = pl[2 * a + 1][k];
+      e = e || !(lo[k][a] <= hi[k][a]) || !isfinite(lo[k][a]) || !isfinite(hi[k][a]);
+    }
+    empty[k] = e;
+    if (!e)
+      for (int a = 0; a < 3; ++a) org[a] = fminf(org[a], lo[k][a]);
+  }
+  for (int a = 0; a < 3; ++a)
+    if (!isfinite(org[a])) org[a] = 0.0f;
+  int ex[3];
+  for (int a = 0; a < 3; ++a) {
+    double ext = 0.0;
+    for (int k = 0; k < 4; ++k)
+      if (!empty[k]) ext = fmax(ext, (double)hi[k][a] - (double)org[a]);
+    int e = 0;
+    if (ext > 0.0) {
+      int k2;
+      frexp(ext, &k2);  // ext <= 2^k2
+      e = min(127, max(-128, k2 - 15));  // quantised offsets <= 2^15 < 65504
+    }
+    ex[a] = e;
+  }
+  uint32_t w[3][4];
+  for (int a = 0; a < 3; ++a) {
+    uint16_t ql[4], qh[4];
+    for (int k = 0; k < 4; ++k) {
+      if (empty[k]) {
+        ql[k] = 0x7c00u;  // lo = +inf
+        qh[k] = 0xfc00u;  // hi = -inf
+      } else {
+        ql[k] = half_dir(ldexp((double)lo[k][a] - (double)org[a], -ex[a]), false);
+        qh[k] = half_dir(ldexp((double)hi[k][a] - (double)org[a], -ex[a]), true);
+      }
+    }
+    w[a][0] = ql[0] | ((uint32_t)ql[1] << 16);
+    w[a][1] = ql[2] | ((uint32_t)ql[3] << 16);
+    w[a][2] = qh[0] | ((uint32_t)qh[1] << 16);
+    w[a][3] = qh[2] | ((uint32_t)qh[3] << 16);
+  }
+  DNodeC c;
+  c.ox = org[0];
+  c.oy = org[1];
+  c.oz = org[2];
+  c.ex = (uint32_t)(ex[0] & 0xff) | ((uint32_t)(ex[1] & 0xff) << 8) | ((uint32_t)(ex[2] & 0xff) << 16);
+  c.x = make_uint4(w[0][0], w[0][1], w[0][2], w[0][3]);
+  c.y = make_uint4(w[1][0], w[1][1], w[1][2], w[1][3]);
+  c.z = make_uint4(w[2][0], w[2][1], w[2][2], w[2][3]);
+  c.ref = d.ref;
+  out[i] = c;
+}
+
 __global__ void k_wide(const DNode2* __restrict__ bin, const WItem* __restrict__ in, int n_in, WItem* out,
                        int* n_out, int* n_nodes, int* max_stack, DNode8* nodes, int4* hi4) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -666,6 +732,12 @@ __global__ void k_wide(const DNode2* __restrict__ bin, const WItem* __restrict__
     hipError_t e_ = (x);            \
     if (e_ != hipSuccess) return e_; \
   } while (0)
+
+extern "C" hipError_t ptk_compress4(const DNode* in, int n, DNodeC* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(lbvh::k_compress4, dim3((n + 127) / 128), dim3(128), 0, s, in, n, out);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t ptk_build_wide(const DNode2* bin, int n_bin, WideOut* out, hipStream_t s) {
   using namespace lbvh;

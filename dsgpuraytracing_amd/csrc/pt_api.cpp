@@ -170,6 +170,7 @@ struct pt_ctx {
   DevBuf<DNode> nodes;    // the render tree, PT_NODE_WIDTH 4
   DevBuf<DNode8> nodes8;  // the render tree, PT_NODE_WIDTH 8 (+ children 4..7's references)
   DevBuf<int4> nodes8_hi;
+  DevBuf<DNodeC> nodesc;  // the render tree, PT_NODE_COMPRESS (the compressed copy of nodes)
   DevBuf<DNode2> nodes2;  // binary tree for PT_FLAG_REF_COUNTS
   DevBuf<int> prim_map;   // own BVH order (SAH or GPU-built) -> uploaded primitive index (else empty)
   // primitives in the caller's (reference BVH) order, for the reference-count
@@ -314,6 +315,7 @@ int pt_destroy(pt_ctx* c) {
   c->nodes.release();
   c->nodes8.release();
   c->nodes8_hi.release();
+  c->nodesc.release();
   c->nodes2.release();
   c->prim_map.release();
   c->env_tex.release();
@@ -877,6 +879,14 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
     int rc = build_gpu_bvh(c, s);
     if (rc) return rc;
   }
+#if PT_NODE_COMPRESS
+  // the render tree as compressed nodes (host or GPU tree alike), node for node
+  if (c->n_render_nodes >= (size_t)1 << 24)  // (the node step addresses nodes with a 24-bit multiply)
+    return fail(PT_E_INVALID, "pt_upload_scene: compressed render tree limited to 2^24 nodes");
+  HIPCHK(c->nodesc.reserve(std::max<size_t>(1, c->n_render_nodes)));
+  HIPCHK(ptk_compress4(c->nodes.p, (int)c->n_render_nodes, c->nodesc.p, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+#endif
   HIPCHK(hipMemcpy(c->bsdfs.p, bs.data(), bs.size() * sizeof(DBsdf), hipMemcpyHostToDevice));
   if (!ls.empty()) HIPCHK(hipMemcpy(c->lights.p, ls.data(), ls.size() * sizeof(DLight), hipMemcpyHostToDevice));
   c->env_w = n_env ? s->env_width : 0;
@@ -1113,6 +1123,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.nodes = c->nodes.p;
   P.nodes8 = c->nodes8.p;
   P.nodes8_hi = c->nodes8_hi.p;
+  P.nodesc = c->nodesc.p;
   P.nodes2 = c->nodes2.p;
   P.prims = c->prims.p;
   P.norms = c->norms.p;
@@ -1635,7 +1646,9 @@ int pt_intersect(pt_ctx* c, int64_t n, const double* o, const double* d, const d
     HIPCHK(c->q_spill.reserve((size_t)(c->bvh_stack - PT_STACK) * (size_t)((n + PT_BLOCK - 1) / PT_BLOCK * PT_BLOCK)));
     spill = c->q_spill.p;
   }
-  const void* rnodes = PT_NODE_WIDTH == 8 ? (const void*)c->nodes8.p : (const void*)c->nodes.p;
+  const void* rnodes = PT_NODE_WIDTH == 8 ? (const void*)c->nodes8.p
+                       : PT_NODE_COMPRESS ? (const void*)c->nodesc.p
+                                          : (const void*)c->nodes.p;
   HIPCHK(ptk_launch_intersect(rnodes, c->nodes8_hi.p, c->prims.p, c->q_f.p, c->q_f.p + 3 * n, c->q_f.p + 6 * n, n, dh, dt, dp, da,
                               spill, c->prim_map.p, c->stream));
   std::vector<int32_t> ib((size_t)n * 3);

@@ -200,6 +200,26 @@ struct alignas(16) DNode8 {
 };
 static_assert(sizeof(DNode8) == 128, "DNode8 is one 128-B line");
 
+// Compressed 4-wide node (PT_NODE_COMPRESS, round 5): the same tree as DNode
+// (same children, same leaves), its four child boxes as fp16 offsets from an
+// origin, scaled per axis by 2^e and rounded outward (Ylitie et al. 2017's
+// quantisation at width 4).  80 B = five 16-B loads per node step instead of
+// seven, and 20 VGPRs of node data in flight instead of 28.  A plane decodes
+// as t = q * (2^e * inv) + (origin - o) * inv: one v_fma_mix_f32 per plane;
+// the near / far halves of an axis are picked by the ray's direction sign
+// (x / y / z: lo of children 0..3 in dwords 0-1, hi in dwords 2-3).
+struct alignas(16) DNodeC {
+  float ox, oy, oz;  // origin: the lower corner of the union of the child boxes
+  uint32_t ex;       // per-axis scale exponents, signed bytes 0 (x), 1 (y), 2 (z)
+  uint4 x, y, z;     // 4 lo halves, then 4 hi halves, per axis
+  int4 ref;          // children (node indices or leaf cursors, as DNode.ref)
+};
+static_assert(sizeof(DNodeC) == 80, "DNodeC is five 16-B vectors");
+#ifndef PT_NODE_COMPRESS
+#define PT_NODE_COMPRESS 0
+#endif
+static_assert(!PT_NODE_COMPRESS || PT_NODE_WIDTH == 4, "the compressed node is 4-wide");
+
 // Binary node of the reference topology, 64 B: both child boxes + child
 // references (as DNode.ref).  Only traversed by the reference-count launch
 // (PT_FLAG_REF_COUNTS), whose node visits feed SURVEY.md §8(d)'s cost model.
@@ -264,6 +284,7 @@ struct KParams {
   const DNode* nodes;     // the render tree, PT_NODE_WIDTH 4
   const DNode8* nodes8;   // the render tree, PT_NODE_WIDTH 8
   const int4* nodes8_hi;  // its children 4..7's references
+  const DNodeC* nodesc;   // the render tree, PT_NODE_COMPRESS
   const DNode2* nodes2;  // the binary tree (reference-count launch only)
   const DPrim* prims;
   const float* norms;  // 9 floats per primitive (vertex normals n1,n2,n3)
@@ -348,6 +369,8 @@ struct WideOut {
   int max_stack;  // worst-case traversal stack
 };
 extern "C" hipError_t ptk_build_wide(const DNode2* bin, int n_bin, WideOut* out, hipStream_t s);
+// The compressed copy (DNodeC) of a 4-wide render tree, node for node.
+extern "C" hipError_t ptk_compress4(const DNode* in, int n, DNodeC* out, hipStream_t s);
 
 extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, bool ref_counts, hipStream_t s);
 extern "C" hipError_t ptk_launch_resolve(const KParams* P, hipStream_t s);

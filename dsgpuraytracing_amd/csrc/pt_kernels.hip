@@ -628,19 +628,80 @@ __device__ __forceinline__ bool node_step8(const DNode8* __restrict__ nodes, con
   return false;
 }
 
+// Compressed 4-wide node step (DNodeC, PT_NODE_COMPRESS): five 16-B loads
+// (header, x, y, z, references); the near / far halves of each axis picked by
+// the ray's direction sign (two v_cndmask per half-vector), one v_fma_mix_f32
+// per plane against the per-node scales a = 2^e * inv and offsets b =
+// (origin - o) * inv; then the same entry test, order and pushes as node_step.
+template <bool STATS, bool ROOT = false>
+__device__ __forceinline__ bool node_stepc(const DNodeC* __restrict__ nodes, const Stack& stk, Trav& tr,
+                                           Counters& ct, lds_cchar* root = nullptr) {
+  const float kRobust = PT_ROBUST;
+  const float3 o = tr.o, inv = tr.inv;
+  const float kMiss = 3.0e38f;
+  pt_v4i hd, X, Y, Z, rv;
+  if constexpr (ROOT) {
+    typedef __attribute__((address_space(3))) const pt_v4i lds_v4i;
+    hd = *(lds_v4i*)root;
+    X = *(lds_v4i*)(root + 16u);
+    Y = *(lds_v4i*)(root + 32u);
+    Z = *(lds_v4i*)(root + 48u);
+    rv = *(lds_v4i*)(root + 64u);
+  } else {
+    // (node index * 80 as one full-rate 24-bit multiply: pt_upload_scene
+    // keeps compressed trees below 2^24 nodes; the five loads share one
+    // address register and immediate offsets)
+    const pt_v4i* np = (const pt_v4i*)((const char*)nodes + __umul24((uint32_t)tr.node, 80u));
+    hd = np[0];
+    X = np[1];
+    Y = np[2];
+    Z = np[3];
+    rv = np[4];
+    asm volatile("" : "+v"(Z), "+v"(rv));
+  }
+  if (STATS) ct.nodes++;
+  const uint32_t ew = (uint32_t)hd.w;
+  const float ax = __builtin_amdgcn_ldexpf(inv.x, (int)(int8_t)(ew & 0xffu));
+  const float ay = __builtin_amdgcn_ldexpf(inv.y, (int)(int8_t)((ew >> 8) & 0xffu));
+  const float az = __builtin_amdgcn_ldexpf(inv.z, (int)(int8_t)((ew >> 16) & 0xffu));
+  const float bx = (__int_as_float(hd.x) - o.x) * inv.x;
+  const float by = (__int_as_float(hd.y) - o.y) * inv.y;
+  const float bz = (__int_as_float(hd.z) - o.z) * inv.z;
+  // near planes: lo for a positive direction component, hi for a negative one
+  const bool sx = inv.x < 0.0f, sy = inv.y < 0.0f, sz = inv.z < 0.0f;
+  typedef _Float16 pt_h4 __attribute__((ext_vector_type(4)));
+  typedef int pt_v2i __attribute__((ext_vector_type(2)));
+  const pt_h4 NX = __builtin_bit_cast(pt_h4, sx ? X.zw : X.xy), FX = __builtin_bit_cast(pt_h4, sx ? X.xy : X.zw);
+  const pt_h4 NY = __builtin_bit_cast(pt_h4, sy ? Y.zw : Y.xy), FY = __builtin_bit_cast(pt_h4, sy ? Y.xy : Y.zw);
+  const pt_h4 NZ = __builtin_bit_cast(pt_h4, sz ? Z.zw : Z.xy), FZ = __builtin_bit_cast(pt_h4, sz ? Z.xy : Z.zw);
+  float d[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float tn = fmaxf(fmaxf(fmaf((float)NX[k], ax, bx), fmaf((float)NY[k], ay, by)),
+                           fmaxf(fmaf((float)NZ[k], az, bz), 0.0f));
+    const float tf = fminf(fminf(fmaf((float)FX[k], ax, bx), fmaf((float)FY[k], ay, by)),
+                           fminf(fmaf((float)FZ[k], az, bz), tr.tmax)) * kRobust;
+    d[k] = tn <= tf ? tn : kMiss;
+  }
+  return node_order(stk, tr, d, make_int4(rv.x, rv.y, rv.z, rv.w));
+}
+
 // The render tree's node step: 8-wide (DNode8 + nodes_hi) or 4-wide (DNode).
 template <bool STATS, bool ROOT = false>
 __device__ __forceinline__ bool node_stepw(const void* __restrict__ nodes, const int4* __restrict__ nodes_hi,
                                            const Stack& stk, Trav& tr, Counters& ct, lds_cchar* root = nullptr) {
 #if PT_NODE_WIDTH == 8
   return node_step8<STATS, ROOT>((const DNode8*)nodes, nodes_hi, stk, tr, ct, root);
+#elif PT_NODE_COMPRESS
+  (void)nodes_hi;
+  return node_stepc<STATS, ROOT>((const DNodeC*)nodes, stk, tr, ct, root);
 #else
   (void)nodes_hi;
   return node_step<STATS, ROOT>((const DNode*)nodes, stk, tr, ct, root);
 #endif
 }
 // bytes of the workgroup's LDS copy of the root (node + children 4..7's references)
-#define PT_ROOT_BYTES (PT_NODE_WIDTH == 8 ? 144 : 128)
+#define PT_ROOT_BYTES (PT_NODE_WIDTH == 8 ? 144 : PT_NODE_COMPRESS ? 80 : 128)
 
 // Binary node step over the reference topology (reference-count launch).
 template <bool STATS>
@@ -943,6 +1004,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
 #if PT_NODE_WIDTH == 8
     if (lane < 8) s_root[lane] = ((const int4*)P.nodes8)[lane];
     else if (lane == 8) s_root[8] = P.nodes8_hi[0];
+#elif PT_NODE_COMPRESS
+    if (lane < 5) s_root[lane] = ((const int4*)P.nodesc)[lane];
 #else
     if (lane < 8) s_root[lane] = ((const int4*)P.nodes)[lane];
 #endif
@@ -1598,6 +1661,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     // step's vector loads; profiles/r4/ab_layout.txt)
 #if PT_NODE_WIDTH == 8
     const void* t_nodes = P.nodes8;
+#elif PT_NODE_COMPRESS
+    const void* t_nodes = P.nodesc;
 #else
     const void* t_nodes = P.nodes;
 #endif
