@@ -279,7 +279,7 @@ int pt_create(int device, pt_ctx** out) {
     HIPCHK(hipStreamCreateWithFlags(&c->rstream[k], hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
     HIPCHK(hipEventRecord(c->ev_free[k], c->stream));
-    HIPCHK(c->counter[k].reserve(PT_QUEUE_WORDS * PT_QUEUE_HEADS));  // work-queue heads, one 128-B line each
+    HIPCHK(c->counter[k].reserve(PT_QUEUE_WORDS * (PT_QUEUE_HEADS + 1)));  // work-queue heads (+ the tail head), one 128-B line each
   }
   for (auto& tri : c->ev)
     for (auto& e : tri) HIPCHK(hipEventCreate(&e));
@@ -1090,7 +1090,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     HIPCHK(c->tiles[slot].reserve(tl.size()));
     HIPCHK(hipMemcpyAsync(c->tiles[slot].p, th.data(), th.size() * sizeof(int4), hipMemcpyHostToDevice, rs));
   }
-  HIPCHK(hipMemsetAsync(c->counter[slot].p, 0, PT_QUEUE_WORDS * PT_QUEUE_HEADS * sizeof(uint32_t), rs));
+  HIPCHK(hipMemsetAsync(c->counter[slot].p, 0, PT_QUEUE_WORDS * (PT_QUEUE_HEADS + 1) * sizeof(uint32_t), rs));
   if (stats) {
     unsigned long long init[PT_STATS_SLOTS] = {0};
     init[21] = init[23] = init[25] = ~0ull;  // atomicMin slots
@@ -1264,6 +1264,26 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   if ((stats || P.census) && (size_t)grid * PT_WAVE_TRACE + PT_STATS_SLOTS > c->stats.n)
     grid = (int)((c->stats.n - PT_STATS_SLOTS) / PT_WAVE_TRACE);
   grid = std::max(1, grid);
+  // Tail claims (PT_TAIL_CLAIMS): the frame's last PT_TAIL_SLOTS slots per
+  // resident lane are dealt 64 at a time from a second queue head, so that
+  // when the queue runs dry no wave still holds a whole claim's worth of
+  // slots the other waves could have taken.  tail_start is where the dynamic
+  // claims of P.chunk slots (after the statically dealt ones) cross into the
+  // tail; claims of 64 stay inside one block (64 * n_groups is a multiple
+  // of 64).  tail_start >= slots: no tail.
+  P.tail_start = (uint32_t)slots;
+#if PT_TAIL_CLAIMS
+  {
+    int tail_lanes = PT_TAIL_SLOTS;
+    if (const char* t = std::getenv("PT_TAIL_SLOTS")) tail_lanes = std::max(0, std::atoi(t));  // tuning knob (0: off)
+    const int64_t first = (int64_t)grid * P.chunk;  // statically dealt chunks
+    const int64_t tail = (int64_t)grid * 64 * tail_lanes;
+    if (tail > 0 && P.chunk > 64 && slots > first) {
+      const int64_t k = std::max<int64_t>(0, (slots - tail - first) / P.chunk);
+      P.tail_start = (uint32_t)std::min<int64_t>(slots, first + k * P.chunk);
+    }
+  }
+#endif
   if (P.census)  // (a build without -DPT_CENSUS=1 leaves the drain fields 0)
     HIPCHK(hipMemsetAsync(c->stats.p + PT_STATS_SLOTS, 0, (size_t)grid * PT_WAVE_TRACE * 8, rs));
   P.stack_spill = nullptr;

@@ -21,6 +21,12 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #ifndef PT_QUEUE_HEADS
 #define PT_QUEUE_HEADS 1  // queue heads, interleaved chunk by chunk (8, one per XCD: C5 +2%, C3 / C4 / framed C3 -0.5..-1%; off)
 #endif
+#ifndef PT_TAIL_CLAIMS
+#define PT_TAIL_CLAIMS 1
+#endif
+#ifndef PT_TAIL_SLOTS
+#define PT_TAIL_SLOTS 1  // tail slots per resident lane (runtime knob PT_TAIL_SLOTS)
+#endif
 #ifndef PT_GROUP_SPP
 #define PT_GROUP_SPP 4  // default samples per work slot (pt_api.cpp group_size; 8 or more: C3 -4%, C5 -10%)
 #endif
@@ -280,6 +286,7 @@ struct KParams {
   uint32_t grp_m, grp_sh;           // fastdiv by n_groups (pt_fastdiv)
   int sblocks;                      // every chunk lies in one block (64 * n_groups a multiple of chunk): scalar block loads
   int chunk;                        // slots per queue claim (PT_CHUNK or PT_CHUNK_MAX), a multiple of 64
+  uint32_t tail_start;              // slots from here on are claimed 64 at a time from the tail head (PT_TAIL_CLAIMS)
   const int* tile_block0;           // first block of each tile (n_tiles + 1 entries), for the resolve
   const DNode* nodes;     // the render tree, PT_NODE_WIDTH 4
   const DNode8* nodes8;   // the render tree, PT_NODE_WIDTH 8

@@ -780,10 +780,16 @@ __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const
     float ua, va, ta, ub, vb, tb;
     const float da = mt_terms(o, d, f3(a0.x, a0.y, a0.z), f3(a1.x, a1.y, a1.z), f3(a2.x, a2.y, a2.z), ua, va, ta);
     const float db = mt_terms(o, d, f3(b0.x, b0.y, b0.z), f3(b1.x, b1.y, b1.z), f3(b2.x, b2.y, b2.z), ub, vb, tb);
-    // (bitwise &: no short-circuit exec-mask blocks)
-    const bool ha = (da != 0.0f) & (ua >= 0.0f) & (va >= 0.0f) & (ua + va <= 1.0f) & (ta > 0.0f) & (ta < tr.tmax);
+    // (bitwise &: no short-circuit exec-mask blocks.)  Fewer compares, same
+    // predicate: with det == 0 the reciprocal is inf and u, v are +-inf or
+    // NaN, so u + v <= 1 and min(u, v) >= 0 cannot both hold -- the det test
+    // is implied; and min(u, v) >= 0 differs from u >= 0 && v >= 0 only for a
+    // NaN operand, where u + v <= 1 is false anyway.
+    (void)da;
+    (void)db;
+    const bool ha = (fminf(ua, va) >= 0.0f) & (ua + va <= 1.0f) & (ta > 0.0f) & (ta < tr.tmax);
     const float tm = ha ? ta : tr.tmax;
-    const bool hb = two & (db != 0.0f) & (ub >= 0.0f) & (vb >= 0.0f) & (ub + vb <= 1.0f) & (tb > 0.0f) & (tb < tm);
+    const bool hb = two & (fminf(ub, vb) >= 0.0f) & (ub + vb <= 1.0f) & (tb > 0.0f) & (tb < tm);
     tr.tmax = hb ? tb : tm;
     tr.prim = hb ? pb : ha ? pa : tr.prim;
     tr.found = tr.found || ha || hb;
@@ -1523,6 +1529,15 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
             // (the head counts the chunks after the statically dealt ones)
             nbase = __builtin_amdgcn_readfirstlane(__shfl(nbase, 0)) + (PT_STATIC_FIRST ? n_waves * csize : 0u);
+#if PT_TAIL_CLAIMS
+            if (nbase >= P.tail_start) {  // (wave-uniform) the frame's tail: 64-slot claims from the tail head
+              csize = 64u;
+              uint32_t r = 0;
+              if (lane == 0) r = atomicAdd(P.work_counter + PT_QUEUE_WORDS * PT_QUEUE_HEADS, 64u);
+              nbase = __builtin_amdgcn_readfirstlane(__shfl(r, 0)) + P.tail_start;
+              if (STATS) n_atomics += lane == 0;
+            }
+#endif
 #endif
             seen = nbase + csize;
             if (STATS) n_atomics += lane == 0;

@@ -204,13 +204,15 @@ def test_hip_deterministic_and_tile_assignment_independent():
 @pytest.mark.parametrize("scene,w,h", [("c1_default_128x128", 128, 128), ("c1env_64x64", 64, 64)])
 def test_hip_queue_claim_size_never_changes_values(monkeypatch, scene, w, h):
     """The queue's claim size (PT_CHUNK_SLOTS; 128, or 256 for launches with
-    many slots per lane) decides only which wave renders which slots: images
-    are bit-identical for every claim size, also with the launch split into
-    tile shards."""
+    many slots per lane) and the tail dealt in 64-slot claims (PT_TAIL_SLOTS
+    slots per resident lane; 64: the whole dynamic part of a small frame)
+    decide only which wave renders which slots: images are bit-identical for
+    every claim size, also with the launch split into tile shards."""
     ref, _ = gpu_render(scene, w, h, 16, seed=13)
     tiles = tile_fifo(w, h)
-    for c in ("64", "128", "256"):
+    for c, tail in (("64", "1"), ("128", "1"), ("256", "1"), ("128", "0"), ("256", "4"), ("128", "64")):
         monkeypatch.setenv("PT_CHUNK_SLOTS", c)
+        monkeypatch.setenv("PT_TAIL_SLOTS", tail)  # the tail dealt in 64-slot claims from a second head
         img, _ = gpu_render(scene, w, h, 16, seed=13)
         assert np.array_equal(img, ref), c
         parts = np.zeros_like(ref)
@@ -218,6 +220,27 @@ def test_hip_queue_claim_size_never_changes_values(monkeypatch, scene, w, h):
             p, _ = gpu_render(scene, w, h, 16, seed=13, tiles=tiles[shard::2])
             parts += p
         assert np.array_equal(parts, ref), c
+
+
+@pytest.mark.parametrize("scene,w,h,spp", [("c1_default_128x128", 128, 128, 16), ("c1env_64x64", 64, 64, 32)])
+def test_hip_tail_claims_never_change_values(monkeypatch, scene, w, h, spp):
+    """With one resident wave per CU the frame's slots outrun the statically
+    dealt chunks, so dynamic claims and the tail head (PT_TAIL_SLOTS) both
+    run: bit-identical images with the tail off, one or four tail slots per
+    lane, and at the full grid (the sample-group size pinned, since it
+    follows the resident grid)."""
+    monkeypatch.setenv("PT_SAMPLE_GROUP", "2")
+    ref, _ = gpu_render(scene, w, h, spp, seed=29)
+    monkeypatch.setenv("PT_WAVES_PER_CU", "1")
+    for tail in ("0", "1", "4"):
+        monkeypatch.setenv("PT_TAIL_SLOTS", tail)
+        img, st = gpu_render(scene, w, h, spp, seed=29, stats=True)
+        assert np.array_equal(img, ref), tail
+        parts = np.zeros_like(ref)
+        for shard, tl in enumerate((tile_fifo(w, h)[0::2], tile_fifo(w, h)[1::2])):
+            p, _ = gpu_render(scene, w, h, spp, seed=29, tiles=tl)
+            parts += p
+        assert np.array_equal(parts, ref), tail
 
 
 @pytest.mark.parametrize("scene,w,h", [("c1_default_128x128", 128, 128), ("c1_sphcam_96x64", 96, 64),
