@@ -1872,6 +1872,9 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
 #undef P
 #endif
 
+#ifndef PT_RESOLVE_WIDE
+#define PT_RESOLVE_WIDE 1
+#endif
 #if !PT_ENV_TU  // (pt_kernels_env.hip emits only the ENV render kernels)
 // Sums each pixel's sample groups in group order, so the sum is a fixed
 // function of the pixel, independent of scheduling and of the tile -> GPU
@@ -1901,8 +1904,38 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
     if (qx >= b.z || qy >= b.w) continue;
     float3 acc = f3(0, 0, 0);
     const float* pa = P.partial + PT_SUM_WORDS * ((size_t)k * 64u + (size_t)q) * (size_t)P.n_groups;
+#if PT_RESOLVE_WIDE && PT_SUM_WORDS == 3
+    if ((P.n_groups & 3) == 0) {
+      // The pixel's run of n_groups 12-B sums (16-B aligned: 48 B per four
+      // groups) read as 16-B vectors, eight groups (six loads) in flight per
+      // step: a wave's 64 runs lie 12 * n_groups B apart, and with one 12-B
+      // load per group every load instruction touched 64 lines that the L1
+      // had evicted again before the next group's load came.  Same summation
+      // order (group 0, 1, 2, ...).
+      const float4* pv = (const float4*)pa;
+      int j = 0;
+      for (; j + 8 <= P.n_groups; j += 8, pv += 6) {
+        float4 v[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) v[i] = pv[i];
+        const float* f = &v[0].x;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) acc = acc + f3(f[3 * g], f[3 * g + 1], f[3 * g + 2]);
+      }
+      if (j < P.n_groups) {  // a last four groups
+        float4 v[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) v[i] = pv[i];
+        const float* f = &v[0].x;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc = acc + f3(f[3 * g], f[3 * g + 1], f[3 * g + 2]);
+      }
+    } else
+#endif
+    {
 #pragma unroll 2
-    for (int j = 0; j < P.n_groups; ++j) acc = acc + ld3(pa + PT_SUM_WORDS * (size_t)j);
+      for (int j = 0; j < P.n_groups; ++j) acc = acc + ld3(pa + PT_SUM_WORDS * (size_t)j);
+    }
     store3(out_at(b.x + qx, b.y + qy), acc * inv_spp);
   }
 }
