@@ -949,6 +949,14 @@ enum : int { SH_RESUME = 1, SH_FOLLOW = 2, SH_STORE = 3, SH_STORE_FOLLOW = 4 };
 // VALU instructions per traversal iteration (PT_PROBE_TRAV_*) or per shading
 // round (PT_PROBE_SHADE_*), to price one more instruction of each kind in each
 // phase (tools/ab.sh against the plain build).
+// Wave priorities of the two phases (s_setprio; shading raised: round 3,
+// profiles/r3/ab_build_options.txt)
+#ifndef PT_PRIO_SHADE
+#define PT_PRIO_SHADE 2
+#endif
+#ifndef PT_PRIO_TRAV
+#define PT_PRIO_TRAV 0
+#endif
 #ifndef PT_PROBE_TRAV_SALU
 #define PT_PROBE_TRAV_SALU 0
 #endif
@@ -1216,7 +1224,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
 #endif
     // the shading round issues at raised wave priority, traversal at the
     // base one (C4 +0.6%, C5 +0.4%, C3 within noise: profiles/r3/ab_build_options.txt)
-    __builtin_amdgcn_s_setprio(2);
+    __builtin_amdgcn_s_setprio(PT_PRIO_SHADE);
     probe_insts<PT_PROBE_SHADE_SALU, PT_PROBE_SHADE_VALU>();
     // ================= shading phase: lanes whose ray finished =================
     if (mode == M_SHADE) {
@@ -1665,7 +1673,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       if (__ballot(mode == M_FETCH) == 0ull) break;
     }
     // ================= traversal phase =================
-    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(PT_PRIO_TRAV);
     // Step every in-flight ray one node at a time; leave as soon as `batch`
     // lanes have finished their ray, so finished lanes are refilled together
     // (coherent shading) while the others keep their traversal state.
@@ -1907,22 +1915,17 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
 #if PT_RESOLVE_WIDE && PT_SUM_WORDS == 3
     if ((P.n_groups & 3) == 0) {
       // The pixel's run of n_groups 12-B sums (16-B aligned: 48 B per four
-      // groups) read as 16-B vectors, eight groups (six loads) in flight per
-      // step: a wave's 64 runs lie 12 * n_groups B apart, and with one 12-B
-      // load per group every load instruction touched 64 lines that the L1
-      // had evicted again before the next group's load came.  Same summation
-      // order (group 0, 1, 2, ...).
+      // groups) read as 16-B vectors, four groups (three loads) per step: a
+      // wave's 64 runs lie 12 * n_groups B apart, and with one 12-B load per
+      // group every load instruction touched 64 lines that the L1 had evicted
+      // again before the next group's load came (lone resolve C3 0.047 ->
+      // 0.033 ms, C4 0.36 -> 0.23 ms).  Same summation order (group 0, 1,
+      // 2, ...).  At most 24 VGPRs: the resolve runs beside the next frame's
+      // render waves (5 per SIMD at <= 96 VGPRs leave 32 per SIMD); with 40
+      // it waited for them (pipelined C3 -5%: profiles/r5/ab_resolve_wide.txt).
       const float4* pv = (const float4*)pa;
-      int j = 0;
-      for (; j + 8 <= P.n_groups; j += 8, pv += 6) {
-        float4 v[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) v[i] = pv[i];
-        const float* f = &v[0].x;
-#pragma unroll
-        for (int g = 0; g < 8; ++g) acc = acc + f3(f[3 * g], f[3 * g + 1], f[3 * g + 2]);
-      }
-      if (j < P.n_groups) {  // a last four groups
+#pragma unroll 1
+      for (int j = 0; j < P.n_groups; j += 4, pv += 3) {
         float4 v[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i) v[i] = pv[i];
