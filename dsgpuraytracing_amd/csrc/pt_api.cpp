@@ -490,10 +490,93 @@ static int build_host_bvh(const pt_scene* s, std::vector<DNode>& dn, std::vector
       const int r = b2[i].ref[s2];
       under[i] += r >= 0 ? under[(size_t)r] : (double)(((~r) & 7) + 1);
     }
-  // which internal child to open next: PT_COLLAPSE=area (default: the largest
-  // surface area), count (the most primitives), sah (area x primitives)
+  // The collapse: PT_COLLAPSE=dp (default: the SAH-optimal choice of the
+  // binary nodes kept as BVH4 nodes, the DP of lbvh.hip's k_dp over this
+  // tree), or greedy -- open the internal child with the largest surface area
+  // (area), the most primitives (count) or area x primitives (sah) until four.
   const char* cm = std::getenv("PT_COLLAPSE");
-  const int crit = !cm ? 0 : std::strcmp(cm, "count") == 0 ? 1 : std::strcmp(cm, "sah") == 0 ? 2 : 0;
+  const int crit = !cm || std::strcmp(cm, "dp") == 0 ? 3
+                   : std::strcmp(cm, "count") == 0   ? 1
+                   : std::strcmp(cm, "sah") == 0     ? 2
+                                                     : 0;
+  // DP tables (crit 3): dpc[4n + i-1] = least expected steps of binary node
+  // n's subtree in <= i slots (a node or a two-primitive leaf step costs one,
+  // weighted by area); dpk = slots for its left child, -1 = as with i - 1
+  std::vector<double> dpc;
+  std::vector<int8_t> dpk;
+  if (crit == 3) {
+    dpc.assign(b2.size() * 4, 0.0);
+    dpk.assign(b2.size() * 4, 0);
+    auto box_area = [](const float lo[3], const float hi[3]) {
+      const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+      return dx * dy + dy * dz + dz * dx;
+    };
+    for (size_t n = b2.size(); n-- > 0;) {  // (pre-order: children after parents)
+      double a[2][5];
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int r = b2[n].ref[s2];
+        for (int i = 1; i <= 4; ++i)
+          a[s2][i] = r >= 0 ? dpc[(size_t)r * 4 + (i - 1)]
+                            : box_area(b2[n].lo[s2], b2[n].hi[s2]) * (double)((((~r) & 7) + 2) / 2);
+      }
+      double dist[5];
+      int8_t arg[5];
+      for (int j = 2; j <= 4; ++j) {
+        dist[j] = INFINITY;
+        arg[j] = 1;
+        for (int k = 1; k < j; ++k)
+          if (a[0][k] + a[1][j - k] < dist[j]) {
+            dist[j] = a[0][k] + a[1][j - k];
+            arg[j] = (int8_t)k;
+          }
+      }
+      float ulo[3], uhi[3];
+      for (int k = 0; k < 3; ++k) {
+        ulo[k] = std::min(b2[n].lo[0][k], b2[n].lo[1][k]);
+        uhi[k] = std::max(b2[n].hi[0][k], b2[n].hi[1][k]);
+      }
+      double prev = box_area(ulo, uhi) + dist[4];
+      dpc[n * 4] = prev;
+      dpk[n * 4] = arg[4];
+      for (int i = 2; i <= 4; ++i) {
+        const bool open = dist[i] < prev;
+        prev = open ? dist[i] : prev;
+        dpc[n * 4 + (i - 1)] = prev;
+        dpk[n * 4 + (i - 1)] = open ? arg[i] : (int8_t)-1;
+      }
+    }
+  }
+  // the DP's children of binary node b kept whole: its two children over four
+  // slots, each opened as its table says, in left-to-right order
+  auto dp_kids = [&](int b, Child out[4]) -> int {
+    int sp = 0, n = 0, sb[8], ss[8], si[8];
+    const int k4 = dpk[(size_t)b * 4];
+    sb[sp] = b; ss[sp] = 1; si[sp++] = 4 - k4;
+    sb[sp] = b; ss[sp] = 0; si[sp++] = k4;
+    while (sp > 0) {
+      --sp;
+      const int pb = sb[sp], side = ss[sp];
+      int i = si[sp];
+      const int r = b2[(size_t)pb].ref[side];
+      if (r >= 0) {
+        while (i > 1 && dpk[(size_t)r * 4 + (i - 1)] == -1) --i;
+        if (i > 1) {
+          const int k = dpk[(size_t)r * 4 + (i - 1)];
+          sb[sp] = r; ss[sp] = 1; si[sp++] = i - k;
+          sb[sp] = r; ss[sp] = 0; si[sp++] = k;
+          continue;
+        }
+      }
+      Child c;
+      for (int k = 0; k < 3; ++k) {
+        c.lo[k] = b2[(size_t)pb].lo[side][k];
+        c.hi[k] = b2[(size_t)pb].hi[side][k];
+      }
+      c.ref = r;
+      out[n++] = c;
+    }
+    return n;
+  };
   auto weight = [&](const Child& c) {
     const double n = c.ref >= 0 ? under[(size_t)c.ref] : 0.0;
     return crit == 0 ? (double)area(c) : crit == 1 ? n : (double)area(c) * n;
@@ -507,6 +590,9 @@ static int build_host_bvh(const pt_scene* s, std::vector<DNode>& dn, std::vector
       st.pop_back();
       Child ch[4];
       int n = 2;
+      if (crit == 3) {
+        n = dp_kids(it.b2node, ch);
+      } else {
       kids(it.b2node, ch);
       while (n < 4) {
         int best = -1;
@@ -521,6 +607,7 @@ static int build_host_bvh(const pt_scene* s, std::vector<DNode>& dn, std::vector
         kids(ch[best].ref, two);
         ch[best] = two[0];
         ch[n++] = two[1];
+      }
       }
       int64_t me = (int64_t)dn.size();
       dn.push_back(DNode{});

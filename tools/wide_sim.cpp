@@ -192,6 +192,97 @@ static int emit(Tree& t, int64_t b) {
   return me;
 }
 
+// SAH-optimal collapse of the binary tree into a 4-wide tree (dynamic
+// programming over (binary node, slots), after Ylitie et al. 2017 at width 4):
+// cost(n, i) = the least expected steps of n's subtree when it fills at most
+// i slots of its parent; a node step and a leaf step of two primitives cost
+// one each, weighted by surface area.
+static std::vector<double> dpc;   // [n * 5 + i]
+static std::vector<int8_t> dpk;   // split of best_dist(n, i): slots for the left child; 0 = n kept whole
+static double sa(int64_t b) {
+  double dx = B[b].bb_max[0] - B[b].bb_min[0], dy = B[b].bb_max[1] - B[b].bb_min[1], dz = B[b].bb_max[2] - B[b].bb_min[2];
+  return dx * dy + dy * dz + dz * dx;
+}
+static double g_cn = 1.0, g_cl = 1.0;
+static void dp_solve(int64_t b) {
+  if (is_leaf(b)) {
+    for (int i = 1; i <= 4; ++i) {
+      dpc[b * 5 + i] = sa(b) * g_cl * ((B[b].range + 1) / 2);
+      dpk[b * 5 + i] = 0;
+    }
+    return;
+  }
+  const int64_t L = B[b].left, R = B[b].right;
+  dp_solve(L);
+  dp_solve(R);
+  auto dist = [&](int j, int& bk) {
+    double best = 1e300;
+    bk = 1;
+    for (int k = 1; k < j; ++k) {
+      double c = dpc[L * 5 + k] + dpc[R * 5 + (j - k)];
+      if (c < best) {
+        best = c;
+        bk = k;
+      }
+    }
+    return best;
+  };
+  int k4;
+  const double node = sa(b) * g_cn + dist(4, k4);
+  dpc[b * 5 + 1] = node;
+  dpk[b * 5 + 1] = 0;
+  for (int i = 2; i <= 4; ++i) {
+    int k;
+    const double d = dist(i, k);
+    if (d < dpc[b * 5 + i - 1]) {
+      dpc[b * 5 + i] = d;
+      dpk[b * 5 + i] = (int8_t)k;
+    } else {
+      dpc[b * 5 + i] = dpc[b * 5 + i - 1];
+      dpk[b * 5 + i] = -1;  // as with i - 1 slots
+    }
+  }
+}
+// the subtrees that fill (at most) i slots for binary node b
+static void dp_collect(int64_t b, int i, std::vector<int64_t>& out) {
+  while (i > 1 && dpk[b * 5 + i] == -1) --i;
+  if (i == 1 || is_leaf(b)) {
+    out.push_back(b);
+    return;
+  }
+  const int k = dpk[b * 5 + i];
+  dp_collect(B[b].left, k, out);
+  dp_collect(B[b].right, i - k, out);
+}
+static int emit_dp(Tree& t, int64_t b) {
+  // b is an internal node kept whole: its children distributed over 4 slots
+  std::vector<int64_t> kids;
+  int k4 = 1;
+  {
+    double best = 1e300;
+    for (int k = 1; k < 4; ++k) {
+      double c = dpc[B[b].left * 5 + k] + dpc[B[b].right * 5 + (4 - k)];
+      if (c < best) {
+        best = c;
+        k4 = k;
+      }
+    }
+  }
+  dp_collect(B[b].left, k4, kids);
+  dp_collect(B[b].right, 4 - k4, kids);
+  std::vector<Child> ch;
+  for (int64_t x : kids) ch.push_back(child_of(t, x));
+  int me = (int)t.nodes.size();
+  t.nodes.push_back(WNode{});
+  t.nodes[me].n = (int)ch.size();
+  for (size_t k = 0; k < ch.size(); ++k) {
+    if (ch[k].ref >= 0) ch[k].ref = emit_dp(t, ch[k].ref);
+    t.nodes[me].c[k] = ch[k];
+  }
+  for (int o = 0; o < 8; ++o) t.nodes[me].slot_of_octant[o] = o < t.nodes[me].n ? o : -1;
+  return me;
+}
+
 struct Ray {
   V3 o, d;
   double tmax;
@@ -372,6 +463,15 @@ int main(int argc, char** argv) {
   emit(t2, 0);
   emit(t8s, 0);
   emit(t4s, 0);
+  Tree t4d;
+  t4d.W = 4;
+  dpc.assign(B.size() * 5, 0.0);
+  dpk.assign(B.size() * 5, 0);
+  if (const char* c = std::getenv("WS_CN")) g_cn = std::atof(c);
+  dp_solve(0);
+  emit_dp(t4d, 0);
+  std::printf("BVH4 greedy nodes %zu, BVH4 dp nodes %zu (dp expected steps %.4f per root area)\n", t4.nodes.size(),
+              t4d.nodes.size(), dpc[0 * 5 + 1] / sa(0));
   auto fill = [](const Tree& t) { double c = 0; for (auto& n : t.nodes) c += n.n; return c / t.nodes.size(); };
   std::printf("children per node: BVH4 %.2f, BVH8 %.2f, BVH8 split %.2f, BVH4 split %.2f\n", fill(t4), fill(t8), fill(t8s), fill(t4s));
   std::printf("prims %lld, binary nodes %lld, BVH4 nodes %zu, BVH8 nodes %zu, leaves %zu\n", (long long)sc.n_prims,
@@ -439,7 +539,7 @@ int main(int argc, char** argv) {
   } layouts[] = {{"BVH2", &t2, SORT},        {"BVH4 sort", &t4, SORT},       {"BVH8 sort", &t8, SORT},
                  {"BVH8 octant", &t8, OCT},  {"BVH8 near+slot", &t8, NEAR_SLOT}, {"BVH8 near+oct", &t8, NEAR_OCT},
                  {"BVH8 fp16 sort", &t8q, SORT}, {"BVH8 fp16 n+slot", &t8q, NEAR_SLOT},
-                 {"BVH4 near+slot", &t4, NEAR_SLOT}};
+                 {"BVH4 near+slot", &t4, NEAR_SLOT}, {"BVH4 dp sort", &t4d, SORT}};
   for (int s = 0; s < 3; ++s) {
     std::printf("-- %s rays (%zu)\n", names[s], sets[s]->size());
     for (const L& l : layouts) {
