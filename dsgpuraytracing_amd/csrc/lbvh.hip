@@ -990,10 +990,14 @@ extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t
       hipLaunchKernelGGL(k_treelet, dim3(gt), dim3(64), 0, s, P, passes > 0 ? 1 : 0);
       LB_CHK(hipGetLastError());
     }
-    // the BVH4 collapse: SAH-optimal DP (default, PT_COLLAPSE=dp) or greedy
-    // (any other PT_COLLAPSE: open the largest-area child until four)
+    // the BVH4 collapse: greedy (default: open the largest-area child until
+    // four) or the SAH-optimal DP (PT_COLLAPSE=dp).  Over this tree the DP
+    // changes little -- C3 traversal steps -0.6%, throughput +-0.2%, C4
+    // +0.7%, C5 / c5big -1.5% (profiles/r5/ab_collapse_dp.txt): the treelet
+    // passes already leave a tree whose greedy collapse is near the SAH
+    // optimum; over the host SAH tree it pays (+10%, pt_api.cpp).
     const char* ce = std::getenv("PT_COLLAPSE");
-    if (!ce || std::strcmp(ce, "dp") == 0) {
+    if (ce && std::strcmp(ce, "dp") == 0) {
       LB_CHK(hipMalloc(&dpc, ni * 4 * sizeof(float)));
       LB_CHK(hipMalloc(&dpk, ni * 4));
       P.dpc = dpc;

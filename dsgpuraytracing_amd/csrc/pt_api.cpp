@@ -490,10 +490,12 @@ static int build_host_bvh(const pt_scene* s, std::vector<DNode>& dn, std::vector
       const int r = b2[i].ref[s2];
       under[i] += r >= 0 ? under[(size_t)r] : (double)(((~r) & 7) + 1);
     }
-  // The collapse: PT_COLLAPSE=dp (default: the SAH-optimal choice of the
-  // binary nodes kept as BVH4 nodes, the DP of lbvh.hip's k_dp over this
-  // tree), or greedy -- open the internal child with the largest surface area
-  // (area), the most primitives (count) or area x primitives (sah) until four.
+  // The collapse: PT_COLLAPSE=dp (default for the host trees: the SAH-optimal
+  // choice of the binary nodes kept as BVH4 nodes, the DP of lbvh.hip's k_dp;
+  // C3 over the host SAH tree 46.2 -> 51.0 G samples/s, +10%:
+  // profiles/r5/ab_collapse_dp.txt), or greedy -- open the internal child with
+  // the largest surface area (area), the most primitives (count) or area x
+  // primitives (sah) until four.
   const char* cm = std::getenv("PT_COLLAPSE");
   const int crit = !cm || std::strcmp(cm, "dp") == 0 ? 3
                    : std::strcmp(cm, "count") == 0   ? 1
