@@ -1119,11 +1119,14 @@ static int64_t traced_px(const pt_ctx* c, int W, int H) {
 
 // Sample groups of a pixel (KParams: n_groups groups of group_spp samples,
 // the last one possibly short).  The grouping decides the float summation
-// order of a pixel, so it is a function of the FRAME -- its size, spp, the
-// pixels its camera rays can reach, the environment light -- and the
-// device's resident grid only, never of the launch's tile set or of a stats
-// build: any split of a frame into tile launches (raytrace_tile calls, the
-// multi-GPU shards) sums every pixel in the same order as the whole frame.
+// order of a pixel, so it is a function of the FRAME only -- its size, spp,
+// the pixels its camera rays can reach, the environment light -- never of
+// the launch's tile set, of a stats build or of the device: any split of a
+// frame into tile launches (raytrace_tile calls, the multi-GPU shards) and
+// any device (a CPX partition, fewer resident waves) sums every pixel in the
+// same order.  The slots-per-lane rule below counts the lanes of a whole
+// MI355X at the default occupancy (PT_GROUP_REF_LANES: 256 CUs x 20 waves x
+// 64), not the running device's.
 //  * group_spp: 4 (C4 +4%, framed C3 +2% over 2), 2 with an environment
 //    light (C5 +2.3%, c5big +2.1%), halved until the traced samples make >= 24
 //    work slots per resident lane: C3's footprint-culled frame gets 2 (+1.5%
@@ -1323,7 +1326,8 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   const int64_t want_plain = std::getenv("PT_WAVES_PER_CU") ? want : c->grid_plain;
   const int64_t frame_blocks = (int64_t)((P.W + 7) / 8) * ((P.H + 7) / 8);
   const int64_t budget_waves = std::max({want, want_plain, (int64_t)c->grid_stats});
-  P.group_spp = group_size(traced_px(c, P.W, P.H), c->env_w > 0, P.spp, want_plain * PT_BLOCK, frame_blocks, budget_waves);
+  P.group_spp = group_size(traced_px(c, P.W, P.H), c->env_w > 0, P.spp, (int64_t)PT_GROUP_REF_LANES, frame_blocks,
+                           budget_waves);
   P.n_groups = (P.spp + P.group_spp - 1) / P.group_spp;
   const int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
   // (slot indices reach past the end by up to a static chunk plus a claimed one per wave)

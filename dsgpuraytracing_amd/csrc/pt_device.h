@@ -33,6 +33,9 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #ifndef PT_GROUP_SPP_ENV
 #define PT_GROUP_SPP_ENV 2  // with an environment light
 #endif
+#ifndef PT_GROUP_REF_LANES
+#define PT_GROUP_REF_LANES (256 * 20 * 64)  // the group-size rule's lanes: a whole MI355X at 20 waves per CU (device-independent)
+#endif
 #ifndef PT_GROUP_MIN_SLOTS
 #define PT_GROUP_MIN_SLOTS 24  // groups are halved until the traced samples make this many slots per lane
 #endif
