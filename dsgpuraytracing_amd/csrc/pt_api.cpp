@@ -208,6 +208,9 @@ struct pt_ctx {
   DevBuf<float> partial[kSlots];   // per-slot sample-group sums
   DevBuf<int> spill[kSlots];       // traversal stack entries beyond PT_STACK
   DevBuf<uint32_t> counter[kSlots];
+  // the slot's queue heads are known to be zero: the last resolve of the slot
+  // reset them (PT_RESOLVE_RESETS), so the next launch needs no memset
+  bool counter_clean[kSlots] = {};
   int64_t culled_px = 0;         // pixels of the last launch outside the footprint
   DevBuf<float> frame;  // device framebuffer for host-output renders
   // Asynchronous one-tile seam (pt_tile_submit / pt_tile_finish): submitted
@@ -1182,7 +1185,13 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     HIPCHK(c->tiles[slot].reserve(tl.size()));
     HIPCHK(hipMemcpyAsync(c->tiles[slot].p, th.data(), th.size() * sizeof(int4), hipMemcpyHostToDevice, rs));
   }
-  HIPCHK(hipMemsetAsync(c->counter[slot].p, 0, PT_QUEUE_WORDS * (PT_QUEUE_HEADS + 1) * sizeof(uint32_t), rs));
+  // Queue heads: zeroed by the slot's previous resolve (PT_RESOLVE_RESETS: a
+  // memset in front of the render is a dependent launch of its own, ~20 us
+  // before the render kernel starts on a lone frame); a memset only when
+  // that did not happen (first use, a launch that failed half-way)
+  if (!c->counter_clean[slot])
+    HIPCHK(hipMemsetAsync(c->counter[slot].p, 0, PT_QUEUE_WORDS * (PT_QUEUE_HEADS + 1) * sizeof(uint32_t), rs));
+  c->counter_clean[slot] = false;
   if (stats) {
     unsigned long long init[PT_STATS_SLOTS] = {0};
     init[21] = init[23] = init[25] = ~0ull;  // atomicMin slots
@@ -1396,6 +1405,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   HIPCHK(hipEventRecord(c->ev1, rs));
   if (rs != s) HIPCHK(hipStreamWaitEvent(s, c->ev1, 0));  // the resolve reads the finished group sums
   HIPCHK(ptk_launch_resolve(&P, s));
+  c->counter_clean[slot] = PT_RESOLVE_RESETS != 0;
   HIPCHK(hipEventRecord(c->ev2, s));
   HIPCHK(hipEventRecord(c->ev_free[slot], s));
   c->census_valid = P.census != 0;

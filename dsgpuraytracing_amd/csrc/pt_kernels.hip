@@ -1895,6 +1895,11 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
   const int ti = (int)blockIdx.x;
   const int4 tile = P.tiles[ti];
   const int tid = (int)threadIdx.x;
+#if PT_RESOLVE_RESETS
+  // the render that wrote these sums is complete, so are its queue claims:
+  // zero the heads for the render slot's next launch (pt_api.cpp launch)
+  if (ti == 0 && tid < PT_QUEUE_WORDS * (PT_QUEUE_HEADS + 1)) P.work_counter[tid] = 0u;
+#endif
   auto out_at = [&](int x, int y) -> float* {
     const size_t o = P.packed ? (size_t)ti * 1024u + (size_t)(y - tile.y) * 32u + (size_t)(x - tile.x)
                               : (size_t)x + (size_t)y * (size_t)P.W;
