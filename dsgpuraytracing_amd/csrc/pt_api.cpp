@@ -163,6 +163,7 @@ struct pt_ctx {
   // triples so device renders need not synchronise (pt_get_launch_times)
   static constexpr int kRing = 256;
   hipEvent_t ev[kRing][3] = {};
+  hipEvent_t ev_call[kRing] = {};  // (PT_RESOLVE_ON_RS) the caller's stream at the launch's start
   int64_t n_launches = 0;   // launches recorded so far (ring slot = index % kRing)
   bool census_valid = false;  // the last launch was a PT_CENSUS plain launch (its trace area holds start/end/CU)
   bool times_pending = false;  // c->last's times belong to a launch not yet synchronised
@@ -286,6 +287,7 @@ int pt_create(int device, pt_ctx** out) {
   }
   for (auto& tri : c->ev)
     for (auto& e : tri) HIPCHK(hipEventCreate(&e));
+  for (auto& e : c->ev_call) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIPCHK(c->stats.reserve(PT_STATS_SLOTS));
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, device));
@@ -350,6 +352,8 @@ int pt_destroy(pt_ctx* c) {
   for (auto& tri : c->ev)
     for (auto& e : tri)
       if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->ev_call)
+    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return PT_OK;
@@ -1163,7 +1167,8 @@ static int group_size(int64_t traced, bool env, int spp, int64_t lanes, int64_t 
 }
 
 // One render: the render kernel on the slot's render stream, then the resolve
-// on the caller's stream `s` (see pt_ctx: the render pipeline).
+// (on the same stream, PT_RESOLVE_ON_RS; else on the caller's stream `s`),
+// the caller's stream `s` ordered after it (see pt_ctx: the render pipeline).
 static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStream_t s, uint32_t flags) {
   const bool stats = (flags & (PT_FLAG_STATS | PT_FLAG_REF_COUNTS)) != 0;
   std::memset(&c->last, 0, sizeof(c->last));
@@ -1400,6 +1405,26 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     c->ev2 = tri[2];
     ++c->n_launches;
   }
+#if PT_RESOLVE_ON_RS
+  // The resolve follows the render on the render stream (a same-queue
+  // dependency: ~6 us from the render's end to the resolve's start on a lone
+  // frame, against ~13 us through a cross-stream event), ordered after the
+  // caller's earlier work on `s` (it writes the caller's buffer) by an event
+  // recorded there now -- long complete when the render ends -- and the
+  // caller's stream then waits for the resolve: everything the caller can
+  // observe on `s` keeps its order.
+  hipEvent_t ev_call = c->ev_call[(c->n_launches - 1) % pt_ctx::kRing];
+  if (rs != s) HIPCHK(hipEventRecord(ev_call, s));
+  HIPCHK(hipEventRecord(c->ev0, rs));
+  HIPCHK(ptk_launch_render(&P, grid, stats, (flags & PT_FLAG_REF_COUNTS) != 0, rs));
+  HIPCHK(hipEventRecord(c->ev1, rs));
+  if (rs != s) HIPCHK(hipStreamWaitEvent(rs, ev_call, 0));
+  HIPCHK(ptk_launch_resolve(&P, rs));
+  c->counter_clean[slot] = PT_RESOLVE_RESETS != 0;
+  HIPCHK(hipEventRecord(c->ev2, rs));
+  HIPCHK(hipEventRecord(c->ev_free[slot], rs));
+  if (rs != s) HIPCHK(hipStreamWaitEvent(s, c->ev2, 0));
+#else
   HIPCHK(hipEventRecord(c->ev0, rs));
   HIPCHK(ptk_launch_render(&P, grid, stats, (flags & PT_FLAG_REF_COUNTS) != 0, rs));
   HIPCHK(hipEventRecord(c->ev1, rs));
@@ -1408,6 +1433,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   c->counter_clean[slot] = PT_RESOLVE_RESETS != 0;
   HIPCHK(hipEventRecord(c->ev2, s));
   HIPCHK(hipEventRecord(c->ev_free[slot], s));
+#endif
   c->census_valid = P.census != 0;
   c->last.grid_blocks = grid;
   c->last.group_spp = P.group_spp;

@@ -21,6 +21,9 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #ifndef PT_QUEUE_HEADS
 #define PT_QUEUE_HEADS 1  // queue heads, interleaved chunk by chunk (8, one per XCD: C5 +2%, C3 / C4 / framed C3 -0.5..-1%; off)
 #endif
+#ifndef PT_RESOLVE_ON_RS
+#define PT_RESOLVE_ON_RS 1  // the resolve on the render slot's stream (pt_api.cpp launch)
+#endif
 #ifndef PT_RESOLVE_RESETS
 #define PT_RESOLVE_RESETS 1  // the resolve zeroes its launch's queue heads for the slot's next launch
 #endif
