@@ -22,7 +22,7 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #define PT_QUEUE_HEADS 1  // queue heads, interleaved chunk by chunk (8, one per XCD: C5 +2%, C3 / C4 / framed C3 -0.5..-1%; off)
 #endif
 #ifndef PT_RESOLVE_ON_RS
-#define PT_RESOLVE_ON_RS 1  // the resolve on the render slot's stream (pt_api.cpp launch)
+#define PT_RESOLVE_ON_RS 0  // 1: the resolve on the render slot's stream (one-frame wall +0.03 ms: profiles/r5/ab_resolve_reset_stream.txt)
 #endif
 #ifndef PT_RESOLVE_RESETS
 #define PT_RESOLVE_RESETS 1  // the resolve zeroes its launch's queue heads for the slot's next launch

@@ -252,6 +252,9 @@ int pt_render_tiles(pt_ctx* ctx, const pt_tile* tiles, int32_t n_tiles, float* h
  * (hipStream_t, NULL = the context's stream).  Returns after the kernel is
  * queued, without waiting for it (a PT_FLAG_STATS / PT_FLAG_REF_COUNTS call
  * waits, to read its counters); synchronise on the stream before reading.
+ * The framebuffer is written in `stream` order: after the work queued on
+ * `stream` before the call, before the work queued after it (the kernels
+ * themselves run on the context's render streams).
  * Replaces CUDAPathTracer::startRayTracingPT (cuda_src/setup.cu:147-179)
  * minus its host copy-back. */
 int pt_render_tiles_device(pt_ctx* ctx, const pt_tile* tiles, int32_t n_tiles, float* hdr_out_dev,
