@@ -514,14 +514,21 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
         # neighbouring frame): the wall-clock render time of ONE frame, and
         # the render kernel's own duration (HIP events around a launch that
         # shares the GPU with nothing)
-        lat = []
+        lat, api, idle = [], [], []
         for _ in range(5):
             torch.cuda.synchronize()
             t0s = time.perf_counter()
             step()
+            t1s = time.perf_counter()
             torch.cuda.synchronize()
             lat.append(time.perf_counter() - t0s)
+            api.append(t1s - t0s)
+            t2s = time.perf_counter()
+            torch.cuda.synchronize()  # (an idle synchronize: the clock's own floor)
+            idle.append(time.perf_counter() - t2s)
         single_ms = float(np.median(lat)) * 1e3
+        single_api_ms = float(np.median(api)) * 1e3
+        sync_floor_ms = float(np.median(idle)) * 1e3
         iso_ms = float(np.median(dev.launch_times(5)[0]))
         # the drop-in pt_render_tiles path: output copied to a host buffer (PCIe-inclusive)
         host = np.zeros((H, W, 3), np.float32)
@@ -572,6 +579,9 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
                        "pipelined_frame_interval_ms": round(elapsed / frames * 1e3, 4),
                        "scene_load_s": round(t_load, 3),
                        "single_frame_ms": None if single_ms is None else round(single_ms, 3),
+                       # host time inside the render call (launch preparation) and an idle synchronize
+                       "single_frame_api_ms": None if single_ms is None else round(single_api_ms, 4),
+                       "sync_floor_ms": None if single_ms is None else round(sync_floor_ms, 4),
                        "bvh": bvh_desc(args.lbvh),
                        "upload_s": round(t_up, 4),
                        "host_output_ms_per_frame": None if host_ms is None else round(host_ms, 3)},

@@ -1180,9 +1180,21 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   static const bool pipeline = (!std::getenv("PT_PIPELINE") || std::atoi(std::getenv("PT_PIPELINE")) != 0);
   const bool census_launch = std::getenv("PT_CENSUS") && !stats;
   const int slot = pipeline && !census_launch ? (int)(c->n_launches % pt_ctx::kSlots) : 0;
-  hipStream_t rs = pipeline && !census_launch ? c->rstream[slot] : s;
+  // A launch that finds every slot's last resolve complete has no frame to
+  // overlap with: it runs on the caller's stream, with no cross-stream waits
+  // in front of the render or between the render and the resolve (a lone
+  // frame's wall clock, PT_IDLE_DIRECT; the slots still alternate).
+  bool idle = false;
+#if PT_IDLE_DIRECT
+  if (pipeline && !census_launch) {
+    idle = true;
+    for (int k = 0; k < pt_ctx::kSlots && idle; ++k) idle = hipEventQuery(c->ev_free[k]) == hipSuccess;
+    (void)hipGetLastError();  // a not-ready query is no error of this launch
+  }
+#endif
+  hipStream_t rs = pipeline && !census_launch && !idle ? c->rstream[slot] : s;
   // the slot's device state is free once the previous resolve that read it ran
-  HIPCHK(hipStreamWaitEvent(rs, c->ev_free[slot], 0));
+  if (!idle) HIPCHK(hipStreamWaitEvent(rs, c->ev_free[slot], 0));
   // the tile list rarely changes between frames: upload it only when it does
   std::vector<int4>& th = c->tiles_host[slot];
   if (tl.size() != th.size() || std::memcmp(tl.data(), th.data(), tl.size() * sizeof(int4)) != 0) {
@@ -1276,6 +1288,8 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   // triangle-only scenes take the render kernel without the sphere test
   // (branch-free leaf steps); PT_NO_TRI_ONLY forces the mixed one (A/B, tests)
   P.tri_only = c->tri_only && !std::getenv("PT_NO_TRI_ONLY") ? 1 : 0;
+  // drain helpers (PT_HELPERS); PT_NO_HELPERS turns them off (A/B, tests)
+  P.helpers = std::getenv("PT_NO_HELPERS") ? 0 : 1;
   P.drain_div = 0;
   if (const char* dd = std::getenv("PT_DRAIN_DIV")) {  // tuning knob
     int v = std::atoi(dd);

@@ -24,6 +24,12 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #ifndef PT_RESOLVE_ON_RS
 #define PT_RESOLVE_ON_RS 0  // 1: the resolve on the render slot's stream (one-frame wall +0.03 ms: profiles/r5/ab_resolve_reset_stream.txt)
 #endif
+#ifndef PT_IDLE_DIRECT
+#define PT_IDLE_DIRECT 1  // a launch with no frame in flight runs on the caller's stream (pt_api.cpp launch)
+#endif
+#ifndef PT_HELPERS
+#define PT_HELPERS 1  // retired lanes trace other lanes' shadow rays in the drain (pt_kernels.hip)
+#endif
 #ifndef PT_RESOLVE_RESETS
 #define PT_RESOLVE_RESETS 1  // the resolve zeroes its launch's queue heads for the slot's next launch
 #endif
@@ -327,6 +333,7 @@ struct KParams {
   int leaf_weight;            // leaf steps run when leaf_weight * leaf lanes >= 16 * node lanes
   int drain_div;              // queue drained: shade once alive/drain_div lanes are ready (0: 3/4 rule)
   int tri_only;               // every primitive is a triangle: the kernel without the sphere test
+  int helpers;                // drain helpers on (PT_HELPERS; PT_NO_HELPERS turns them off per launch)
   int census;                 // plain build: record each wave's start / end / CU / drain in the trace area (PT_CENSUS)
   float root_lo[3], root_hi[3];  // scene bounds (root box, rounded outward)
   int cull_x0, cull_y0, cull_x1, cull_y1;  // pixels outside [x0,x1]x[y0,y1] see no geometry

@@ -339,6 +339,9 @@ __device__ __forceinline__ bool trav_pop(const Stack& stk, Trav& tr) {
 // blocks, each with its own spill test, cost ~20 scalar instructions of
 // exec-mask bookkeeping per traversal iteration, and a scalar instruction in
 // the traversal loop costs more than a vector one (profiles/r5/probes_inst_cost.txt).
+#ifndef PT_FOLLOW_SEL
+#define PT_FOLLOW_SEL 1
+#endif
 #ifndef PT_STACK_FAST
 #define PT_STACK_FAST 1
 #endif
@@ -930,7 +933,7 @@ __device__ __forceinline__ void env_sample(const KP& P, float r1, float r2, floa
 // Lane modes of the persistent kernel.
 enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 // What follows a lane's shadow ray (the `shadow` state; 0 = not a shadow ray).
-enum : int { SH_RESUME = 1, SH_FOLLOW = 2, SH_STORE = 3, SH_STORE_FOLLOW = 4 };
+enum : int { SH_HELPER = -1, SH_RESUME = 1, SH_FOLLOW = 2, SH_STORE = 3, SH_STORE_FOLLOW = 4 };
 // Launch parameters re-read per round (see render_kernel): on for the
 // environment-light build since round 3 (C5 +6.8%, no VGPR spills instead of
 // 8) and for the common one since round 4 (C3 +0.9%, 71 SGPR spills to VGPR
@@ -1093,6 +1096,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // ng, which is dead between a path's last vertex and the next hit record.
   int shadow = 0;
   uint32_t oslot = 0;
+  // (PT_HELPERS) the lane tracing this lane's last shadow ray, -1 for none
+  int hl = -1;
   // the work slot (pixel, sample group) this lane renders: its index (where
   // the group's sum goes), its pixel as packed coordinates (x | y << 16;
   // W, H <= 65535) and its current sample
@@ -1145,6 +1150,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   unsigned long long w_empty = 0ull;  // when this wave first found the queue empty
 #if PT_CENSUS
   int census_alive = -1, census_rounds = 0;  // (census: lanes alive at the drain's first round, rounds since)
+  unsigned long long census_claim = 0ull, census_claim_max = 0ull;  // (census: wall ticks waiting on queue claims)
+  uint32_t census_claims = 0;
 #endif
   unsigned long long slot_t0 = 0ull, slot_lat_sum = 0ull, slot_lat_max = 0ull;  // work-slot latency (wall ticks)
   // per ray: traversal iterations it stepped in / sat out, traversal phases it spanned
@@ -1207,6 +1214,33 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           store_sum(P.partial + PT_SUM_WORDS * (size_t)oslot, tr.found ? acc : pend);
           acc = ng;  // the new group's sum so far (environment seen by its camera rays that missed)
         }
+#if PT_FOLLOW_SEL
+        if (shadow == SH_STORE) {
+          mode = M_DONE;
+        } else {
+          Trav nt;
+          trav_init(nt, hp, ns, 3.0e38f, false);
+          tr.o = nt.o;
+#if PT_TRAV_DIR
+          tr.d = nt.d;
+#endif
+          tr.inv = nt.inv;
+          tr.any = false;
+          mode = M_TRAV;
+        }
+        shadow = 0;
+      }
+    }
+    // the follow-up ray's traversal state by selects, outside the branch: the
+    // loop-carried node / stack / tmax / primitive keep one register each
+    // (with the branch the compiler copied them to and fro every iteration)
+    const bool fo = done && mode == M_TRAV;
+    tr.node = fo ? 0 : tr.node;
+    tr.sp = fo ? 0 : tr.sp;
+    tr.tmax = fo ? 3.0e38f : tr.tmax;
+    tr.prim = fo ? -1 : tr.prim;
+    tr.found = fo ? false : tr.found;
+#else
         if (shadow == SH_STORE) {
           mode = M_DONE;
         } else {
@@ -1216,6 +1250,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         shadow = 0;
       }
     }
+#endif
   };
 
   for (;;) {
@@ -1226,8 +1261,30 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     // base one (C4 +0.6%, C5 +0.4%, C3 within noise: profiles/r3/ab_build_options.txt)
     __builtin_amdgcn_s_setprio(PT_PRIO_SHADE);
     probe_insts<PT_PROBE_SHADE_SALU, PT_PROBE_SHADE_VALU>();
+#if PT_HELPERS
+    // Drain helpers (the pairing is at the end of the refill): a helper's
+    // shadow ray ended -- its owner adds the light sample if the ray was
+    // clear, before anything else of its path (the order of trace_ray's
+    // additions is kept), and the helper retires again.  An owner whose path
+    // ray ended first waits in M_SHADE until then.
+    if constexpr (!DBG && !BIN) {
+      const bool hdone = shadow == SH_HELPER && mode == M_SHADE;
+      const unsigned long long hd = __ballot(hdone);
+      if (hd != 0ull) {  // (wave-uniform)
+        const unsigned long long hc = __ballot(hdone && !tr.found);
+        if (hl >= 0 && ((hd >> hl) & 1ull)) {
+          if ((hc >> hl) & 1ull) acc = acc + pend;
+          hl = -1;
+        }
+        if (hdone) {
+          mode = M_DONE;
+          shadow = 0;
+        }
+      }
+    }
+#endif
     // ================= shading phase: lanes whose ray finished =================
-    if (mode == M_SHADE) {
+    if (mode == M_SHADE && (!PT_HELPERS || hl < 0)) {
       const bool found = tr.found;
       bool finish = false;  // the sample is complete
       bool group_end = false;  // the group's last sample ended: store its sum
@@ -1534,9 +1591,21 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             }
             if (nbase >= total_slots) csize = 0;  // every head ran dry: drained
 #else
+#if PT_CENSUS
+            const unsigned long long c_t0 = census ? wall_clock64() : 0ull;
+#endif
             if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
             // (the head counts the chunks after the statically dealt ones)
             nbase = __builtin_amdgcn_readfirstlane(__shfl(nbase, 0)) + (PT_STATIC_FIRST ? n_waves * csize : 0u);
+#if PT_CENSUS
+            if (census) {  // (diagnostics: how long the claim's atomic took to return)
+              asm volatile("" ::"s"(nbase));
+              const unsigned long long c_d = wall_clock64() - c_t0;
+              census_claim += c_d;
+              census_claim_max = c_d > census_claim_max ? c_d : census_claim_max;
+              ++census_claims;
+            }
+#endif
 #if PT_TAIL_CLAIMS
             if (nbase >= P.tail_start) {  // (wave-uniform) the frame's tail: 64-slot claims from the tail head
               csize = 64u;
@@ -1672,6 +1741,63 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       PT_STAMP(S_CAMERA);
       if (__ballot(mode == M_FETCH) == 0ull) break;
     }
+#if PT_HELPERS
+    // Drain helpers: once the wave's share of the queue is gone, its retired
+    // lanes (M_DONE) take the shadow rays just emitted by lanes with an
+    // extension ray behind them (SH_FOLLOW), and those lanes start that ray
+    // at once instead of after the shadow ray: the two rays of a path vertex
+    // are traced side by side, which shortens the paths the launch ends on.
+    // The k-th such lane is paired with the k-th retired one through two
+    // cross-lane permutes; the helper copies the ray (o, d, 1/d, tmax), and
+    // the owner applies the result when its helper is done (above).
+    if constexpr (!DBG && !BIN) {
+      const unsigned long long idle = __ballot(mode == M_DONE);
+      const bool want = mode == M_TRAV && shadow == SH_FOLLOW && tr.node == 0;
+      const unsigned long long wm = __ballot(want);
+      if (P.helpers && idle != 0ull && wm != 0ull) {  // (wave-uniform)
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        const int ri = __popcll(idle & lt), rw = __popcll(wm & lt);
+        const int np = min(__popcll(idle), __popcll(wm));
+        // lane r of idl / own: the lane of the r-th retired / wanting lane
+        // (the others write to lane 63, which no pair reads: the two sets are
+        // disjoint, so both are non-empty only with fewer than 64 members each)
+        const int idl = __builtin_amdgcn_ds_permute((mode == M_DONE ? ri : 63) << 2, lane);
+        const int own = __builtin_amdgcn_ds_permute((want ? rw : 63) << 2, lane);
+        const bool helper = mode == M_DONE && ri < np;
+        const bool owner = want && rw < np;
+        const int o_lane = __builtin_amdgcn_ds_bpermute(min(ri, 63) << 2, own);
+        const int h_lane = __builtin_amdgcn_ds_bpermute(min(rw, 63) << 2, idl);
+        const int src = (helper ? o_lane : lane) << 2;
+        auto pull = [&](float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(v))); };
+        const float3 so = f3(pull(tr.o.x), pull(tr.o.y), pull(tr.o.z));
+        const float3 si = f3(pull(tr.inv.x), pull(tr.inv.y), pull(tr.inv.z));
+#if PT_TRAV_DIR
+        const float3 sd = f3(pull(tr.d.x), pull(tr.d.y), pull(tr.d.z));
+#endif
+        const float st = pull(tr.tmax);
+        if (helper) {
+          tr.o = so;
+#if PT_TRAV_DIR
+          tr.d = sd;
+#endif
+          tr.inv = si;
+          tr.tmax = st;
+          tr.node = 0;
+          tr.sp = 0;
+          tr.any = true;
+          tr.found = false;
+          tr.prim = -1;
+          mode = M_TRAV;
+          shadow = SH_HELPER;
+        }
+        if (owner) {
+          trav_init(tr, hp, ns, 3.0e38f, false);
+          shadow = 0;
+          hl = h_lane;
+        }
+      }
+    }
+#endif
     // ================= traversal phase =================
     __builtin_amdgcn_s_setprio(PT_PRIO_TRAV);
     // Step every in-flight ray one node at a time; leave as soon as `batch`
@@ -1800,6 +1926,9 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       census[1] = e;
       census[4] = (unsigned long long)census_alive;
       census[5] = (unsigned long long)census_rounds;
+      census[6] = census_claim;
+      census[7] = census_claims;
+      census[8] = census_claim_max;
     }
   }
 #endif

@@ -89,6 +89,11 @@ def main():
                           "drain_us_quantiles": [round(float(np.nanquantile(end - emp, x)), 1) for x in q],
                           "alive_at_empty_quantiles": [int(np.quantile(tr[:, 4], x)) for x in q],
                           "drain_rounds_quantiles": [int(np.quantile(tr[:, 5], x)) for x in q],
+                          # queue claims (atomics on the head): wait per claim, per wave's total, the longest
+                          "claims_per_wave_mean": round(float(tr[:, 7].mean()), 2),
+                          "claim_wait_us_mean": round(float(tr[:, 6].sum() / max(1, tr[:, 7].sum()) * 0.01), 3),
+                          "claim_wait_us_per_wave_quantiles": [round(float(np.quantile(tr[:, 6] * 0.01, x)), 1) for x in q],
+                          "claim_wait_max_us_quantiles": [round(float(np.quantile(tr[:, 8] * 0.01, x)), 2) for x in q],
                           "alive_at_empty_hist8": np.bincount(np.clip(tr[:, 4], 0, 64) // 8, minlength=9).tolist(),
                           "late_starts": int((~early).sum()), "cus_seen": int(len(np.unique(cu_key))),
                           "early_waves_per_cu_min_max": [int(per_cu.min()), int(per_cu.max())],
