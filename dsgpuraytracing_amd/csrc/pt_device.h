@@ -19,7 +19,12 @@
 static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand");
 #define PT_QUEUE_WORDS 32  // a work-queue head, alone in its 128-B line
 #ifndef PT_QUEUE_HEADS
-#define PT_QUEUE_HEADS 1  // queue heads, interleaved chunk by chunk (8, one per XCD: C5 +2%, C3 / C4 / framed C3 -0.5..-1%; off)
+// queue heads, interleaved chunk by chunk, a wave starting at its XCD's: with
+// the drain helpers, 8 measured C3 +1.9% pipelined, lone launch -4.0%, C5
+// +2.2%, C4 +-0 (profiles/r5/ab_queue_heads.txt; a claim on the one head
+// waited ~1 us: census_claims.txt).  (Round 4, before the helpers: C5 +2%,
+// C3 -0.5..-1%.)
+#define PT_QUEUE_HEADS 8
 #endif
 #ifndef PT_RESOLVE_ON_RS
 #define PT_RESOLVE_ON_RS 0  // 1: the resolve on the render slot's stream (one-frame wall +0.03 ms: profiles/r5/ab_resolve_reset_stream.txt)

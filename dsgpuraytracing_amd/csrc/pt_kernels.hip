@@ -1571,6 +1571,9 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             first_claim = false;
           } else {
             csize = (uint32_t)P.chunk;
+#if PT_CENSUS
+            const unsigned long long c_t0 = census ? wall_clock64() : 0ull;
+#endif
 #if PT_QUEUE_HEADS > 1
             const uint32_t base0 = PT_STATIC_FIRST ? n_waves * csize : 0u;  // (after the statically dealt chunks)
             // PT_QUEUE_HEADS heads, one per XCD, each in its own 128-B line:
@@ -1591,21 +1594,9 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             }
             if (nbase >= total_slots) csize = 0;  // every head ran dry: drained
 #else
-#if PT_CENSUS
-            const unsigned long long c_t0 = census ? wall_clock64() : 0ull;
-#endif
             if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
             // (the head counts the chunks after the statically dealt ones)
             nbase = __builtin_amdgcn_readfirstlane(__shfl(nbase, 0)) + (PT_STATIC_FIRST ? n_waves * csize : 0u);
-#if PT_CENSUS
-            if (census) {  // (diagnostics: how long the claim's atomic took to return)
-              asm volatile("" ::"s"(nbase));
-              const unsigned long long c_d = wall_clock64() - c_t0;
-              census_claim += c_d;
-              census_claim_max = c_d > census_claim_max ? c_d : census_claim_max;
-              ++census_claims;
-            }
-#endif
 #if PT_TAIL_CLAIMS
             if (nbase >= P.tail_start) {  // (wave-uniform) the frame's tail: 64-slot claims from the tail head
               csize = 64u;
@@ -1615,6 +1606,15 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
               if (STATS) n_atomics += lane == 0;
             }
 #endif
+#endif
+#if PT_CENSUS
+            if (census) {  // (diagnostics: how long the claim's atomics took to return)
+              asm volatile("" ::"s"(nbase));
+              const unsigned long long c_d = wall_clock64() - c_t0;
+              census_claim += c_d;
+              census_claim_max = c_d > census_claim_max ? c_d : census_claim_max;
+              ++census_claims;
+            }
 #endif
             seen = nbase + csize;
             if (STATS) n_atomics += lane == 0;
@@ -2027,7 +2027,8 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
 #if PT_RESOLVE_RESETS
   // the render that wrote these sums is complete, so are its queue claims:
   // zero the heads for the render slot's next launch (pt_api.cpp launch)
-  if (ti == 0 && tid < PT_QUEUE_WORDS * (PT_QUEUE_HEADS + 1)) P.work_counter[tid] = 0u;
+  if (ti == 0)
+    for (int i = tid; i < PT_QUEUE_WORDS * (PT_QUEUE_HEADS + 1); i += 256) P.work_counter[i] = 0u;
 #endif
   auto out_at = [&](int x, int y) -> float* {
     const size_t o = P.packed ? (size_t)ti * 1024u + (size_t)(y - tile.y) * 32u + (size_t)(x - tile.x)
