@@ -1184,14 +1184,10 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   // overlap with: it runs on the caller's stream, with no cross-stream waits
   // in front of the render or between the render and the resolve (a lone
   // frame's wall clock, PT_IDLE_DIRECT; the slots still alternate).
-  bool idle = false;
-#if PT_IDLE_DIRECT
-  if (pipeline && !census_launch) {
-    idle = true;
-    for (int k = 0; k < pt_ctx::kSlots && idle; ++k) idle = hipEventQuery(c->ev_free[k]) == hipSuccess;
-    (void)hipGetLastError();  // a not-ready query is no error of this launch
-  }
-#endif
+  bool gpu_idle = true;  // no earlier render of this context still running or queued
+  for (int k = 0; k < pt_ctx::kSlots && gpu_idle; ++k) gpu_idle = hipEventQuery(c->ev_free[k]) == hipSuccess;
+  (void)hipGetLastError();  // a not-ready query is no error of this launch
+  const bool idle = PT_IDLE_DIRECT && pipeline && !census_launch && gpu_idle;
   hipStream_t rs = pipeline && !census_launch && !idle ? c->rstream[slot] : s;
   // the slot's device state is free once the previous resolve that read it ran
   if (!idle) HIPCHK(hipStreamWaitEvent(rs, c->ev_free[slot], 0));
@@ -1363,7 +1359,14 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   pt_fastdiv_init((uint32_t)P.n_groups, &P.grp_m, &P.grp_sh);
   // queue claims: bigger for frames with many slots per lane (fewer atomics
   // on the one head; a lone small frame's drain prefers the smaller claim)
-  P.chunk = slots >= (int64_t)PT_CHUNK_BIG_SLOTS * want_plain * PT_BLOCK ? PT_CHUNK_MAX : PT_CHUNK;
+  // and for a frame queued behind another (PT_CHUNK_BUSY): its drain overlaps
+  // the previous frame's -- the throughput case -- while a frame launched on
+  // an idle GPU is the latency case, whose end the smaller claim shortens
+  // (C3: 256-slot claims +2.9% pipelined, lone launch +9%:
+  // profiles/r5/ab_chunk_heads.txt).  A claim size never changes a value.
+  P.chunk = slots >= (int64_t)PT_CHUNK_BIG_SLOTS * want_plain * PT_BLOCK || (PT_CHUNK_BUSY && !gpu_idle)
+                ? PT_CHUNK_MAX
+                : PT_CHUNK;
   if (const char* cs = std::getenv("PT_CHUNK_SLOTS")) {  // tuning knob (64..PT_CHUNK_MAX, a multiple of 64)
     const int v = std::atoi(cs);
     if (v >= 64 && v <= PT_CHUNK_MAX && v % 64 == 0) P.chunk = v;
