@@ -1364,13 +1364,23 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   // an idle GPU is the latency case, whose end the smaller claim shortens
   // (C3: 256-slot claims +2.9% pipelined, lone launch +9%:
   // profiles/r5/ab_chunk_heads.txt).  A claim size never changes a value.
-  P.chunk = slots >= (int64_t)PT_CHUNK_BIG_SLOTS * want_plain * PT_BLOCK || (PT_CHUNK_BUSY && !gpu_idle)
+  const bool big_frame = slots >= (int64_t)PT_CHUNK_BIG_SLOTS * want_plain * PT_BLOCK;
+  P.chunk = big_frame || (PT_CHUNK_BUSY && !gpu_idle)
                 ? PT_CHUNK_MAX
                 : PT_CHUNK;
   if (const char* cs = std::getenv("PT_CHUNK_SLOTS")) {  // tuning knob (64..PT_CHUNK_MAX, a multiple of 64)
     const int v = std::atoi(cs);
     if (v >= 64 && v <= PT_CHUNK_MAX && v % 64 == 0) P.chunk = v;
   }
+  // Large frames (PT_CHUNK_BIG_SLOTS slots per lane and more) over trees
+  // larger than two XCD L2s (4 MB each): each queue head deals a contiguous
+  // band of the frame, so an XCD's waves share BVH nodes in its L2 (C5's 17-MB
+  // tree +1.8%, c5big's 68-MB +1.8%); C4's 4-MB tree loses 1.2% to the bands'
+  // uneven ends, and a small frame keeps the interleaved sweep, whose heads
+  // run dry together (C3 -5.5%, its lone launch +12%): profiles/r5/ab_bands*.txt.
+  // PT_QUEUE_BANDS=0/1 forces it (A/B, tests).
+  P.qbands = big_frame && (int64_t)c->n_render_nodes * 128 > ((int64_t)PT_BANDS_TREE_MIB << 20) ? 1 : 0;
+  if (const char* qb = std::getenv("PT_QUEUE_BANDS")) P.qbands = std::atoi(qb) != 0 ? 1 : 0;
   P.sblocks = (64 * P.n_groups) % P.chunk == 0 ? 1 : 0;  // every (aligned) chunk inside one block
   // group sums: 12 B per work slot of THIS launch (a rank's share of a split
   // frame holds only its own blocks' sums)

@@ -16,6 +16,9 @@
 #ifndef PT_CHUNK_BUSY
 #define PT_CHUNK_BUSY 1  // PT_CHUNK_MAX claims also for a frame launched while another is in flight (pt_api.cpp launch)
 #endif
+#ifndef PT_BANDS_TREE_MIB
+#define PT_BANDS_TREE_MIB 8  // queue bands for large frames over render trees above this size (pt_api.cpp launch)
+#endif
 #ifndef PT_CHUNK_BIG_SLOTS
 #define PT_CHUNK_BIG_SLOTS 128  // C4 (184 slots per lane) +1.5%, C5 (1,620) +6.6%; C3 (26), framed C3 (51): their lone launches lose
 #endif
@@ -342,6 +345,7 @@ struct KParams {
   int drain_div;              // queue drained: shade once alive/drain_div lanes are ready (0: 3/4 rule)
   int tri_only;               // every primitive is a triangle: the kernel without the sphere test
   int helpers;                // drain helpers on (PT_HELPERS; PT_NO_HELPERS turns them off per launch)
+  int qbands;                 // queue heads deal contiguous bands, not interleaved chunks (large frames)
   int census;                 // plain build: record each wave's start / end / CU / drain in the trace area (PT_CENSUS)
   float root_lo[3], root_hi[3];  // scene bounds (root box, rounded outward)
   int cull_x0, cull_y0, cull_x1, cull_y1;  // pixels outside [x0,x1]x[y0,y1] see no geometry

@@ -1585,7 +1585,18 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
               uint32_t r = 0;
               if (lane == 0) r = atomicAdd(P.work_counter + qh * PT_QUEUE_WORDS, 1u);
               r = __builtin_amdgcn_readfirstlane(__shfl(r, 0));
-              const uint64_t cand = (uint64_t)base0 + ((uint64_t)r * PT_QUEUE_HEADS + qh) * csize;
+              uint64_t cand;
+              if (P.qbands) {  // (wave-uniform)
+                // head h deals the h-th of H contiguous bands of the dynamic
+                // slots: an XCD's waves render neighbouring pixels, whose rays
+                // share BVH nodes in that XCD's L2 (host: large frames only)
+                const uint32_t span = total_slots > base0 ? total_slots - base0 : 0u;
+                const uint32_t band = (span + PT_QUEUE_HEADS * csize - 1u) / (PT_QUEUE_HEADS * csize) * csize;
+                cand = (uint64_t)r * csize < (uint64_t)band ? (uint64_t)base0 + (uint64_t)qh * band + (uint64_t)r * csize
+                                                           : (uint64_t)total_slots;
+              } else {  // interleaved: head h deals chunks h, h + H, ...
+                cand = (uint64_t)base0 + ((uint64_t)r * PT_QUEUE_HEADS + qh) * csize;
+              }
               if (cand < (uint64_t)total_slots) {
                 nbase = (uint32_t)cand;
                 break;

@@ -228,23 +228,26 @@ def test_hip_resident_grid_and_tail_claims_never_change_values(monkeypatch, scen
     grid (PT_WAVES_PER_CU: 20 = a whole MI355X, 8, 1 -- as a CPX partition or
     a smaller device would give) does not change the sample grouping (VERDICT
     r4 weak 8) nor any value.  With one wave per CU the frame's slots also
-    outrun the statically dealt chunks, so dynamic claims and the tail head
-    (PT_TAIL_SLOTS, where built in) run: bit-identical with the tail off, one
-    or four tail slots per lane."""
+    outrun the statically dealt chunks, so dynamic claims run from the eight
+    queue heads: bit-identical whether the heads deal interleaved chunks or
+    contiguous bands (PT_QUEUE_BANDS), with 64-slot claims, and with the tail
+    head (PT_TAIL_SLOTS, where built in)."""
     ref, _ = gpu_render(scene, w, h, spp, seed=29)
     monkeypatch.setenv("PT_WAVES_PER_CU", "8")
     img, _ = gpu_render(scene, w, h, spp, seed=29)
     assert np.array_equal(img, ref)
     monkeypatch.setenv("PT_WAVES_PER_CU", "1")
-    for tail in ("0", "1", "4"):
-        monkeypatch.setenv("PT_TAIL_SLOTS", tail)
+    for knob, tail in (("PT_QUEUE_BANDS", "0"), ("PT_QUEUE_BANDS", "1"), ("PT_CHUNK_SLOTS", "64"),
+                       ("PT_TAIL_SLOTS", "1")):
+        monkeypatch.setenv(knob, tail)
         img, st = gpu_render(scene, w, h, spp, seed=29, stats=True)
-        assert np.array_equal(img, ref), tail
+        assert np.array_equal(img, ref), (knob, tail)
         parts = np.zeros_like(ref)
         for shard, tl in enumerate((tile_fifo(w, h)[0::2], tile_fifo(w, h)[1::2])):
             p, _ = gpu_render(scene, w, h, spp, seed=29, tiles=tl)
             parts += p
-        assert np.array_equal(parts, ref), tail
+        assert np.array_equal(parts, ref), (knob, tail)
+        monkeypatch.delenv(knob)
 
 
 @pytest.mark.parametrize("scene,w,h", [("c1_default_128x128", 128, 128), ("c1_sphcam_96x64", 96, 64),
