@@ -1359,13 +1359,15 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   pt_fastdiv_init((uint32_t)P.n_groups, &P.grp_m, &P.grp_sh);
   // queue claims: bigger for frames with many slots per lane (fewer atomics
   // on the one head; a lone small frame's drain prefers the smaller claim)
-  // and for a frame queued behind another (PT_CHUNK_BUSY): its drain overlaps
-  // the previous frame's -- the throughput case -- while a frame launched on
-  // an idle GPU is the latency case, whose end the smaller claim shortens
+  // and for a frame queued behind another in the render pipeline
+  // (PT_CHUNK_BUSY): its drain overlaps the previous frame's -- the
+  // throughput case -- while a frame launched on an idle GPU, or with the
+  // pipeline off (PT_PIPELINE=0: no two launches overlap), is the latency
+  // case, whose end the smaller claim shortens
   // (C3: 256-slot claims +2.9% pipelined, lone launch +9%:
   // profiles/r5/ab_chunk_heads.txt).  A claim size never changes a value.
   const bool big_frame = slots >= (int64_t)PT_CHUNK_BIG_SLOTS * want_plain * PT_BLOCK;
-  P.chunk = big_frame || (PT_CHUNK_BUSY && !gpu_idle)
+  P.chunk = big_frame || (PT_CHUNK_BUSY && pipeline && !census_launch && !gpu_idle)
                 ? PT_CHUNK_MAX
                 : PT_CHUNK;
   if (const char* cs = std::getenv("PT_CHUNK_SLOTS")) {  // tuning knob (64..PT_CHUNK_MAX, a multiple of 64)
