@@ -1628,6 +1628,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             }
 #endif
             seen = nbase + csize;
+#if PT_QUEUE_HEADS > 1
+            // (several heads: the end of one head's range -- the last chunk of
+            // the frame, or of a band -- is not the queue's; the wave has seen
+            // the queue drained only when every head was dry, csize == 0)
+            if (csize != 0u) seen = min(seen, total_slots - 1u);
+#endif
             if (STATS) n_atomics += lane == 0;
           }
         }
@@ -1667,8 +1673,13 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
           uint32_t slot = rank < avail ? chunk_next + rank : nbase + (rank - avail);
           if (slot >= total_slots) {
-            mode = shadow ? M_TRAV : M_DONE;  // (a pending shadow ray is traced first)
-            if ((STATS || (PT_CENSUS && census)) && w_empty == 0ull) w_empty = wall_clock64();
+            // past the end of the claimed chunk's range: retire once the queue
+            // is drained; otherwise (a partial last chunk of one head's range)
+            // stay M_FETCH for the refill's next claim
+            if (seen >= total_slots) {
+              mode = shadow ? M_TRAV : M_DONE;  // (a pending shadow ray is traced first)
+              if ((STATS || (PT_CENSUS && census)) && w_empty == 0ull) w_empty = wall_clock64();
+            }
           } else {
             // Blocks are <= 8x8 pixel rectangles of the tiles, clipped to the
             // scene's screen footprint (pixels outside are written 0 by
@@ -1691,8 +1702,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           }
         }
         if (cnt > avail) {  // wave-uniform
-          chunk_next = nbase + (cnt - avail);
-          chunk_end = nbase + csize;
+          chunk_end = min(nbase + csize, total_slots);  // (a partial last chunk ends at the frame's end)
+          chunk_next = min(nbase + (cnt - avail), chunk_end);
           if (csize == 0) chunk_next = chunk_end = total_slots;  // drained: nothing left to hand out
         } else {
           chunk_next += cnt;
