@@ -1370,9 +1370,14 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.chunk = big_frame || (PT_CHUNK_BUSY && pipeline && !census_launch && !gpu_idle)
                 ? PT_CHUNK_MAX
                 : PT_CHUNK;
-  if (const char* cs = std::getenv("PT_CHUNK_SLOTS")) {  // tuning knob (64..PT_CHUNK_MAX, a multiple of 64)
+  // large frames claim PT_CHUNK_BIG (512) where the slot indices and the
+  // one-block-per-chunk rule allow it: half the atomics again (C5 +1.0%, C4
+  // +0.7%; C3's queued frames lose 7% at 512: profiles/r5/ab_chunk512.txt)
+  if (big_frame && slots + 2 * want * PT_CHUNK_BIG < (int64_t)INT32_MAX && (64 * P.n_groups) % PT_CHUNK_BIG == 0)
+    P.chunk = PT_CHUNK_BIG;
+  if (const char* cs = std::getenv("PT_CHUNK_SLOTS")) {  // tuning knob (64..PT_CHUNK_BIG, a multiple of 64)
     const int v = std::atoi(cs);
-    if (v >= 64 && v <= PT_CHUNK_MAX && v % 64 == 0) P.chunk = v;
+    if (v >= 64 && v <= PT_CHUNK_BIG && v % 64 == 0 && slots + 2 * want * v < (int64_t)INT32_MAX) P.chunk = v;
   }
   // Large frames (PT_CHUNK_BIG_SLOTS slots per lane and more) over trees
   // larger than two XCD L2s (4 MB each): each queue head deals a contiguous

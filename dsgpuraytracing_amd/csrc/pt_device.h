@@ -13,6 +13,9 @@
 #ifndef PT_CHUNK_MAX
 #define PT_CHUNK_MAX 256  // the claim for frames with >= PT_CHUNK_BIG_SLOTS slots per resident lane
 #endif
+#ifndef PT_CHUNK_BIG
+#define PT_CHUNK_BIG 512  // the claim for large frames where it fits (pt_api.cpp launch)
+#endif
 #ifndef PT_CHUNK_BUSY
 #define PT_CHUNK_BUSY 1  // PT_CHUNK_MAX claims also for a frame launched while another is in flight (pt_api.cpp launch)
 #endif
