@@ -1358,7 +1358,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   if (slots + 2 * want * PT_CHUNK_MAX >= (int64_t)INT32_MAX) return fail(PT_E_INVALID, "frame too large for one launch");
   pt_fastdiv_init((uint32_t)P.n_groups, &P.grp_m, &P.grp_sh);
   // queue claims: bigger for frames with many slots per lane (fewer atomics
-  // on the one head; a lone small frame's drain prefers the smaller claim)
+  // on the heads; a lone small frame's drain prefers the smaller claim)
   // and for a frame queued behind another in the render pipeline
   // (PT_CHUNK_BUSY): its drain overlaps the previous frame's -- the
   // throughput case -- while a frame launched on an idle GPU, or with the

@@ -1544,11 +1544,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       unsigned long long m = __ballot(need);
       if (m != 0ull) {
         // Lanes are served from the wave's private chunk of P.chunk
-        // consecutive slots; one atomic on the one queue head (memory-side,
-        // since the XCD L2s are not coherent) refills it.  128 slots, 256 for
-        // launches with >= 128 slots per lane (half the atomics: C5 +6.6%, C4
-        // +1.5%), chosen on the host (profiles/r4/ab_chunk_claims.txt).  (One queue per XCD
-        // over bands of the frame measured C3 -9%.)
+        // consecutive slots; one atomic on a queue head (memory-side, since
+        // the XCD L2s are not coherent; PT_QUEUE_HEADS of them, a wave starting
+        // at its XCD's) refills it.  The claim size (128 / 256 / 512) and the
+        // heads' dealing (interleaved chunks or contiguous bands) are chosen
+        // on the host per launch (pt_api.cpp launch; profiles/r5/ab_chunk_*.txt,
+        // ab_queue_heads.txt, ab_bands*.txt).
         uint32_t cnt = (uint32_t)__popcll(m);
         uint32_t avail = chunk_end - chunk_next;
         uint32_t nbase = 0, csize = 0;
