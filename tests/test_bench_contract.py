@@ -91,6 +91,23 @@ def test_committed_bench_lines_keep_the_contract():
     assert d["dist"]["world_size"] == 1
 
 
+def test_round5_line_reports_one_frames_wall_clock():
+    """config.render_time_s is ONE frame's start-to-image
+    wall clock (single_frame_ms), not the pipelined interval; the host's share
+    of it and an idle synchronize are on the line beside it."""
+    path = os.path.join(ROOT, "profiles", "r5", "bench_c3_default.jsonl")
+    with open(path) as f:
+        d = json.loads(f.read().strip().splitlines()[-1])
+    c = d["config"]
+    assert c["render_time_s"] == pytest.approx(c["single_frame_ms"] / 1e3, rel=1e-3)
+    assert c["wall_clock_frame_ms"] == pytest.approx(c["single_frame_ms"], rel=1e-6)
+    assert 0.0 < c["single_frame_api_ms"] < c["single_frame_ms"]
+    assert 0.0 < c["sync_floor_ms"] < c["single_frame_ms"]
+    # one frame alone takes at least one lone launch, the pipelined step less
+    assert c["single_frame_ms"] >= d["roofline"]["isolated_kernel_ms"] >= d["ms_per_step"] * 0.9
+    assert d["cpu_baseline_published"]["cores"] == 8
+
+
 def test_kernel_sha_reads_the_device_code_section():
     from dsgpuraytracing_amd import elfsha, native
     lib = native.LIB_PATH
