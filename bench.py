@@ -14,19 +14,19 @@ the scene.
 
   * N = 1 (default): C3 = CBdragon proxy CBbunny_sub1 (114,316 triangles;
     CBdragon.dae is absent), 1024x1024, 64 spp.
-  * N > 1 (torchrun, one process per GPU), default: the SAME C3 workload per
-    GPU ("scaling": "weak"): rank r renders one 64-spp pass of the whole
-    frame over sample indices 64r .. 64r+63 (the counter RNG is keyed by the
-    sample index, so the passes are disjoint slices of one 64N-spp render),
-    then ONE RCCL sum-reduce assembles the 64N-spp image on rank 0; value =
-    N*W*H*64 / max-rank time.  Per-GPU work is the N = 1 line's, so the
-    driver's per-N values form a scaling curve of one workload.
-  * --workload c4 --scaling strong: BASELINE C4 = the same scene at
-    1920x1080, 256 spp, ONE frame's 32x32 tiles dealt diagonally over the
-    GPUs, each rank rendering its tiles into a packed buffer, then ONE RCCL
-    gather of the packed tiles onto rank 0; value =
-    W*H*256 / max-rank time ("scaling": "strong"), the image bit-identical
-    to the 1-GPU image.
+  * N > 1 (torchrun, one process per GPU), default: the SAME C3 frame split
+    over the GPUs ("scaling": "strong", north_star's "near-linear tile
+    scaling"): the frame's 32x32 tiles dealt diagonally, each rank rendering
+    its tiles into a packed buffer, then ONE RCCL gather of the packed tiles
+    onto rank 0, pipelined: frame k's gather + scatter run
+    on a side stream behind an event while frame k+1 renders (double-
+    buffered packed tiles, dist.PipelinedExchange); value = W*H*64 *
+    frames / max-rank time, the image bit-identical to the 1-GPU image.
+    `efficiency` = value / (N * rate_1), rate_1 measured by rank 0 rendering
+    the whole frame alone behind a barrier (null when ranks share a device).
+    Companions: BASELINE C4 (1080p, 256 spp) split the same way, and the weak
+    C3 pass (each rank one 64-spp pass over disjoint sample indices + one
+    RCCL sum-reduce; `--scaling weak` makes it the value).
 The exchange is inside the timed region.  Device renders are queued back to
 back and consecutive frames overlap on the GPU (pt_api.cpp's two-slot render
 pipeline: the next frame's waves fill the CUs the previous frame's drain
@@ -319,7 +319,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the companion measurements (N = 1: framed C3, single-GPU C4 and C5, host-SAH tree, "
-                         "per-tile seams; N > 1: strong scaling of the C3 and C4 frames)")
+                         "per-tile seams; N > 1: the C4 frame split and the weak C3 pass)")
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
                     help="default: c3 (the headline config) at every N")
     ap.add_argument("--lbvh", action="store_true", help="build the BVH on the GPU (pt_upload_scene_lbvh)")
@@ -327,10 +327,10 @@ def main():
     ap.add_argument("--emulate-shard", type=int, default=0,
                     help="diagnostic: render only one rank's share of an N-GPU split on this one GPU")
     ap.add_argument("--emulate-rank", type=int, default=0, help="the rank --emulate-shard renders")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="N > 1: weak = one pass of the whole frame per GPU over disjoint sample ranges + one RCCL "
-                         "reduce (default); strong = one frame's tiles split across the GPUs + one RCCL gather "
-                         "(BASELINE C4: --workload c4 --scaling strong)")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="N > 1: strong = one frame's tiles split across the GPUs + one pipelined RCCL gather "
+                         "(default; BASELINE C4: --workload c4); weak = one pass of the whole frame per GPU over "
+                         "disjoint sample ranges + one RCCL reduce")
     args = ap.parse_args()
     if os.environ.get("PT_BENCH_LBVH") == "1":  # A/B arms (tools/ab.sh): the GPU-built tree
         args.lbvh = True
@@ -338,7 +338,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from dsgpuraytracing_amd.dist import RankFailure, StepGuard, TileExchange, check_value_knobs, init_from_env, shard_tiles
+    from dsgpuraytracing_amd.dist import (PipelinedExchange, RankFailure, StepGuard, check_value_knobs, init_from_env,
+                                          shard_tiles)
     # PT_DIST_BACKEND=gloo + PT_BENCH_DEVICE=0: rehearsal of the N-rank flow
     # with every rank on one GPU (the exchange then stages through host memory)
     backend = os.environ.get("PT_DIST_BACKEND", "nccl")
@@ -353,7 +354,7 @@ def main():
     torch.cuda.set_stream(torch.cuda.Stream(device=local))
     rank, world, _ = init_from_env(backend)
     try:
-        bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExchange, check_value_knobs, shard_tiles)
+        bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, check_value_knobs, shard_tiles)
     except RankFailure as e:
         # every rank raises it (dist.agree_status): report, leave the group, exit non-zero
         print(f"[bench rank {rank}] aborted: {e}", file=sys.stderr, flush=True)
@@ -366,7 +367,7 @@ def main():
         dist.destroy_process_group()
 
 
-def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExchange, check_value_knobs, shard_tiles):
+def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, check_value_knobs, shard_tiles):
     import torch
     import torch.distributed as dist
 
@@ -401,13 +402,19 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
     stream = torch.cuda.current_stream().cuda_stream
 
     # strong: this rank's share of the tiles; weak (and one GPU): every tile
-    mine_arr = np.asarray(tiles if weak else shard_tiles(tiles, rank, world), dtype=np.int32).reshape(-1, 4)
+    mine_arr = np.asarray(tiles, dtype=np.int32).reshape(-1, 4)
     if args.emulate_shard > 1:
         mine_arr = np.asarray(shard_tiles(tiles, args.emulate_rank, args.emulate_shard, "diag"),
                               dtype=np.int32).reshape(-1, 4)
-    ex = TileExchange(tiles, W, H, rank, world, frame.device) if world > 1 and not weak else None
-    if ex is not None:
-        mine_arr = np.asarray(ex.mine, dtype=np.int32).reshape(-1, 4)
+    # strong: double-buffered packed tiles, the gather on a side stream
+    pex = PipelinedExchange(tiles, W, H, rank, world, frame.device) if world > 1 and not weak else None
+    if args.emulate_shard > 1:
+        # one rank's share through the same packed render + side-stream
+        # exchange (here a device copy of the share's packed tiles and their
+        # scatter: the gather's link time is not in it), host overheads included
+        pex = PipelinedExchange([tuple(int(v) for v in t) for t in mine_arr], W, H, 0, 1, frame.device)
+    if pex is not None:
+        mine_arr = np.asarray(pex.mine, dtype=np.int32).reshape(-1, 4)
 
     band = [frame]  # weak: the rows the reduce carries (set from the launch's screen footprint below)
 
@@ -430,9 +437,10 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
     # collective at the synchronisation points) then stops every rank with the
     # failing rank's error (dsgpuraytracing_amd.dist.RankFailure).
     guard = StepGuard()
+    kframe = [0]  # frames issued (the strong split's packed buffer is frame % 2)
 
     def step(stats=False, timed=False):
-        if ex is None:  # the whole tile FIFO straight into the frame (one GPU, or this rank's pass)
+        if pex is None:  # the whole tile FIFO straight into the frame (one GPU, or this rank's pass)
             guard.run(dev.render_tiles_device, mine_arr, frame.data_ptr(), stream, stats=stats)
             if weak:
                 e0 = torch.cuda.Event(enable_timing=True)
@@ -442,15 +450,13 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
                 e1.record()
                 if timed:
                     xev.append((e0, e1))
-        else:  # this rank's tiles into its packed buffer, then one gather onto rank 0
-            guard.run(dev.render_tiles_device, mine_arr, ex.packed.data_ptr(), stream, stats=stats, packed=True)
-            e0 = torch.cuda.Event(enable_timing=True)
-            e0.record()
-            ex.exchange(frame)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record()
-            if timed:
-                xev.append((e0, e1))
+        else:  # this rank's tiles into a packed buffer, then one gather onto rank 0 off the render's stream
+            k = kframe[0]
+            kframe[0] += 1
+            buf = pex.packed_for(k)
+            guard.run(dev.render_tiles_device, mine_arr, buf.data_ptr(), stream, stats=stats, packed=True,
+                      out_floats=buf.numel())
+            pex.exchange(k, frame, timed=timed)
         return guard.run(dev.stats) if stats else None
 
     # counters for the roofline's algorithmic bytes: the reference's binary BVH
@@ -480,6 +486,8 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
     t0 = time.perf_counter()
     for _ in range(args.steps):  # asynchronous: nothing waits on the GPU inside a step
         step(timed=True)
+    if pex is not None:
+        pex.drain()  # (the render stream waits for the last side-stream exchange)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -488,23 +496,31 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
     # HIP events recorded around every launch on its stream (the timed ones)
     kernel_ms, resolve_ms = dev.launch_times(args.steps)
     xchg_ms = float(np.mean([a.elapsed_time(b) for a, b in xev])) if xev else 0.0
+    if pex is not None:
+        xchg_ms = pex.exchange_ms()
+    # strong split: the 1-GPU point of the curve, rank 0 rendering the whole
+    # frame alone behind a barrier (the other ranks idle), same clock and frames
+    rate1, shared = None, False
+    if world > 1 and not weak:
+        rate1, shared = single_gpu_rate(dev, tiles, W, H, SPP, frame, stream, rank, backend, args.steps)
     per_rank = None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         mine = torch.tensor([float(np.mean(kernel_ms)), float(np.mean(resolve_ms)), xchg_ms,
-                             float(np.sum(mine_arr[:, 2] * mine_arr[:, 3])), float(st_perf["partial_bytes"])],
+                             float(np.sum(mine_arr[:, 2] * mine_arr[:, 3])), float(st_perf["partial_bytes"]),
+                             float(st_counts["culled_samples"])],
                             dtype=torch.float64, device="cpu" if backend == "gloo" else f"cuda:{local}")
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         per_rank = [[round(float(v), 4) for v in r.cpu().tolist()] for r in allr]
 
-    strong = None
-    if world > 1 and not args.no_extras and weak:
+    multi = None
+    if world > 1 and not args.no_extras:
         # every rank takes part (collectives inside)
-        strong = strong_companions(local, rank, world, backend, StepGuard, TileExchange,
-                                   frames=max(3, min(args.steps, 10)))
+        multi = multi_gpu_companions(local, rank, world, backend, StepGuard, PipelinedExchange,
+                                     frames=max(3, min(args.steps, 10)), with_weak=not weak)
 
     host_ms = None
     single_ms = None
@@ -569,7 +585,7 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
                        "spp_total": SPP * world if weak else SPP,
                        "parallelism": (f"samples{world}" if weak else f"tiles{world}") if world > 1 else "single",
                        "exchange_bytes_per_rank": (int(band[0].numel() * 4) if weak else
-                                                   (int(ex.packed.numel() * 4) if ex is not None else 0)),
+                                                   (int(pex.ex.packed.numel() * 4) if pex is not None else 0)),
                        # BASELINE's "wall-clock render time": ONE frame start to image,
                        # synchronised on both sides (the reference's timer spans one
                        # render, application.cpp:776-780); the pipelined frame
@@ -603,13 +619,36 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
         }
         rays = st_counts["camera_rays"] + st_counts["bounce_rays"] + st_counts["shadow_rays"]
         out["ray_casts_per_s_M"] = round(rays * frames * (world if weak else 1) / elapsed / 1e6, 1)
+        # The rates a reader needs beside `value`: samples
+        # actually traced (the footprint cull's samples excluded; a strong
+        # split sums its ranks' culls), and one frame alone (no overlap with a
+        # neighbouring frame: W*H*spp / single_frame_ms)
+        culled = (sum(r[5] for r in per_rank) if (per_rank and not weak) else
+                  st_counts["culled_samples"] * (world if weak else 1))
+        out["traced_samples_per_s_M"] = round((W * H * SPP * (world if weak else 1) - culled) * frames / elapsed / 1e6, 1)
+        out["single_frame_Mrays"] = None if single_ms is None else round(W * H * SPP / (single_ms * 1e-3) / 1e6, 1)
+        # the graded kernel fraction: the isolated launch's VALU-issue fraction
+        vv = out["roofline"]["views"].get("valu")
+        out["roofline"]["frac_kernel"] = vv.get("frac_isolated") if vv else None
         if per_rank is not None:
-            out["per_rank"] = {"fields": ["kernel_ms", "resolve_ms", "exchange_ms", "pixels", "partial_bytes"],
+            out["per_rank"] = {"fields": ["kernel_ms", "resolve_ms", "exchange_ms", "pixels", "partial_bytes",
+                                          "culled_samples"],
                                "ranks": per_rank}
-        if strong is not None:
-            out["companions"] = strong
-        elif xev:
+        if xev or pex is not None:
             out["exchange_ms"] = round(xchg_ms, 4)
+        if world > 1 and not weak:
+            # the strong split's scaling inputs (ADVICE r5:
+            # rate_1 from rank 0 alone, efficiency null when ranks share a GPU)
+            out["single_gpu_value"] = None if rate1 is None else round(rate1, 1)
+            out["efficiency"] = None if (rate1 is None or shared) else round(value / (world * rate1), 4)
+            out["shared_device"] = shared
+            out["exchange"] = "pipelined: packed-tile gather + scatter of frame k on a side stream behind an event, " \
+                              "overlapping frame k+1's render (double-buffered packed tiles)"
+            if per_rank:
+                kms = [r[0] for r in per_rank]
+                out["kernel_ms_slowest_over_mean"] = round(max(kms) / max(1e-9, float(np.mean(kms))), 4)
+        if multi is not None:
+            out["companions"] = multi
         if world == 1 and not args.no_extras and workload == "c3" and not args.scene_dump:
             out["companions"] = companions(dev, local, stream, max(2, min(args.steps, 5)))
         out["dist"] = {"backend": backend if world > 1 else None,
@@ -636,108 +675,211 @@ def bench_run(args, backend, local, rank, world, RankFailure, StepGuard, TileExc
         print(json.dumps(out), flush=True)
 
 
-def strong_companions(local, rank, world, backend, StepGuard, TileExchange, frames=5, warmup=2):
-    """N > 1 companions (never `value`): STRONG scaling of one frame -- its
-    32x32 tiles dealt diagonally over the N GPUs, each rank rendering its
-    tiles into a packed buffer, ONE RCCL gather onto rank 0
-    -- for the headline C3 frame and for BASELINE C4 (1080p, 256 spp, the
-    multi-GPU config).  Same clock as the headline: barrier + synchronise on
-    both sides of `frames` back-to-back frames, max over ranks; value =
-    W*H*spp*frames / that time.  Images are bit-identical to 1 GPU
-    (tests/test_dist.py, test_c4_fullsize_eight_way_split_bit_identical)."""
+def device_fingerprint(local: int) -> str:
+    """This rank's GPU: host and device UUID (or ordinal): two ranks with the
+    same fingerprint share one device (the one-GPU rehearsal)."""
+    import socket
+
+    import torch
+    try:
+        dev_id = str(torch.cuda.get_device_properties(local).uuid)
+    except Exception:  # pragma: no cover - older torch without uuid
+        dev_id = str(local)
+    return f"{socket.gethostname()}:{dev_id}"
+
+
+def single_gpu_rate(dev, tiles, w, h, spp, frame, stream, rank, backend, frames, warmup=2):
+    """Collective.  The 1-GPU point of the strong-split curve: rank 0 renders
+    the WHOLE frame `frames` times alone, back to back, behind a barrier (the
+    other ranks wait in it, their GPUs idle), synchronised on both sides ->
+    M samples/s, broadcast to every rank.  Also whether two ranks share a
+    device (then the N-rank value is no scaling point: efficiency null)."""
+    import torch
+    import torch.distributed as dist
+
+    fps = [None] * dist.get_world_size()
+    dist.all_gather_object(fps, device_fingerprint(torch.cuda.current_device()))
+    shared = len(set(fps)) < len(fps)
+    dist.barrier()
+    rate = torch.zeros(1, dtype=torch.float64, device="cpu" if backend == "gloo" else frame.device)
+    if rank == 0:
+        whole = np.asarray(tiles, dtype=np.int32).reshape(-1, 4)
+        scratch = torch.empty_like(frame)
+        for _ in range(warmup):
+            dev.render_tiles_device(whole, scratch.data_ptr(), stream)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            dev.render_tiles_device(whole, scratch.data_ptr(), stream)
+        torch.cuda.synchronize()
+        rate.fill_(w * h * spp * frames / (time.perf_counter() - t0) / 1e6)
+        del scratch
+    dist.barrier()
+    dist.broadcast(rate, src=0)
+    return float(rate.item()), shared
+
+
+def timed_max(el, backend, local):
+    """Collective: the slowest rank's time of a region every rank timed."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([el], dtype=torch.float64, device="cpu" if backend == "gloo" else f"cuda:{local}")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def multi_gpu_companions(local, rank, world, backend, StepGuard, PipelinedExchange, frames=5, warmup=2,
+                         with_weak=True):
+    """N > 1 companions (never `value`), same clock as the headline (barrier +
+    synchronise on both sides of `frames` back-to-back frames, max over
+    ranks):
+      * c4_strong: BASELINE C4 (1080p, 256 spp, the multi-GPU config), its
+        32x32 tiles dealt diagonally over the N GPUs, packed tiles gathered
+        onto rank 0 on a side stream while the next frame renders (SURVEY.md
+        §8(e)); efficiency against rank 0 rendering the whole frame alone;
+        images bit-identical to 1 GPU (tests/test_dist.py,
+        test_c4_fullsize_eight_way_split_bit_identical);
+      * c3_weak: the headline frame as N disjoint 64-spp passes, one per GPU
+        (sample indices 64r .. 64r+63; the counter RNG is keyed by the sample
+        index), then ONE RCCL sum-reduce of the footprint's rows onto rank 0:
+        a 64N-spp image; value = N*W*H*64*frames / time."""
     import torch
     import torch.distributed as dist
 
     from dsgpuraytracing_amd.pathtracer import Device, Scene, tile_fifo
     res = {}
     stream = torch.cuda.current_stream().cuda_stream
-    for name in ("c3", "c4"):
-        wl = WORKLOADS[name]
-        w, h, spp = wl["w"], wl["h"], wl["spp"]
-        dae, envmap, cam = workload_scene(wl)
-        sc = Scene.from_dae(dae, w, h, cam_info=cam, envmap=envmap)
-        dev = Device(local)
-        dev.upload_scene(sc)
-        dev.set_camera(sc.camera)
-        dev.set_params(w, h, spp, DEPTH, NSL, SEED)
-        frame = torch.zeros((h, w, 3), dtype=torch.float32, device=f"cuda:{local}")
-        ex = TileExchange(tile_fifo(w, h), w, h, rank, world, frame.device)
-        mine = np.asarray(ex.mine, dtype=np.int32).reshape(-1, 4)
-        guard = StepGuard()
-        xev = []
-        # the 1-GPU point of the curve, in this process: every rank renders the
-        # WHOLE frame alone (no exchange), same clock; efficiency = rate_N /
-        # (N * rate_1)
-        whole = np.asarray(tile_fifo(w, h), dtype=np.int32).reshape(-1, 4)
-        for _ in range(warmup):
-            guard.run(dev.render_tiles_device, whole, frame.data_ptr(), stream)
-        guard.check()
-        dist.barrier()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(frames):
-            guard.run(dev.render_tiles_device, whole, frame.data_ptr(), stream)
-        dist.barrier()
-        torch.cuda.synchronize()
-        el1 = time.perf_counter() - t1
-        guard.check()
-        t = torch.tensor([el1], dtype=torch.float64, device="cpu" if backend == "gloo" else f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        rate1 = w * h * spp * frames / float(t.item()) / 1e6
-        frame.zero_()
+    wl = WORKLOADS["c4"]
+    w, h, spp = wl["w"], wl["h"], wl["spp"]
+    dae, envmap, cam = workload_scene(wl)
+    sc = Scene.from_dae(dae, w, h, cam_info=cam, envmap=envmap)
+    dev = Device(local)
+    dev.upload_scene(sc)
+    dev.set_camera(sc.camera)
+    dev.set_params(w, h, spp, DEPTH, NSL, SEED)
+    frame = torch.zeros((h, w, 3), dtype=torch.float32, device=f"cuda:{local}")
+    tiles = tile_fifo(w, h)
+    pex = PipelinedExchange(tiles, w, h, rank, world, frame.device)
+    mine = np.asarray(pex.mine, dtype=np.int32).reshape(-1, 4)
+    guard = StepGuard()
+    kf = [0]
 
-        def step(timed=False):
-            guard.run(dev.render_tiles_device, mine, ex.packed.data_ptr(), stream, packed=True,
-                      out_floats=ex.packed.numel())
-            e0 = torch.cuda.Event(enable_timing=True)
-            e0.record()
-            ex.exchange(frame)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record()
-            if timed:
-                xev.append((e0, e1))
+    def step(timed=False, stats=False):
+        k = kf[0]
+        kf[0] += 1
+        buf = pex.packed_for(k)
+        guard.run(dev.render_tiles_device, mine, buf.data_ptr(), stream, packed=True, out_floats=buf.numel(),
+                  stats=stats)
+        pex.exchange(k, frame, timed=timed)
 
-        for _ in range(warmup):
-            step()
-        guard.check()
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(frames):
-            step(timed=True)
-        dist.barrier()
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-        guard.check()
-        t = torch.tensor([el], dtype=torch.float64, device="cpu" if backend == "gloo" else f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-        # the efficiency inputs of the tile-sharded curve: each rank's render
-        # (HIP events) and gather times, its pixels and group-sum bytes
-        k_ms, _ = dev.launch_times(frames)
-        dev.render_tiles_device(mine, ex.packed.data_ptr(), stream, stats=True, packed=True,
-                                out_floats=ex.packed.numel())
-        st = dev.stats()
-        mine_v = torch.tensor([float(np.mean(k_ms)), float(np.mean([a.elapsed_time(b) for a, b in xev])),
-                               float(np.sum(mine[:, 2] * mine[:, 3])), float(st["partial_bytes"])],
-                              dtype=torch.float64, device="cpu" if backend == "gloo" else f"cuda:{local}")
-        allr = [torch.zeros_like(mine_v) for _ in range(world)]
-        dist.all_gather(allr, mine_v)
-        ranks = [[round(float(v), 4) for v in r.cpu().tolist()] for r in allr]
-        kms = [r[0] for r in ranks]
-        res[f"{name}_strong"] = {
-            "workload": wl["desc"] + f", one frame's tiles over {world} GPUs + one gather (strong)",
-            "value": round(w * h * spp * frames / el / 1e6, 1), "unit": "Mrays/s",
-            "single_gpu_value": round(rate1, 1),
-            "efficiency": round(w * h * spp * frames / el / 1e6 / (world * rate1), 4),
-            "ms_per_frame": round(el / frames * 1e3, 3), "frames": frames, "scaling": "strong",
-            "gather_bytes_per_rank": int(ex.packed.numel() * 4),
-            "kernel_ms_slowest_over_mean": round(max(kms) / max(1e-9, float(np.mean(kms))), 4),
-            "per_rank": {"fields": ["kernel_ms", "gather_ms", "pixels", "partial_bytes"], "ranks": ranks},
-            "image_mean": float(frame.mean().item()) if rank == 0 else None}
-        dev.close()
-        del frame, ex
+    for _ in range(warmup):
+        step()
+    guard.check()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        step(timed=True)
+    pex.drain()
+    dist.barrier()
+    torch.cuda.synchronize()
+    el = timed_max(time.perf_counter() - t0, backend, local)
+    guard.check()
+    k_ms, _ = dev.launch_times(frames)
+    step(stats=True)
+    st = dev.stats()
+    rate1, shared = single_gpu_rate(dev, tiles, w, h, spp, frame, stream, rank, backend, frames)
+    mine_v = torch.tensor([float(np.mean(k_ms)), pex.exchange_ms(), float(np.sum(mine[:, 2] * mine[:, 3])),
+                           float(st["partial_bytes"])],
+                          dtype=torch.float64, device="cpu" if backend == "gloo" else f"cuda:{local}")
+    allr = [torch.zeros_like(mine_v) for _ in range(world)]
+    dist.all_gather(allr, mine_v)
+    ranks = [[round(float(v), 4) for v in r.cpu().tolist()] for r in allr]
+    kms = [r[0] for r in ranks]
+    value = w * h * spp * frames / el / 1e6
+    res["c4_strong"] = {
+        "workload": wl["desc"] + f", one frame's tiles over {world} GPUs + one pipelined gather (strong)",
+        "value": round(value, 1), "unit": "Mrays/s", "single_gpu_value": round(rate1, 1),
+        "efficiency": None if shared else round(value / (world * rate1), 4), "shared_device": shared,
+        "ms_per_frame": round(el / frames * 1e3, 3), "frames": frames, "scaling": "strong",
+        "gather_bytes_per_rank": int(pex.ex.packed.numel() * 4),
+        "kernel_ms_slowest_over_mean": round(max(kms) / max(1e-9, float(np.mean(kms))), 4),
+        "per_rank": {"fields": ["kernel_ms", "exchange_ms", "pixels", "partial_bytes"], "ranks": ranks},
+        "image_mean": float(frame.mean().item()) if rank == 0 else None}
+    dev.close()
+    del frame, pex
+    if with_weak:
+        res["c3_weak"] = weak_companion(local, rank, world, backend, StepGuard, frames, warmup)
     return res
+
+
+def weak_companion(local, rank, world, backend, StepGuard, frames, warmup=2):
+    """c3_weak (see multi_gpu_companions)."""
+    import torch
+    import torch.distributed as dist
+
+    from dsgpuraytracing_amd.pathtracer import Device, Scene, tile_fifo
+    wl = WORKLOADS["c3"]
+    w, h, spp = wl["w"], wl["h"], wl["spp"]
+    dae, envmap, cam = workload_scene(wl)
+    sc = Scene.from_dae(dae, w, h, cam_info=cam, envmap=envmap)
+    dev = Device(local)
+    dev.upload_scene(sc)
+    dev.set_camera(sc.camera)
+    dev.set_params(w, h, spp, DEPTH, NSL, SEED, sample_base=spp * rank)
+    stream = torch.cuda.current_stream().cuda_stream
+    frame = torch.zeros((h, w, 3), dtype=torch.float32, device=f"cuda:{local}")
+    whole = np.asarray(tile_fifo(w, h), dtype=np.int32).reshape(-1, 4)
+    guard = StepGuard()
+    guard.run(dev.render_tiles_device, whole, frame.data_ptr(), stream, stats=True)
+    st = guard.run(dev.stats)
+    guard.check()
+    # rows outside the screen footprint are 0 in every pass: the reduce carries the footprint's rows only
+    y0, y1 = st["footprint"][1], st["footprint"][3]
+    rows = frame[y0:y1 + 1] if y1 >= y0 else frame[:0]
+    xev = []
+
+    def step(timed=False):
+        guard.run(dev.render_tiles_device, whole, frame.data_ptr(), stream)
+        if rows.numel() == 0:
+            return
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        if backend == "gloo":  # host staging (one-GPU rehearsals)
+            hb = rows.cpu()
+            dist.reduce(hb, dst=0)
+            if rank == 0:
+                rows.copy_(hb)
+        else:
+            dist.reduce(rows, dst=0)
+        if rank == 0:
+            rows.mul_(1.0 / world)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        if timed:
+            xev.append((e0, e1))
+
+    for _ in range(warmup):
+        step()
+    guard.check()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        step(timed=True)
+    dist.barrier()
+    torch.cuda.synchronize()
+    el = timed_max(time.perf_counter() - t0, backend, local)
+    guard.check()
+    out = {"workload": wl["desc"] + f", one 64-spp pass per GPU over disjoint sample indices + one RCCL reduce "
+                                    f"(a {spp * world}-spp image; weak)",
+           "value": round(world * w * h * spp * frames / el / 1e6, 1), "unit": "Mrays/s",
+           "ms_per_frame": round(el / frames * 1e3, 3), "frames": frames, "scaling": "weak",
+           "reduce_bytes_per_rank": int(rows.numel() * 4),
+           "reduce_ms": round(float(np.mean([a.elapsed_time(b) for a, b in xev])), 4) if xev else 0.0,
+           "image_mean": float(frame.mean().item()) if rank == 0 else None}
+    dev.close()
+    return out
 
 
 def bvh_desc(lbvh=False):

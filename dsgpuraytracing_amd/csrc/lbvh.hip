@@ -627,212 +627,6 @@ __global__ void k_gather(Params P, const float* __restrict__ norms_in, DPrim* pr
   prim_map[i] = s;
 }
 
-// ---- 8-wide render tree (DNode8, round 5) from a binary tree in DNode2 form.
-// Both render-tree sources feed it: the GPU tree's binary nodes (k_emit_bin,
-// leaf cursors already in the final primitive order) and the host trees'
-// (pt_api.cpp build_host_bvh).  One level per launch, top-down: an item opens
-// the largest-area internal child until eight children (as the BVH4 collapse),
-// allocates its internal children as one contiguous block after itself
-// (references only point forward) and writes the quantised node.
-
-struct WItem {
-  int bin;    // binary node
-  int idx;    // its 8-wide node
-  int stack;  // worst-case stack entries on entering it
-};
-
-__device__ __forceinline__ void bin_kid(const DNode2& b, int side, float lo[3], float hi[3], int& ref) {
-  if (side == 0) {
-    lo[0] = b.a.x; hi[0] = b.a.y; lo[1] = b.a.z; hi[1] = b.a.w; lo[2] = b.c.x; hi[2] = b.c.y;
-    ref = b.e.x;
-  } else {
-    lo[0] = b.b.x; hi[0] = b.b.y; lo[1] = b.b.z; hi[1] = b.b.w; lo[2] = b.c.z; hi[2] = b.c.w;
-    ref = b.e.y;
-  }
-}
-
-// fp16 bits of x >= 0 rounded down (up = false) or up: the nearest half, then
-// stepped (non-negative halves order like their bits) until it is on x's side.
-__device__ uint16_t half_dir(double x, bool up) {
-  const _Float16 h0 = (_Float16)(float)x;
-  uint16_t b = __builtin_bit_cast(uint16_t, h0);
-  auto val = [](uint16_t u) { return (double)(float)__builtin_bit_cast(_Float16, u); };
-  if (up) {
-    while (val(b) < x) ++b;
-  } else {
-    while (b > 0 && val(b) > x) --b;
-  }
-  return b;
-}
-
-// Quantises the nk child boxes (float, already rounded outward) into d / h.
-__device__ void encode8(const float (*lo)[3], const float (*hi)[3], const int* ref, int nk, DNode8& d, int4& h) {
-  bool empty[8];
-  float org[3] = {INFINITY, INFINITY, INFINITY};
-  for (int k = 0; k < 8; ++k) {
-    bool e = k >= nk;
-    for (int a = 0; a < 3 && !e; ++a) e = !(lo[k][a] <= hi[k][a]) || !isfinite(lo[k][a]) || !isfinite(hi[k][a]);
-    empty[k] = e;
-    if (!e)
-      for (int a = 0; a < 3; ++a) org[a] = fminf(org[a], lo[k][a]);
-  }
-  for (int a = 0; a < 3; ++a)
-    if (!isfinite(org[a])) org[a] = 0.0f;
-  int ex[3];
-  for (int a = 0; a < 3; ++a) {
-    double ext = 0.0;
-    for (int k = 0; k < 8; ++k)
-      if (!empty[k]) ext = fmax(ext, (double)hi[k][a] - (double)org[a]);
-    int e = 0;
-    if (ext > 0.0) {
-      int k2;
-      frexp(ext, &k2);  // ext <= 2^k2
-      e = min(127, max(-128, k2 - 15));  // quantised offsets <= 2^15 < 65504
-    }
-    ex[a] = e;
-  }
-  uint16_t q[6][8];
-  for (int k = 0; k < 8; ++k)
-    for (int a = 0; a < 3; ++a) {
-      if (empty[k]) {
-        q[2 * a][k] = 0x7c00u;      // lo = +inf
-        q[2 * a + 1][k] = 0xfc00u;  // hi = -inf
-      } else {
-        q[2 * a][k] = half_dir(ldexp((double)lo[k][a] - (double)org[a], -ex[a]), false);
-        q[2 * a + 1][k] = half_dir(ldexp((double)hi[k][a] - (double)org[a], -ex[a]), true);
-      }
-    }
-  d.ox = org[0];
-  d.oy = org[1];
-  d.oz = org[2];
-  d.ex = (uint32_t)(ex[0] & 0xff) | ((uint32_t)(ex[1] & 0xff) << 8) | ((uint32_t)(ex[2] & 0xff) << 16);
-  uint4* planes[6] = {&d.lox, &d.hix, &d.loy, &d.hiy, &d.loz, &d.hiz};
-  for (int p = 0; p < 6; ++p)
-    *planes[p] = make_uint4(q[p][0] | ((uint32_t)q[p][1] << 16), q[p][2] | ((uint32_t)q[p][3] << 16),
-                            q[p][4] | ((uint32_t)q[p][5] << 16), q[p][6] | ((uint32_t)q[p][7] << 16));
-  int r[8];
-  for (int k = 0; k < 8; ++k) r[k] = empty[k] ? cursor(0, 1) : ref[k];
-  d.ref = make_int4(r[0], r[1], r[2], r[3]);
-  h = make_int4(r[4], r[5], r[6], r[7]);
-}
-
-// Compressed 4-wide node from a DNode: the same quantisation as encode8 over
-// four children (empty slots -- boxes at +inf -- become lo = +inf / hi = -inf
-// halves, never entered).
-__global__ void k_compress4(const DNode* __restrict__ in, int n, DNodeC* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const DNode d = in[i];
-  const float* pl[6] = {&d.lox.x, &d.hix.x, &d.loy.x, &d.hiy.x, &d.loz.x, &d.hiz.x};
-  float lo[4][3], hi[4][3];
-  bool empty[4];
-  float org[3] = {INFINITY, INFINITY, INFINITY};
-  for (int k = 0; k < 4; ++k) {
-    bool e = false;
-    for (int a = 0; a < 3; ++a) {
-      lo[k][a] = pl[2 * a][k];
-      hi[k][a] = pl[2 * a + 1][k];
-      e = e || !(lo[k][a] <= hi[k][a]) || !isfinite(lo[k][a]) || !isfinite(hi[k][a]);
-    }
-    empty[k] = e;
-    if (!e)
-      for (int a = 0; a < 3; ++a) org[a] = fminf(org[a], lo[k][a]);
-  }
-  for (int a = 0; a < 3; ++a)
-    if (!isfinite(org[a])) org[a] = 0.0f;
-  int ex[3];
-  for (int a = 0; a < 3; ++a) {
-    double ext = 0.0;
-    for (int k = 0; k < 4; ++k)
-      if (!empty[k]) ext = fmax(ext, (double)hi[k][a] - (double)org[a]);
-    int e = 0;
-    if (ext > 0.0) {
-      int k2;
-      frexp(ext, &k2);  // ext <= 2^k2
-      e = min(127, max(-128, k2 - 15));  // quantised offsets <= 2^15 < 65504
-    }
-    ex[a] = e;
-  }
-  uint32_t w[3][4];
-  for (int a = 0; a < 3; ++a) {
-    uint16_t ql[4], qh[4];
-    for (int k = 0; k < 4; ++k) {
-      if (empty[k]) {
-        ql[k] = 0x7c00u;  // lo = +inf
-        qh[k] = 0xfc00u;  // hi = -inf
-      } else {
-        ql[k] = half_dir(ldexp((double)lo[k][a] - (double)org[a], -ex[a]), false);
-        qh[k] = half_dir(ldexp((double)hi[k][a] - (double)org[a], -ex[a]), true);
-      }
-    }
-    w[a][0] = ql[0] | ((uint32_t)ql[1] << 16);
-    w[a][1] = ql[2] | ((uint32_t)ql[3] << 16);
-    w[a][2] = qh[0] | ((uint32_t)qh[1] << 16);
-    w[a][3] = qh[2] | ((uint32_t)qh[3] << 16);
-  }
-  DNodeC c;
-  c.ox = org[0];
-  c.oy = org[1];
-  c.oz = org[2];
-  c.ex = (uint32_t)(ex[0] & 0xff) | ((uint32_t)(ex[1] & 0xff) << 8) | ((uint32_t)(ex[2] & 0xff) << 16);
-  c.x = make_uint4(w[0][0], w[0][1], w[0][2], w[0][3]);
-  c.y = make_uint4(w[1][0], w[1][1], w[1][2], w[1][3]);
-  c.z = make_uint4(w[2][0], w[2][1], w[2][2], w[2][3]);
-  c.ref = d.ref;
-  out[i] = c;
-}
-
-__global__ void k_wide(const DNode2* __restrict__ bin, const WItem* __restrict__ in, int n_in, WItem* out,
-                       int* n_out, int* n_nodes, int* max_stack, DNode8* nodes, int4* hi4) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_in) return;
-  const WItem it = in[t];
-  float klo[8][3], khi[8][3];
-  int kref[8];
-  int nk = 2;
-  {
-    const DNode2 b = bin[it.bin];
-    bin_kid(b, 0, klo[0], khi[0], kref[0]);
-    bin_kid(b, 1, klo[1], khi[1], kref[1]);
-  }
-  while (nk < 8) {
-    int best = -1;
-    float ba = -1.0f;
-    for (int k = 0; k < nk; ++k)
-      if (kref[k] >= 0) {
-        const float a = half_area(klo[k], khi[k]);
-        if (a > ba) {
-          ba = a;
-          best = k;
-        }
-      }
-    if (best < 0) break;
-    const DNode2 b = bin[kref[best]];
-    bin_kid(b, 0, klo[best], khi[best], kref[best]);
-    bin_kid(b, 1, klo[nk], khi[nk], kref[nk]);
-    ++nk;
-  }
-  const int below = it.stack + nk - 1;
-  atomicMax(max_stack, below);
-  int ni = 0;
-  for (int k = 0; k < nk; ++k) ni += kref[k] >= 0;
-  if (ni > 0) {
-    const int base = atomicAdd(n_nodes, ni), obase = atomicAdd(n_out, ni);
-    int j = 0;
-    for (int k = 0; k < nk; ++k)
-      if (kref[k] >= 0) {
-        out[obase + j] = WItem{kref[k], base + j, below};
-        kref[k] = base + j;
-        ++j;
-      }
-  }
-  DNode8 d;
-  int4 h;
-  encode8(klo, khi, kref, nk, d, h);
-  nodes[it.idx] = d;
-  hi4[it.idx] = h;
-}
-
 }  // namespace lbvh
 
 #define LB_CHK(x)                   \
@@ -840,49 +634,6 @@ __global__ void k_wide(const DNode2* __restrict__ bin, const WItem* __restrict__
     hipError_t e_ = (x);            \
     if (e_ != hipSuccess) return e_; \
   } while (0)
-
-extern "C" hipError_t ptk_compress4(const DNode* in, int n, DNodeC* out, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(lbvh::k_compress4, dim3((n + 127) / 128), dim3(128), 0, s, in, n, out);
-  return hipGetLastError();
-}
-
-extern "C" hipError_t ptk_build_wide(const DNode2* bin, int n_bin, WideOut* out, hipStream_t s) {
-  using namespace lbvh;
-  *out = WideOut{};
-  const int cap = std::max(1, n_bin);  // an 8-wide node per binary internal node at most
-  LB_CHK(hipMalloc(&out->nodes, (size_t)cap * sizeof(DNode8)));
-  LB_CHK(hipMalloc(&out->hi, (size_t)cap * sizeof(int4)));
-  WItem *fa = nullptr, *fb = nullptr;
-  int* counters = nullptr;  // n_nodes, n_out, max_stack
-  LB_CHK(hipMalloc(&fa, (size_t)cap * sizeof(WItem)));
-  LB_CHK(hipMalloc(&fb, (size_t)cap * sizeof(WItem)));
-  LB_CHK(hipMalloc(&counters, 16));
-  const WItem root{0, 0, 0};
-  const int init[3] = {1, 0, 0};
-  LB_CHK(hipMemcpyAsync(fa, &root, sizeof(root), hipMemcpyHostToDevice, s));
-  LB_CHK(hipMemcpyAsync(counters, init, sizeof(init), hipMemcpyHostToDevice, s));
-  int n_in = 1;
-  const int B = 128;
-  while (n_in > 0) {  // one launch per level
-    LB_CHK(hipMemsetAsync(counters + 1, 0, 4, s));
-    hipLaunchKernelGGL(k_wide, dim3((n_in + B - 1) / B), dim3(B), 0, s, bin, fa, n_in, fb, counters + 1, counters,
-                       counters + 2, out->nodes, out->hi);
-    LB_CHK(hipGetLastError());
-    LB_CHK(hipMemcpyAsync(&n_in, counters + 1, 4, hipMemcpyDeviceToHost, s));
-    LB_CHK(hipStreamSynchronize(s));
-    std::swap(fa, fb);
-  }
-  int cnt[3] = {0, 0, 0};
-  LB_CHK(hipMemcpyAsync(cnt, counters, 12, hipMemcpyDeviceToHost, s));
-  LB_CHK(hipStreamSynchronize(s));
-  out->n = cnt[0];
-  out->max_stack = cnt[2];
-  (void)hipFree(fa);
-  (void)hipFree(fb);
-  (void)hipFree(counters);
-  return hipSuccess;
-}
 
 extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t s) {
   using namespace lbvh;

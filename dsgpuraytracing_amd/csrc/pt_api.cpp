@@ -163,15 +163,11 @@ struct pt_ctx {
   // triples so device renders need not synchronise (pt_get_launch_times)
   static constexpr int kRing = 256;
   hipEvent_t ev[kRing][3] = {};
-  hipEvent_t ev_call[kRing] = {};  // (PT_RESOLVE_ON_RS) the caller's stream at the launch's start
   int64_t n_launches = 0;   // launches recorded so far (ring slot = index % kRing)
   bool census_valid = false;  // the last launch was a PT_CENSUS plain launch (its trace area holds start/end/CU)
   bool times_pending = false;  // c->last's times belong to a launch not yet synchronised
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;  // the current launch's triple
-  DevBuf<DNode> nodes;    // the render tree, PT_NODE_WIDTH 4
-  DevBuf<DNode8> nodes8;  // the render tree, PT_NODE_WIDTH 8 (+ children 4..7's references)
-  DevBuf<int4> nodes8_hi;
-  DevBuf<DNodeC> nodesc;  // the render tree, PT_NODE_COMPRESS (the compressed copy of nodes)
+  DevBuf<DNode> nodes;    // the render tree (BVH4)
   DevBuf<DNode2> nodes2;  // binary tree for PT_FLAG_REF_COUNTS
   DevBuf<int> prim_map;   // own BVH order (SAH or GPU-built) -> uploaded primitive index (else empty)
   // primitives in the caller's (reference BVH) order, for the reference-count
@@ -283,11 +279,10 @@ int pt_create(int device, pt_ctx** out) {
     HIPCHK(hipStreamCreateWithFlags(&c->rstream[k], hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
     HIPCHK(hipEventRecord(c->ev_free[k], c->stream));
-    HIPCHK(c->counter[k].reserve(PT_QUEUE_WORDS * (PT_QUEUE_HEADS + 1)));  // work-queue heads (+ the tail head), one 128-B line each
+    HIPCHK(c->counter[k].reserve(PT_QUEUE_WORDS * PT_QUEUE_HEADS));  // work-queue heads, one 128-B line each
   }
   for (auto& tri : c->ev)
     for (auto& e : tri) HIPCHK(hipEventCreate(&e));
-  for (auto& e : c->ev_call) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIPCHK(c->stats.reserve(PT_STATS_SLOTS));
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, device));
@@ -318,9 +313,6 @@ int pt_destroy(pt_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();  // no render of this context may still be running
   c->nodes.release();
-  c->nodes8.release();
-  c->nodes8_hi.release();
-  c->nodesc.release();
   c->nodes2.release();
   c->prim_map.release();
   c->env_tex.release();
@@ -352,8 +344,6 @@ int pt_destroy(pt_ctx* c) {
   for (auto& tri : c->ev)
     for (auto& e : tri)
       if (e) (void)hipEventDestroy(e);
-  for (auto& e : c->ev_call)
-    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return PT_OK;
@@ -691,19 +681,6 @@ static int build_host_bvh(const pt_scene* s, std::vector<DNode>& dn, std::vector
   return PT_OK;
 }
 
-// The 8-wide render tree from a binary tree already on the device
-// (ptk_build_wide): replaces c->nodes8 / c->nodes8_hi; the worst-case
-// traversal stack goes to *max_stack.
-static int build_wide(pt_ctx* c, const DNode2* bin_dev, int n_bin, int* max_stack) {
-  WideOut w{};
-  HIPCHK(ptk_build_wide(bin_dev, n_bin, &w, c->stream));
-  c->nodes8.adopt(w.nodes, (size_t)std::max(1, w.n));
-  c->nodes8_hi.adopt(w.hi, (size_t)std::max(1, w.n));
-  c->n_render_nodes = (size_t)w.n;
-  *max_stack = w.max_stack;
-  return PT_OK;
-}
-
 // GPU linear-BVH build over the primitives already in c->prims / c->norms
 // (CUDAPathTracer::buildBVH, cuda_src/setup.cu:478-686; kernels in lbvh.hip).
 static int build_gpu_bvh(pt_ctx* c, const pt_scene* s) {
@@ -736,11 +713,6 @@ static int build_gpu_bvh(pt_ctx* c, const pt_scene* s) {
   c->nodes.adopt(out.nodes4, (size_t)out.n4);
   c->nodes2.adopt(out.nodes2, (size_t)std::max(1, out.n2));
   c->n_render_nodes = (size_t)out.n4;
-#if PT_NODE_WIDTH == 8
-  // (the BVH4 emission still numbers the primitives in depth-first leaf order,
-  // which the binary nodes' leaf cursors refer to)
-  if (int rc = build_wide(c, out.nodes2, std::max(1, out.n2), &out.max_stack)) return rc;
-#endif
   if (out.max_stack > PT_STACK_MAX)
     return fail(PT_E_INVALID, "pt_upload_scene_lbvh: BVH needs a deeper traversal stack (" +
                                   std::to_string(out.max_stack) + " > " + std::to_string(PT_STACK_MAX) + ")");
@@ -931,19 +903,6 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
     int max_stack = 0;
     int rc = build_host_bvh(s, dn, d2, max_stack);
     if (rc) return rc;
-#if PT_NODE_WIDTH == 8
-    {  // the 8-wide render tree from the host tree's binary nodes, collapsed on the device
-      DevBuf<DNode2> bin;
-      HIPCHK(bin.reserve(d2.size()));
-      HIPCHK(hipMemcpy(bin.p, d2.data(), d2.size() * sizeof(DNode2), hipMemcpyHostToDevice));
-      rc = build_wide(c, bin.p, (int)d2.size(), &max_stack);
-      bin.release();
-      if (rc) return rc;
-      if (max_stack > PT_STACK_MAX)
-        return fail(PT_E_INVALID, "pt_upload_scene: BVH needs a deeper traversal stack (" + std::to_string(max_stack) +
-                                      " > " + std::to_string(PT_STACK_MAX) + ")");
-    }
-#endif
     if (s != s0) {  // the reference-count launch walks the caller's (reference) tree
       std::vector<DNode> dn0;
       int ms0 = 0;
@@ -961,9 +920,7 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
       HIPCHK(hipMemcpy(c->prim_map.p, pm.data(), pm.size() * sizeof(int), hipMemcpyHostToDevice));
     }
     c->bvh_stack = max_stack;
-#if PT_NODE_WIDTH == 4
     c->n_render_nodes = dn.size();
-#endif
     const pt_bvh_node* N = s->nodes;
     for (int k = 0; k < 3; ++k) {
       c->root_lo[k] = round_down(N[0].bb_min[k]);
@@ -975,14 +932,6 @@ static int upload_impl(pt_ctx* c, const pt_scene* s, bool gpu_bvh) {
     int rc = build_gpu_bvh(c, s);
     if (rc) return rc;
   }
-#if PT_NODE_COMPRESS
-  // the render tree as compressed nodes (host or GPU tree alike), node for node
-  if (c->n_render_nodes >= (size_t)1 << 24)  // (the node step addresses nodes with a 24-bit multiply)
-    return fail(PT_E_INVALID, "pt_upload_scene: compressed render tree limited to 2^24 nodes");
-  HIPCHK(c->nodesc.reserve(std::max<size_t>(1, c->n_render_nodes)));
-  HIPCHK(ptk_compress4(c->nodes.p, (int)c->n_render_nodes, c->nodesc.p, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-#endif
   HIPCHK(hipMemcpy(c->bsdfs.p, bs.data(), bs.size() * sizeof(DBsdf), hipMemcpyHostToDevice));
   if (!ls.empty()) HIPCHK(hipMemcpy(c->lights.p, ls.data(), ls.size() * sizeof(DLight), hipMemcpyHostToDevice));
   c->env_w = n_env ? s->env_width : 0;
@@ -1158,7 +1107,7 @@ static int group_size(int64_t traced, bool env, int spp, int64_t lanes, int64_t 
     // slot, for the whole frame's blocks (so every tile split gets the same
     // layout)
     const int64_t slots = frame_blocks * 64 * ((spp + gs - 1) / gs);
-    if ((slots + 2 * budget_waves * PT_CHUNK_MAX < (int64_t)INT32_MAX && slots * 4 * PT_SUM_WORDS <= ((int64_t)PT_GROUP_SUM_GIB << 30)) ||
+    if ((slots + 2 * budget_waves * PT_CHUNK_MAX < (int64_t)INT32_MAX && slots * PT_SUM_BYTES <= ((int64_t)PT_GROUP_SUM_GIB << 30)) ||
         gs >= spp)
       break;
     gs = std::min(spp, gs * 2);
@@ -1167,8 +1116,9 @@ static int group_size(int64_t traced, bool env, int spp, int64_t lanes, int64_t 
 }
 
 // One render: the render kernel on the slot's render stream, then the resolve
-// (on the same stream, PT_RESOLVE_ON_RS; else on the caller's stream `s`),
-// the caller's stream `s` ordered after it (see pt_ctx: the render pipeline).
+// on the caller's stream `s`, ordered after the render (see pt_ctx: the render
+// pipeline).  (The resolve on the render stream instead measured one frame
+// +0.03 ms: profiles/r5/ab_resolve_reset_stream.txt.)
 static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStream_t s, uint32_t flags) {
   const bool stats = (flags & (PT_FLAG_STATS | PT_FLAG_REF_COUNTS)) != 0;
   std::memset(&c->last, 0, sizeof(c->last));
@@ -1183,11 +1133,20 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   // A launch that finds every slot's last resolve complete has no frame to
   // overlap with: it runs on the caller's stream, with no cross-stream waits
   // in front of the render or between the render and the resolve (a lone
-  // frame's wall clock, PT_IDLE_DIRECT; the slots still alternate).
+  // frame's wall clock; the slots still alternate).  Only hipErrorNotReady
+  // means busy: any other result is a fault of an earlier render, reported
+  // here instead of being absorbed into the choice.
   bool gpu_idle = true;  // no earlier render of this context still running or queued
-  for (int k = 0; k < pt_ctx::kSlots && gpu_idle; ++k) gpu_idle = hipEventQuery(c->ev_free[k]) == hipSuccess;
-  (void)hipGetLastError();  // a not-ready query is no error of this launch
-  const bool idle = PT_IDLE_DIRECT && pipeline && !census_launch && gpu_idle;
+  for (int k = 0; k < pt_ctx::kSlots && gpu_idle; ++k) {
+    const hipError_t q = hipEventQuery(c->ev_free[k]);
+    if (q == hipErrorNotReady) {
+      (void)hipGetLastError();  // (a not-ready query is no error of this launch)
+      gpu_idle = false;
+    } else if (q != hipSuccess) {
+      return fail(PT_E_HIP, std::string("render: an earlier launch failed: ") + hipGetErrorString(q));
+    }
+  }
+  const bool idle = pipeline && !census_launch && gpu_idle;
   hipStream_t rs = pipeline && !census_launch && !idle ? c->rstream[slot] : s;
   // the slot's device state is free once the previous resolve that read it ran
   if (!idle) HIPCHK(hipStreamWaitEvent(rs, c->ev_free[slot], 0));
@@ -1198,12 +1157,11 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     HIPCHK(c->tiles[slot].reserve(tl.size()));
     HIPCHK(hipMemcpyAsync(c->tiles[slot].p, th.data(), th.size() * sizeof(int4), hipMemcpyHostToDevice, rs));
   }
-  // Queue heads: zeroed by the slot's previous resolve (PT_RESOLVE_RESETS: a
-  // memset in front of the render is a dependent launch of its own, ~20 us
+  // Queue heads: zeroed by the slot's previous resolve (a memset in front of the render is a dependent launch of its own, ~20 us
   // before the render kernel starts on a lone frame); a memset only when
   // that did not happen (first use, a launch that failed half-way)
   if (!c->counter_clean[slot])
-    HIPCHK(hipMemsetAsync(c->counter[slot].p, 0, PT_QUEUE_WORDS * (PT_QUEUE_HEADS + 1) * sizeof(uint32_t), rs));
+    HIPCHK(hipMemsetAsync(c->counter[slot].p, 0, PT_QUEUE_WORDS * PT_QUEUE_HEADS * sizeof(uint32_t), rs));
   c->counter_clean[slot] = false;
   if (stats) {
     unsigned long long init[PT_STATS_SLOTS] = {0};
@@ -1235,9 +1193,6 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.n_bsdfs = c->n_bsdfs;
   P.n_tiles = (int)tl.size();
   P.nodes = c->nodes.p;
-  P.nodes8 = c->nodes8.p;
-  P.nodes8_hi = c->nodes8_hi.p;
-  P.nodesc = c->nodesc.p;
   P.nodes2 = c->nodes2.p;
   P.prims = c->prims.p;
   P.norms = c->norms.p;
@@ -1284,7 +1239,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   // triangle-only scenes take the render kernel without the sphere test
   // (branch-free leaf steps); PT_NO_TRI_ONLY forces the mixed one (A/B, tests)
   P.tri_only = c->tri_only && !std::getenv("PT_NO_TRI_ONLY") ? 1 : 0;
-  // drain helpers (PT_HELPERS); PT_NO_HELPERS turns them off (A/B, tests)
+  // drain helpers; PT_NO_HELPERS turns them off (A/B, tests)
   P.helpers = std::getenv("PT_NO_HELPERS") ? 0 : 1;
   P.drain_div = 0;
   if (const char* dd = std::getenv("PT_DRAIN_DIV")) {  // tuning knob
@@ -1360,14 +1315,14 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   // queue claims: bigger for frames with many slots per lane (fewer atomics
   // on the heads; a lone small frame's drain prefers the smaller claim)
   // and for a frame queued behind another in the render pipeline
-  // (PT_CHUNK_BUSY): its drain overlaps the previous frame's -- the
+  // (profiles/r5/ab_chunk_busy.txt): its drain overlaps the previous frame's -- the
   // throughput case -- while a frame launched on an idle GPU, or with the
   // pipeline off (PT_PIPELINE=0: no two launches overlap), is the latency
   // case, whose end the smaller claim shortens
   // (C3: 256-slot claims +2.9% pipelined, lone launch +9%:
   // profiles/r5/ab_chunk_heads.txt).  A claim size never changes a value.
   const bool big_frame = slots >= (int64_t)PT_CHUNK_BIG_SLOTS * want_plain * PT_BLOCK;
-  P.chunk = big_frame || (PT_CHUNK_BUSY && pipeline && !census_launch && !gpu_idle)
+  P.chunk = big_frame || (pipeline && !census_launch && !gpu_idle)
                 ? PT_CHUNK_MAX
                 : PT_CHUNK;
   // large frames claim PT_CHUNK_BIG (512) where the slot indices and the
@@ -1391,9 +1346,9 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.sblocks = (64 * P.n_groups) % P.chunk == 0 ? 1 : 0;  // every (aligned) chunk inside one block
   // group sums: 12 B per work slot of THIS launch (a rank's share of a split
   // frame holds only its own blocks' sums)
-  HIPCHK(c->partial[slot].reserve((size_t)std::max<int64_t>(slots, 1) * PT_SUM_WORDS));
+  HIPCHK(c->partial[slot].reserve((size_t)std::max<int64_t>(slots, 1) * 3));
   P.partial = c->partial[slot].p;
-  c->last.partial_bytes = slots * 4 * PT_SUM_WORDS;
+  c->last.partial_bytes = slots * PT_SUM_BYTES;
   auto log2_exact = [](int v) {  // log2(v) for a power of two, else -1
     int k = 0;
     while ((1 << k) < v && k < 30) ++k;
@@ -1405,26 +1360,6 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   if ((stats || P.census) && (size_t)grid * PT_WAVE_TRACE + PT_STATS_SLOTS > c->stats.n)
     grid = (int)((c->stats.n - PT_STATS_SLOTS) / PT_WAVE_TRACE);
   grid = std::max(1, grid);
-  // Tail claims (PT_TAIL_CLAIMS): the frame's last PT_TAIL_SLOTS slots per
-  // resident lane are dealt 64 at a time from a second queue head, so that
-  // when the queue runs dry no wave still holds a whole claim's worth of
-  // slots the other waves could have taken.  tail_start is where the dynamic
-  // claims of P.chunk slots (after the statically dealt ones) cross into the
-  // tail; claims of 64 stay inside one block (64 * n_groups is a multiple
-  // of 64).  tail_start >= slots: no tail.
-  P.tail_start = (uint32_t)slots;
-#if PT_TAIL_CLAIMS
-  {
-    int tail_lanes = PT_TAIL_SLOTS;
-    if (const char* t = std::getenv("PT_TAIL_SLOTS")) tail_lanes = std::max(0, std::atoi(t));  // tuning knob (0: off)
-    const int64_t first = (int64_t)grid * P.chunk;  // statically dealt chunks
-    const int64_t tail = (int64_t)grid * 64 * tail_lanes;
-    if (tail > 0 && P.chunk > 64 && slots > first) {
-      const int64_t k = std::max<int64_t>(0, (slots - tail - first) / P.chunk);
-      P.tail_start = (uint32_t)std::min<int64_t>(slots, first + k * P.chunk);
-    }
-  }
-#endif
   if (P.census)  // (a build without -DPT_CENSUS=1 leaves the drain fields 0)
     HIPCHK(hipMemsetAsync(c->stats.p + PT_STATS_SLOTS, 0, (size_t)grid * PT_WAVE_TRACE * 8, rs));
   P.stack_spill = nullptr;
@@ -1439,35 +1374,14 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     c->ev2 = tri[2];
     ++c->n_launches;
   }
-#if PT_RESOLVE_ON_RS
-  // The resolve follows the render on the render stream (a same-queue
-  // dependency: ~6 us from the render's end to the resolve's start on a lone
-  // frame, against ~13 us through a cross-stream event), ordered after the
-  // caller's earlier work on `s` (it writes the caller's buffer) by an event
-  // recorded there now -- long complete when the render ends -- and the
-  // caller's stream then waits for the resolve: everything the caller can
-  // observe on `s` keeps its order.
-  hipEvent_t ev_call = c->ev_call[(c->n_launches - 1) % pt_ctx::kRing];
-  if (rs != s) HIPCHK(hipEventRecord(ev_call, s));
-  HIPCHK(hipEventRecord(c->ev0, rs));
-  HIPCHK(ptk_launch_render(&P, grid, stats, (flags & PT_FLAG_REF_COUNTS) != 0, rs));
-  HIPCHK(hipEventRecord(c->ev1, rs));
-  if (rs != s) HIPCHK(hipStreamWaitEvent(rs, ev_call, 0));
-  HIPCHK(ptk_launch_resolve(&P, rs));
-  c->counter_clean[slot] = PT_RESOLVE_RESETS != 0;
-  HIPCHK(hipEventRecord(c->ev2, rs));
-  HIPCHK(hipEventRecord(c->ev_free[slot], rs));
-  if (rs != s) HIPCHK(hipStreamWaitEvent(s, c->ev2, 0));
-#else
   HIPCHK(hipEventRecord(c->ev0, rs));
   HIPCHK(ptk_launch_render(&P, grid, stats, (flags & PT_FLAG_REF_COUNTS) != 0, rs));
   HIPCHK(hipEventRecord(c->ev1, rs));
   if (rs != s) HIPCHK(hipStreamWaitEvent(s, c->ev1, 0));  // the resolve reads the finished group sums
   HIPCHK(ptk_launch_resolve(&P, s));
-  c->counter_clean[slot] = PT_RESOLVE_RESETS != 0;
+  c->counter_clean[slot] = true;  // (the resolve zeroed the slot's queue heads)
   HIPCHK(hipEventRecord(c->ev2, s));
   HIPCHK(hipEventRecord(c->ev_free[slot], s));
-#endif
   c->census_valid = P.census != 0;
   c->last.grid_blocks = grid;
   c->last.group_spp = P.group_spp;
@@ -1829,10 +1743,7 @@ int pt_intersect(pt_ctx* c, int64_t n, const double* o, const double* d, const d
     HIPCHK(c->q_spill.reserve((size_t)(c->bvh_stack - PT_STACK) * (size_t)((n + PT_BLOCK - 1) / PT_BLOCK * PT_BLOCK)));
     spill = c->q_spill.p;
   }
-  const void* rnodes = PT_NODE_WIDTH == 8 ? (const void*)c->nodes8.p
-                       : PT_NODE_COMPRESS ? (const void*)c->nodesc.p
-                                          : (const void*)c->nodes.p;
-  HIPCHK(ptk_launch_intersect(rnodes, c->nodes8_hi.p, c->prims.p, c->q_f.p, c->q_f.p + 3 * n, c->q_f.p + 6 * n, n, dh, dt, dp, da,
+  HIPCHK(ptk_launch_intersect(c->nodes.p, c->prims.p, c->q_f.p, c->q_f.p + 3 * n, c->q_f.p + 6 * n, n, dh, dt, dp, da,
                               spill, c->prim_map.p, c->stream));
   std::vector<int32_t> ib((size_t)n * 3);
   std::vector<float> tb((size_t)n);

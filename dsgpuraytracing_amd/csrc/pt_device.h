@@ -16,9 +16,6 @@
 #ifndef PT_CHUNK_BIG
 #define PT_CHUNK_BIG 512  // the claim for large frames where it fits (pt_api.cpp launch)
 #endif
-#ifndef PT_CHUNK_BUSY
-#define PT_CHUNK_BUSY 1  // PT_CHUNK_MAX claims also for a frame launched while another is in flight (pt_api.cpp launch)
-#endif
 #ifndef PT_BANDS_TREE_MIB
 #define PT_BANDS_TREE_MIB 8  // queue bands for large frames over render trees above this size (pt_api.cpp launch)
 #endif
@@ -27,32 +24,14 @@
 #endif
 static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand");
 #define PT_QUEUE_WORDS 32  // a work-queue head, alone in its 128-B line
-#ifndef PT_QUEUE_HEADS
-// queue heads, interleaved chunk by chunk, a wave starting at its XCD's: with
+// Queue heads, interleaved chunk by chunk, a wave starting at its XCD's: with
 // the drain helpers, 8 measured C3 +1.9% pipelined, lone launch -4.0%, C5
-// +2.2%, C4 +-0 (profiles/r5/ab_queue_heads.txt; a claim on the one head
-// waited ~1 us: census_claims.txt).  (Round 4, before the helpers: C5 +2%,
-// C3 -0.5..-1%.)
+// +2.2%, C4 +-0 over one head (profiles/r5/ab_queue_heads.txt; a claim on the
+// one head waited ~1 us: census_claims.txt).  The resolve zeroes a launch's
+// heads for the render slot's next launch (pt_kernels.hip resolve_kernel).
+// (Measured and removed: a tail of 64-slot claims from a second head, C3 -2.6%
+// -- profiles/r5/ab_tail_claims.txt.)
 #define PT_QUEUE_HEADS 8
-#endif
-#ifndef PT_RESOLVE_ON_RS
-#define PT_RESOLVE_ON_RS 0  // 1: the resolve on the render slot's stream (one-frame wall +0.03 ms: profiles/r5/ab_resolve_reset_stream.txt)
-#endif
-#ifndef PT_IDLE_DIRECT
-#define PT_IDLE_DIRECT 1  // a launch with no frame in flight runs on the caller's stream (pt_api.cpp launch)
-#endif
-#ifndef PT_HELPERS
-#define PT_HELPERS 1  // retired lanes trace other lanes' shadow rays in the drain (pt_kernels.hip)
-#endif
-#ifndef PT_RESOLVE_RESETS
-#define PT_RESOLVE_RESETS 1  // the resolve zeroes its launch's queue heads for the slot's next launch
-#endif
-#ifndef PT_TAIL_CLAIMS
-#define PT_TAIL_CLAIMS 0  // (measured C3 -2.6% at one tail slot per lane, -5% at two: profiles/r5/ab_tail_claims.txt)
-#endif
-#ifndef PT_TAIL_SLOTS
-#define PT_TAIL_SLOTS 1  // tail slots per resident lane (runtime knob PT_TAIL_SLOTS)
-#endif
 #ifndef PT_GROUP_SPP
 #define PT_GROUP_SPP 4  // default samples per work slot (pt_api.cpp group_size; 8 or more: C3 -4%, C5 -10%)
 #endif
@@ -65,13 +44,9 @@ static_assert(PT_CHUNK >= PT_BLOCK, "a refill must cover a whole wave's demand")
 #ifndef PT_GROUP_MIN_SLOTS
 #define PT_GROUP_MIN_SLOTS 24  // groups are halved until the traced samples make this many slots per lane
 #endif
-// Floats per group sum in memory: 3 (packed float3, 12 B) or 4 (float4, 16 B:
-// every record inside one 16-B aligned chunk -- the write-back experiment of
-// round 5).
-#ifndef PT_SUM_WORDS
-#define PT_SUM_WORDS 3
-#endif
-static_assert(PT_SUM_WORDS == 3 || PT_SUM_WORDS == 4, "PT_SUM_WORDS is 3 or 4");
+// A group sum in memory: a packed float3, 12 B (16-B records measured C3
+// -1.5%: profiles/r5/ab_order_ballot.txt).
+#define PT_SUM_BYTES 12
 #ifndef PT_GROUP_SUM_GIB
 #define PT_GROUP_SUM_GIB 8  // group-sum budget per render slot (GiB): a group size that needs more doubles
 #endif
@@ -196,7 +171,7 @@ __host__ __device__ inline int record_lower_bound(const float* __restrict__ a, f
 #define PT_STACK 24  // traversal stack entries per lane in LDS (lane-contiguous)
 #endif
 #ifndef PT_STACK_MAX
-#define PT_STACK_MAX 256  // deepest worst-case stack accepted (entries past PT_STACK spill to global memory; 8-wide nodes push up to 7 per level)
+#define PT_STACK_MAX 256  // deepest worst-case stack accepted (entries past PT_STACK spill to global memory)
 #endif
 
 // BVH4 node, 128 B (one L2 line): four child boxes in SoA form, component k
@@ -210,50 +185,10 @@ struct alignas(16) DNode {
   int4 pad;
 };
 
-// Node width of the render tree: 8 (DNode8, round 5) or 4 (DNode, rounds 1-4;
-// kept as the A/B arm, -DPT_NODE_WIDTH=4).
-#ifndef PT_NODE_WIDTH
-#define PT_NODE_WIDTH 4
-#endif
-static_assert(PT_NODE_WIDTH == 4 || PT_NODE_WIDTH == 8, "PT_NODE_WIDTH is 4 or 8");
-
-// BVH8 node, 128 B (one L2 line): eight child boxes quantised to fp16 offsets
-// from the node's origin (Ylitie et al. 2017 style, with fp16 instead of 8-bit
-// codes so that a plane decodes with ONE v_fma_mix_f32 and no conversion):
-//   plane = origin[a] + q * 2^e[a], q an fp16 (lox..hiz component k = child k),
-// lo planes rounded down and hi planes rounded up (the quantised box contains
-// the child's float box); then the references of children 0..3.  Children
-// 4..7's references live in a side array (one int4 per node, KParams.nodes8_hi), so a node
-// step is 9 16-B loads over 1.125 lines.  References as DNode.ref (node index
-// or leaf cursor); empty slots hold the inverted box (lo = +inf, hi = -inf),
-// which no ray enters.
-struct alignas(16) DNode8 {
-  float ox, oy, oz;  // origin: the lower corner of the union of the child boxes
-  uint32_t ex;       // per-axis scale exponents, signed bytes 0 (x), 1 (y), 2 (z)
-  uint4 lox, hix, loy, hiy, loz, hiz;  // 8 fp16 each
-  int4 ref;          // children 0..3
-};
-static_assert(sizeof(DNode8) == 128, "DNode8 is one 128-B line");
-
-// Compressed 4-wide node (PT_NODE_COMPRESS, round 5): the same tree as DNode
-// (same children, same leaves), its four child boxes as fp16 offsets from an
-// origin, scaled per axis by 2^e and rounded outward (Ylitie et al. 2017's
-// quantisation at width 4).  80 B = five 16-B loads per node step instead of
-// seven, and 20 VGPRs of node data in flight instead of 28.  A plane decodes
-// as t = q * (2^e * inv) + (origin - o) * inv: one v_fma_mix_f32 per plane;
-// the near / far halves of an axis are picked by the ray's direction sign
-// (x / y / z: lo of children 0..3 in dwords 0-1, hi in dwords 2-3).
-struct alignas(16) DNodeC {
-  float ox, oy, oz;  // origin: the lower corner of the union of the child boxes
-  uint32_t ex;       // per-axis scale exponents, signed bytes 0 (x), 1 (y), 2 (z)
-  uint4 x, y, z;     // 4 lo halves, then 4 hi halves, per axis
-  int4 ref;          // children (node indices or leaf cursors, as DNode.ref)
-};
-static_assert(sizeof(DNodeC) == 80, "DNodeC is five 16-B vectors");
-#ifndef PT_NODE_COMPRESS
-#define PT_NODE_COMPRESS 0
-#endif
-static_assert(!PT_NODE_COMPRESS || PT_NODE_WIDTH == 4, "the compressed node is 4-wide");
+// (Round 5 built and measured two other render-tree encodings, removed in
+// round 6 with their records kept: an 8-wide node with fp16 planes from a node
+// origin, C3 -8.2%, and the 4-wide node compressed the same way to 80 B, C3
+// -2.4%: profiles/r5/ab_stack_fast_w8.txt, ab_sel_spill_compress.txt.)
 
 // Binary node of the reference topology, 64 B: both child boxes + child
 // references (as DNode.ref).  Only traversed by the reference-count launch
@@ -315,12 +250,8 @@ struct KParams {
   uint32_t grp_m, grp_sh;           // fastdiv by n_groups (pt_fastdiv)
   int sblocks;                      // every chunk lies in one block (64 * n_groups a multiple of chunk): scalar block loads
   int chunk;                        // slots per queue claim (PT_CHUNK or PT_CHUNK_MAX), a multiple of 64
-  uint32_t tail_start;              // slots from here on are claimed 64 at a time from the tail head (PT_TAIL_CLAIMS)
   const int* tile_block0;           // first block of each tile (n_tiles + 1 entries), for the resolve
-  const DNode* nodes;     // the render tree, PT_NODE_WIDTH 4
-  const DNode8* nodes8;   // the render tree, PT_NODE_WIDTH 8
-  const int4* nodes8_hi;  // its children 4..7's references
-  const DNodeC* nodesc;   // the render tree, PT_NODE_COMPRESS
+  const DNode* nodes;     // the render tree (BVH4)
   const DNode2* nodes2;  // the binary tree (reference-count launch only)
   const DPrim* prims;
   const float* norms;  // 9 floats per primitive (vertex normals n1,n2,n3)
@@ -396,24 +327,9 @@ struct LbvhOut {
 };
 extern "C" hipError_t ptk_build_lbvh(const LbvhIn* in, LbvhOut* out, hipStream_t s);
 
-// 8-wide render tree (DNode8) collapsed on the device from a binary tree in
-// DNode2 form (bin[0] the root; child references >= 0 index bin, < 0 are leaf
-// cursors), opening the largest-area internal child until eight children.
-// Outputs hipMalloc'd (the caller owns them).
-struct WideOut {
-  DNode8* nodes;
-  int4* hi;       // children 4..7's references, one int4 per node
-  int n;
-  int max_stack;  // worst-case traversal stack
-};
-extern "C" hipError_t ptk_build_wide(const DNode2* bin, int n_bin, WideOut* out, hipStream_t s);
-// The compressed copy (DNodeC) of a 4-wide render tree, node for node.
-extern "C" hipError_t ptk_compress4(const DNode* in, int n, DNodeC* out, hipStream_t s);
-
 extern "C" hipError_t ptk_launch_render(const KParams* P, int grid, bool stats, bool ref_counts, hipStream_t s);
 extern "C" hipError_t ptk_launch_resolve(const KParams* P, hipStream_t s);
-// nodes: DNode (PT_NODE_WIDTH 4) or DNode8 (8, with nodes_hi)
-extern "C" hipError_t ptk_launch_intersect(const void* nodes, const int4* nodes_hi, const DPrim* prims, const float* o, const float* d,
+extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prims, const float* o, const float* d,
                                            const float* maxt, int64_t n, int32_t* hit, float* t, int32_t* prim,
                                            int32_t* anyhit, int* spill, const int* prim_map, hipStream_t s);
 extern "C" hipError_t ptk_render_occupancy(int* waves_per_cu, bool stats, bool env, bool gtab);

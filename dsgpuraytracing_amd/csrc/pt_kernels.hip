@@ -73,26 +73,11 @@ __device__ __forceinline__ void store3(float* p, float3 v) {
   p[1] = v.y;
   p[2] = v.z;
 }
-// A group sum: written once, read once by the resolve.  Non-temporal stores
-// (PT_NT_SUMS=1: no L2 allocation) trade FETCH_SIZE for WRITE_SIZE -- C3
-// -27% / +27%, C5 -6% / +6% -- at throughput within noise (C5 +0.2%, C3 ±0,
-// C4 +0.3%, c5big +0.9%: profiles/r4/ab_nt_sums.txt); left off.
-#ifndef PT_NT_SUMS
-#define PT_NT_SUMS 0
-#endif
-__device__ __forceinline__ void store_sum(float* p, float3 v) {
-#if PT_SUM_WORDS == 4
-  *(float4*)p = make_float4(v.x, v.y, v.z, 0.0f);
-  return;
-#endif
-#if PT_NT_SUMS
-  __builtin_nontemporal_store(v.x, p);
-  __builtin_nontemporal_store(v.y, p + 1);
-  __builtin_nontemporal_store(v.z, p + 2);
-#else
-  store3(p, v);
-#endif
-}
+// A group sum (12 B): written once, read once by the resolve.  (Measured and
+// removed: non-temporal stores, which trade FETCH_SIZE for WRITE_SIZE at
+// throughput within noise -- profiles/r4/ab_nt_sums.txt, r5/ab_nt_sums_final.txt;
+// 16-B records, C3 -1.5% -- r5/ab_order_ballot.txt.)
+__device__ __forceinline__ void store_sum(float* p, float3 v) { store3(p, v); }
 // Pixel q (0..1023) of a tile in 8x8 blocks (4 blocks per row); (-1,-1) when
 // it lies outside a ragged tile.
 __device__ __forceinline__ int2 tile_pixel(int4 tile, uint32_t q) {
@@ -166,43 +151,23 @@ struct Counters {
 // The closest hit is (tmax, prim): the shading round rebuilds the barycentrics
 // and reads the material from the primitive record, so no more of the hit is
 // carried through traversal (every persistent value costs a VGPR in all waves).
-// PT_TRAV_DIR 0: the ray keeps its reciprocal direction only and re-derives
-// the direction where a primitive test or the shading round needs it (tdir,
-// three v_rcp_f32) -- three VGPRs fewer in every wave, which the 8-wide node
-// step needs to stay spill-free; every consumer derives it the same way, so
-// the hit record's barycentrics still equal the traversal test's bit for bit.
-// With 4-wide nodes the direction is kept (the re-derivation measured C3
-// -1.1%, framed C3 -0.5%, C5 -2.1%: profiles/r5/ab_dfree_*.txt).
-#ifndef PT_TRAV_DIR
-#define PT_TRAV_DIR (PT_NODE_WIDTH == 4)
-#endif
+// (Re-deriving the direction from 1/d instead of keeping it measured C3 -1.1%,
+// C5 -2.1%: profiles/r5/ab_dfree_*.txt.)
 struct Trav {
-#if PT_TRAV_DIR
   float3 o, d, inv;
-#else
-  float3 o, inv;
-#endif
   float tmax;
   int node, sp;
   int prim;
   bool any, found;
 };
-__device__ __forceinline__ float3 tdir(const Trav& t) {
-#if PT_TRAV_DIR
-  return t.d;
-#else
-  return f3(rcp(t.inv.x), rcp(t.inv.y), rcp(t.inv.z));
-#endif
-}
+__device__ __forceinline__ float3 tdir(const Trav& t) { return t.d; }
 
 __device__ __forceinline__ void trav_init(Trav& tr, float3 o, float3 d, float tmax, bool any) {
   const float kTiny = 1e-20f;
   float3 dd = f3(fabsf(d.x) < kTiny ? copysignf(kTiny, d.x) : d.x, fabsf(d.y) < kTiny ? copysignf(kTiny, d.y) : d.y,
                  fabsf(d.z) < kTiny ? copysignf(kTiny, d.z) : d.z);
   tr.o = o;
-#if PT_TRAV_DIR
   tr.d = d;
-#endif
   tr.inv = f3(rcp(dd.x), rcp(dd.y), rcp(dd.z));
   tr.tmax = tmax;
   tr.node = 0;
@@ -285,9 +250,6 @@ __device__ __forceinline__ bool prim_test(const float4 v0, const float4 e1, cons
 // compiler merge the LDS / spill paths into FLAT accesses, which occupy the
 // vector-memory (TA/TD) path the node and primitive fetches need.
 typedef __attribute__((address_space(3))) int lds_int;
-#ifndef PT_SPILL_WAIT
-#define PT_SPILL_WAIT 1
-#endif
 
 struct Stack {
   lds_int* lds;   // s_stack + lane, stride PT_BLOCK
@@ -315,12 +277,10 @@ struct Stack {
       v = lds[i * PT_BLOCK];
     } else {
       v = *spill_at(i);
-#if PT_SPILL_WAIT
       // wait for the (rare) spill load here: otherwise the loop latch and
       // header wait vmcnt(0) for it on every iteration, and with it for the
-      // group-sum stores the iteration issued
+      // group-sum stores the iteration issued (C3 +0.5%: r5/ab_sel_spill_compress.txt)
       asm volatile("" : "+v"(v));
-#endif
     }
     return v;
   }
@@ -333,21 +293,13 @@ __device__ __forceinline__ bool trav_pop(const Stack& stk, Trav& tr) {
   return false;
 }
 
-// Stack fast path (PT_STACK_FAST): when no lane of the wave can touch the
-// global spill area in this step (a wave-uniform ballot), pushes and pops are
-// plain LDS accesses without per-lane branches: the divergent push / pop
-// blocks, each with its own spill test, cost ~20 scalar instructions of
-// exec-mask bookkeeping per traversal iteration, and a scalar instruction in
-// the traversal loop costs more than a vector one (profiles/r5/probes_inst_cost.txt).
-#ifndef PT_FOLLOW_SEL
-#define PT_FOLLOW_SEL 1
-#endif
-#ifndef PT_STACK_FAST
-#define PT_STACK_FAST 1
-#endif
-#ifndef PT_SEL_SIMPLE
-#define PT_SEL_SIMPLE 1
-#endif
+// Stack fast path: when no lane of the wave can touch the global spill area
+// in this step (a wave-uniform ballot), pushes and pops are plain LDS
+// accesses without per-lane branches: the divergent push / pop blocks, each
+// with its own spill test, cost ~20 scalar instructions of exec-mask
+// bookkeeping per traversal iteration, and a scalar instruction in the
+// traversal loop costs more than a vector one (profiles/r5/probes_inst_cost.txt;
+// C3 +1.5%: r5/ab_stack_fast_w8.txt).
 // Pop for the lanes with `pop` set, every lane's stack top in LDS (sp <=
 // PT_STACK); returns true for a lane whose stack was empty (its traversal is
 // over).  The LDS read is issued for every lane (entry 0 for an empty stack).
@@ -370,55 +322,18 @@ __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb) {
   ra = tr;
 }
 
-// Child order of a node step (PT_NODE_ORDER): 1 = continue with the NEAREST
-// entered child and push the other entered ones in slot order (slot 3 first,
-// the lowest slot on top); 0 = the round-1..4 full sort (5-exchange network,
-// farthest pushed first).  Rays enter 1.02 children per node on average, so
-// the order of the pushed ones hardly matters: the CPU traversal census of
-// the C3 ray mix (tools/wide_sim.cpp) gives the same node and leaf steps per
-// ray for both (camera 6.40 / 6.40, bounce 7.17 / 7.13, shadow 6.00 / 6.00),
-// and the nearest-only selection is a third of the network's VALU.  On the
-// GPU the network measured faster all the same (same session, 3 rounds: C3
-// +1.3%, lone launch -2.5%; C5 +1.8%: profiles/r5/ab_order_ballot.txt), so it
-// stays the default.
-#ifndef PT_NODE_ORDER
-#define PT_NODE_ORDER 0
-#endif
-
+// Child order of a node step: the full sort (5-exchange network, farthest
+// pushed first).  Rays enter 1.02 children per node on average, so the order
+// of the pushed ones hardly matters (CPU traversal census of the C3 ray mix,
+// tools/wide_sim.cpp), and continuing with the nearest child while pushing
+// the rest in slot order is a third of the network's VALU -- yet the network
+// measured faster on the GPU (C3 +1.3%, C5 +1.8%: profiles/r5/ab_order_ballot.txt).
+//
 // Second half of a node step: entry distances d (kMiss = not entered) and
 // references rf of the four children -> continue with the nearest, push the
 // other hits.
 __device__ __forceinline__ bool node_order(const Stack& stk, Trav& tr, const float* d, const int4 rf) {
   const float kMiss = 3.0e38f;
-#if PT_NODE_ORDER == 1
-  {
-    const int r[4] = {rf.x, rf.y, rf.z, rf.w};
-    float dmin = d[0];
-    int rn = r[0];
-#pragma unroll
-    for (int k = 1; k < 4; ++k) {
-      const bool nearer = d[k] < dmin;
-      dmin = fminf(dmin, d[k]);
-      rn = nearer ? r[k] : rn;
-    }
-    if (dmin == kMiss) return trav_pop(stk, tr);
-    int sp = tr.sp;
-    if (sp + 4 <= PT_STACK) {
-#pragma unroll
-      for (int k = 3; k >= 0; --k) {
-        stk.lds[sp * PT_BLOCK] = r[k];
-        sp += d[k] != kMiss && r[k] != rn;
-      }
-    } else {
-#pragma unroll
-      for (int k = 3; k >= 0; --k)
-        if (d[k] != kMiss && r[k] != rn) stk.put(sp++, r[k]);
-    }
-    tr.sp = sp;
-    tr.node = rn;
-    return false;
-  }
-#endif
   int r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
   float d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3];
   // near-first order: 5-exchange sorting network on the entry distances
@@ -427,7 +342,6 @@ __device__ __forceinline__ bool node_order(const Stack& stk, Trav& tr, const flo
   cswap(d0, r0, d2, r2);
   cswap(d1, r1, d3, r3);
   cswap(d1, r1, d2, r2);
-#if PT_STACK_FAST
   if (__ballot(tr.sp > PT_STACK - 3) == 0ull) {  // (wave-uniform) three pushes and a pop stay in LDS
     // the hits are a sorted prefix: all three candidates are written, the top
     // advances past hits only; a lane that entered no child pushed nothing
@@ -445,7 +359,6 @@ __device__ __forceinline__ bool node_order(const Stack& stk, Trav& tr, const flo
     if (__ballot(miss) == 0ull) return false;
     return trav_pop_lds(stk, tr, miss);
   }
-#endif
   if (d0 == kMiss) return trav_pop(stk, tr);
   // push the farther hits (farthest first), continue with the nearest.  The
   // hits are a sorted prefix, so with room for three entries every candidate
@@ -537,174 +450,12 @@ __device__ __forceinline__ bool node_step(const DNode* __restrict__ nodes, const
   return node_order(stk, tr, d, rf);
 }
 
-// 8-wide node step (DNode8, round 5; Ylitie et al. 2017 style, fp16 planes).
-// A plane decodes as t = q * (2^e * inv) + (origin - o) * inv: per node the
-// three scales a = ldexp(inv, e) and offsets b, per plane ONE v_fma_mix_f32
-// (the fp16 operand is read from its half of the dword by op_sel, no
-// conversion).  Near
-// and far planes are picked by the ray's direction signs through the load
-// addresses, as in node_step.  Child order: continue with the NEAREST entered
-// child, push the other entered ones in slot order (lowest slot on top) --
-// the traversal census of the C3 ray mix (tools/wide_sim.cpp)
-// gives the same node and leaf steps per ray as a full distance sort (4.97 vs
-// 4.96 camera, 5.57 vs 5.53 bounce, 4.43 vs 4.44 shadow) for a third of its
-// VALU: rays enter 1.03 children per node on average.  Nine 16-B loads: the
-// header, six plane vectors (8 halves each), two reference vectors.
-typedef _Float16 pt_h8 __attribute__((ext_vector_type(8)));
-template <bool STATS, bool ROOT = false>
-__device__ __forceinline__ bool node_step8(const DNode8* __restrict__ nodes, const int4* __restrict__ nodes_hi,
-                                           const Stack& stk, Trav& tr, Counters& ct, lds_cchar* root = nullptr) {
-  const float kRobust = PT_ROBUST;
-  const float3 o = tr.o, inv = tr.inv;
-  const uint32_t sx = (__float_as_uint(inv.x) >> 27) & 16u, sy = (__float_as_uint(inv.y) >> 27) & 16u,
-                 sz = (__float_as_uint(inv.z) >> 27) & 16u;
-  pt_v4i hd, nx, fx, ny, fy, nz, fz, r0, r1;
-  if constexpr (ROOT) {
-    typedef __attribute__((address_space(3))) const pt_v4i lds_v4i;
-    hd = *(lds_v4i*)root;
-    nx = *(lds_v4i*)(root + (16u + sx));
-    fx = *(lds_v4i*)(root + (16u + (sx ^ 16u)));
-    ny = *(lds_v4i*)(root + (48u + sy));
-    fy = *(lds_v4i*)(root + (48u + (sy ^ 16u)));
-    nz = *(lds_v4i*)(root + (80u + sz));
-    fz = *(lds_v4i*)(root + (80u + (sz ^ 16u)));
-    r0 = *(lds_v4i*)(root + 112u);
-    r1 = *(lds_v4i*)(root + 128u);
-  } else {
-    const char* nb = (const char*)nodes;
-    const uint32_t base = (uint32_t)tr.node << 7;
-    hd = *(const pt_v4i*)(nb + base);
-    nx = *(const pt_v4i*)(nb + (base + 16u + sx));
-    fx = *(const pt_v4i*)(nb + (base + 16u + (sx ^ 16u)));
-    ny = *(const pt_v4i*)(nb + (base + 48u + sy));
-    fy = *(const pt_v4i*)(nb + (base + 48u + (sy ^ 16u)));
-    nz = *(const pt_v4i*)(nb + (base + 80u + sz));
-    fz = *(const pt_v4i*)(nb + (base + 80u + (sz ^ 16u)));
-    r0 = *(const pt_v4i*)(nb + (base + 112u));
-    r1 = *(const pt_v4i*)((const char*)nodes_hi + ((uint32_t)tr.node << 4));
-    asm volatile("" : "+v"(fz), "+v"(r0), "+v"(r1));
-  }
-  if (STATS) ct.nodes++;
-  const uint32_t ew = (uint32_t)hd.w;
-  const float ax = __builtin_amdgcn_ldexpf(inv.x, (int)(int8_t)(ew & 0xffu));
-  const float ay = __builtin_amdgcn_ldexpf(inv.y, (int)(int8_t)((ew >> 8) & 0xffu));
-  const float az = __builtin_amdgcn_ldexpf(inv.z, (int)(int8_t)((ew >> 16) & 0xffu));
-  const float bx = (__int_as_float(hd.x) - o.x) * inv.x;
-  const float by = (__int_as_float(hd.y) - o.y) * inv.y;
-  const float bz = (__int_as_float(hd.z) - o.z) * inv.z;
-  const pt_h8 NX = __builtin_bit_cast(pt_h8, nx), FX = __builtin_bit_cast(pt_h8, fx);
-  const pt_h8 NY = __builtin_bit_cast(pt_h8, ny), FY = __builtin_bit_cast(pt_h8, fy);
-  const pt_h8 NZ = __builtin_bit_cast(pt_h8, nz), FZ = __builtin_bit_cast(pt_h8, fz);
-  const int ref[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-  bool hit[8];
-  float dmin = __builtin_inff();
-  int rn = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const float tn = fmaxf(fmaxf(fmaf((float)NX[k], ax, bx), fmaf((float)NY[k], ay, by)),
-                           fmaxf(fmaf((float)NZ[k], az, bz), 0.0f));
-    const float tf = fminf(fminf(fmaf((float)FX[k], ax, bx), fmaf((float)FY[k], ay, by)),
-                           fminf(fmaf((float)FZ[k], az, bz), tr.tmax)) * kRobust;
-    hit[k] = tn <= tf;
-    const bool nearer = hit[k] && tn < dmin;
-    dmin = nearer ? tn : dmin;
-    rn = nearer ? ref[k] : rn;
-  }
-  if (dmin == __builtin_inff()) return trav_pop(stk, tr);
-  // push the other entered children, slot 7 first (lowest slot on top); with
-  // room for eight entries every candidate is written and the top advances
-  // only past pushed ones (no branches)
-  int sp = tr.sp;
-  if (sp + 8 <= PT_STACK) {
-#pragma unroll
-    for (int k = 7; k >= 0; --k) {
-      stk.lds[sp * PT_BLOCK] = ref[k];
-      sp += hit[k] && ref[k] != rn;
-    }
-  } else {
-#pragma unroll
-    for (int k = 7; k >= 0; --k)
-      if (hit[k] && ref[k] != rn) stk.put(sp++, ref[k]);
-  }
-  tr.sp = sp;
-  tr.node = rn;
-  return false;
-}
+// (Round 5 measured and removed two other node encodings: an 8-wide node with
+// fp16 planes, C3 -8.2% / C4 -11.5% / C5 -9.8% -- more primitive tests and leaf
+// steps than the 4-wide tree; and this 4-wide node compressed to fp16 planes
+// from a node origin, 80 B, C3 -2.4%: profiles/r5/ab_stack_fast_w8.txt,
+// ab_sel_spill_compress.txt; DESIGN.md "Why the wide node loses".)
 
-// Compressed 4-wide node step (DNodeC, PT_NODE_COMPRESS): five 16-B loads
-// (header, x, y, z, references); the near / far halves of each axis picked by
-// the ray's direction sign (two v_cndmask per half-vector), one v_fma_mix_f32
-// per plane against the per-node scales a = 2^e * inv and offsets b =
-// (origin - o) * inv; then the same entry test, order and pushes as node_step.
-template <bool STATS, bool ROOT = false>
-__device__ __forceinline__ bool node_stepc(const DNodeC* __restrict__ nodes, const Stack& stk, Trav& tr,
-                                           Counters& ct, lds_cchar* root = nullptr) {
-  const float kRobust = PT_ROBUST;
-  const float3 o = tr.o, inv = tr.inv;
-  const float kMiss = 3.0e38f;
-  pt_v4i hd, X, Y, Z, rv;
-  if constexpr (ROOT) {
-    typedef __attribute__((address_space(3))) const pt_v4i lds_v4i;
-    hd = *(lds_v4i*)root;
-    X = *(lds_v4i*)(root + 16u);
-    Y = *(lds_v4i*)(root + 32u);
-    Z = *(lds_v4i*)(root + 48u);
-    rv = *(lds_v4i*)(root + 64u);
-  } else {
-    // (node index * 80 as one full-rate 24-bit multiply: pt_upload_scene
-    // keeps compressed trees below 2^24 nodes; the five loads share one
-    // address register and immediate offsets)
-    const pt_v4i* np = (const pt_v4i*)((const char*)nodes + __umul24((uint32_t)tr.node, 80u));
-    hd = np[0];
-    X = np[1];
-    Y = np[2];
-    Z = np[3];
-    rv = np[4];
-    asm volatile("" : "+v"(Z), "+v"(rv));
-  }
-  if (STATS) ct.nodes++;
-  const uint32_t ew = (uint32_t)hd.w;
-  const float ax = __builtin_amdgcn_ldexpf(inv.x, (int)(int8_t)(ew & 0xffu));
-  const float ay = __builtin_amdgcn_ldexpf(inv.y, (int)(int8_t)((ew >> 8) & 0xffu));
-  const float az = __builtin_amdgcn_ldexpf(inv.z, (int)(int8_t)((ew >> 16) & 0xffu));
-  const float bx = (__int_as_float(hd.x) - o.x) * inv.x;
-  const float by = (__int_as_float(hd.y) - o.y) * inv.y;
-  const float bz = (__int_as_float(hd.z) - o.z) * inv.z;
-  // near planes: lo for a positive direction component, hi for a negative one
-  const bool sx = inv.x < 0.0f, sy = inv.y < 0.0f, sz = inv.z < 0.0f;
-  typedef _Float16 pt_h4 __attribute__((ext_vector_type(4)));
-  typedef int pt_v2i __attribute__((ext_vector_type(2)));
-  const pt_h4 NX = __builtin_bit_cast(pt_h4, sx ? X.zw : X.xy), FX = __builtin_bit_cast(pt_h4, sx ? X.xy : X.zw);
-  const pt_h4 NY = __builtin_bit_cast(pt_h4, sy ? Y.zw : Y.xy), FY = __builtin_bit_cast(pt_h4, sy ? Y.xy : Y.zw);
-  const pt_h4 NZ = __builtin_bit_cast(pt_h4, sz ? Z.zw : Z.xy), FZ = __builtin_bit_cast(pt_h4, sz ? Z.xy : Z.zw);
-  float d[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float tn = fmaxf(fmaxf(fmaf((float)NX[k], ax, bx), fmaf((float)NY[k], ay, by)),
-                           fmaxf(fmaf((float)NZ[k], az, bz), 0.0f));
-    const float tf = fminf(fminf(fmaf((float)FX[k], ax, bx), fmaf((float)FY[k], ay, by)),
-                           fminf(fmaf((float)FZ[k], az, bz), tr.tmax)) * kRobust;
-    d[k] = tn <= tf ? tn : kMiss;
-  }
-  return node_order(stk, tr, d, make_int4(rv.x, rv.y, rv.z, rv.w));
-}
-
-// The render tree's node step: 8-wide (DNode8 + nodes_hi) or 4-wide (DNode).
-template <bool STATS, bool ROOT = false>
-__device__ __forceinline__ bool node_stepw(const void* __restrict__ nodes, const int4* __restrict__ nodes_hi,
-                                           const Stack& stk, Trav& tr, Counters& ct, lds_cchar* root = nullptr) {
-#if PT_NODE_WIDTH == 8
-  return node_step8<STATS, ROOT>((const DNode8*)nodes, nodes_hi, stk, tr, ct, root);
-#elif PT_NODE_COMPRESS
-  (void)nodes_hi;
-  return node_stepc<STATS, ROOT>((const DNodeC*)nodes, stk, tr, ct, root);
-#else
-  (void)nodes_hi;
-  return node_step<STATS, ROOT>((const DNode*)nodes, stk, tr, ct, root);
-#endif
-}
-// bytes of the workgroup's LDS copy of the root (node + children 4..7's references)
-#define PT_ROOT_BYTES (PT_NODE_WIDTH == 8 ? 144 : PT_NODE_COMPRESS ? 80 : 128)
 
 // Binary node step over the reference topology (reference-count launch).
 template <bool STATS>
@@ -797,7 +548,6 @@ __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const
     tr.prim = hb ? pb : ha ? pa : tr.prim;
     tr.found = tr.found || ha || hb;
     if (STATS) ct.tris += two ? 2u : 1u;
-#if PT_STACK_FAST
     if (__ballot(tr.sp > PT_STACK) == 0ull) {  // (wave-uniform) every pop reads LDS
       const bool stop = tr.any & (ha | hb);   // occlusion found: the ray is done
       const bool more = n > 2;                // the leaf's next two primitives
@@ -806,7 +556,6 @@ __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const
       if (__ballot(pop) == 0ull) return stop;
       return stop | trav_pop_lds(stk, tr, pop);
     }
-#endif
     if (tr.any && (ha || hb)) return true;
   } else {
     if (prim_test<STATS>(a0, a1, a2, pa, tr, ct)) return true;
@@ -820,18 +569,18 @@ __device__ __forceinline__ bool leaf_step(const DPrim* __restrict__ prims, const
 }
 
 template <bool STATS>
-__device__ __forceinline__ bool trav_step(const void* __restrict__ nodes, const int4* __restrict__ nodes_hi,
-                                          const DPrim* __restrict__ prims, const Stack& stk, Trav& tr, Counters& ct) {
-  return tr.node < 0 ? leaf_step<STATS>(prims, stk, tr, ct) : node_stepw<STATS>(nodes, nodes_hi, stk, tr, ct);
+__device__ __forceinline__ bool trav_step(const DNode* __restrict__ nodes, const DPrim* __restrict__ prims,
+                                          const Stack& stk, Trav& tr, Counters& ct) {
+  return tr.node < 0 ? leaf_step<STATS>(prims, stk, tr, ct) : node_step<STATS>(nodes, stk, tr, ct);
 }
 
 template <bool STATS>
-__device__ __forceinline__ bool traverse(const void* __restrict__ nodes, const int4* __restrict__ nodes_hi,
-                                         const DPrim* __restrict__ prims, const Stack& stk, float3 o, float3 d,
+__device__ __forceinline__ bool traverse(const DNode* __restrict__ nodes, const DPrim* __restrict__ prims,
+                                         const Stack& stk, float3 o, float3 d,
                                          float tmax, bool any, Hit& hit, Counters& ct) {
   Trav tr;
   trav_init(tr, o, d, tmax, any);
-  while (!trav_step<STATS>(nodes, nodes_hi, prims, stk, tr, ct)) {
+  while (!trav_step<STATS>(nodes, prims, stk, tr, ct)) {
   }
   hit.t = tr.tmax;
   hit.prim = tr.prim;
@@ -900,10 +649,8 @@ __device__ __forceinline__ float3 env_dir(const KP& P, float3 d) {
 // looked up at the texel coordinates the sample was drawn at, (x - 0.5,
 // y - 0.5) -- what sample_dir's acos round trip of wi yields up to float
 // rounding (~1e-5 texel), without its two acosf and a division on the
-// NEE's dependent chain: returned in (tu, tv) for env_uv.
-#ifndef PT_ENV_DIRECT_UV
-#define PT_ENV_DIRECT_UV 1
-#endif
+// NEE's dependent chain: returned in (tu, tv) for env_uv (C5 +1.5%:
+// profiles/r4/ab_env_uv_groups.txt).
 template <class KP>
 __device__ __forceinline__ void env_sample(const KP& P, float r1, float r2, float3& wi, float& pdf, float& tu,
                                            float& tv) {
@@ -934,24 +681,6 @@ __device__ __forceinline__ void env_sample(const KP& P, float r1, float r2, floa
 enum : int { M_TRAV = 0, M_SHADE = 1, M_FETCH = 2, M_CAMERA = 3, M_DONE = 4 };
 // What follows a lane's shadow ray (the `shadow` state; 0 = not a shadow ray).
 enum : int { SH_HELPER = -1, SH_RESUME = 1, SH_FOLLOW = 2, SH_STORE = 3, SH_STORE_FOLLOW = 4 };
-// Launch parameters re-read per round (see render_kernel): on for the
-// environment-light build since round 3 (C5 +6.8%, no VGPR spills instead of
-// 8) and for the common one since round 4 (C3 +0.9%, 71 SGPR spills to VGPR
-// lanes removed; it measured C3 -1.1% on the round-3 kernel:
-// profiles/r3/ab_kernarg_round.txt, profiles/r4/ab_layout.txt).
-#ifndef PT_KARG_ROUND
-#define PT_KARG_ROUND 1
-#endif
-#ifndef PT_STATIC_FIRST
-#define PT_STATIC_FIRST 1
-#endif
-#ifndef PT_BALLOT_SPLIT
-#define PT_BALLOT_SPLIT 1
-#endif
-// Instruction-cost probes (diagnostics, 0 = off): N extra independent SALU or
-// VALU instructions per traversal iteration (PT_PROBE_TRAV_*) or per shading
-// round (PT_PROBE_SHADE_*), to price one more instruction of each kind in each
-// phase (tools/ab.sh against the plain build).
 // Wave priorities of the two phases (s_setprio; shading raised: round 3,
 // profiles/r3/ab_build_options.txt)
 #ifndef PT_PRIO_SHADE
@@ -960,31 +689,6 @@ enum : int { SH_HELPER = -1, SH_RESUME = 1, SH_FOLLOW = 2, SH_STORE = 3, SH_STOR
 #ifndef PT_PRIO_TRAV
 #define PT_PRIO_TRAV 0
 #endif
-#ifndef PT_PROBE_TRAV_SALU
-#define PT_PROBE_TRAV_SALU 0
-#endif
-#ifndef PT_PROBE_TRAV_VALU
-#define PT_PROBE_TRAV_VALU 0
-#endif
-#ifndef PT_PROBE_SHADE_SALU
-#define PT_PROBE_SHADE_SALU 0
-#endif
-#ifndef PT_PROBE_SHADE_VALU
-#define PT_PROBE_SHADE_VALU 0
-#endif
-template <int NS, int NV>
-__device__ __forceinline__ void probe_insts() {
-#pragma unroll
-  for (int k = 0; k < NS; ++k) {
-    int s;
-    asm volatile("s_mov_b32 %0, %1" : "=s"(s) : "i"(k));
-  }
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    int v;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "i"(k));
-  }
-}
 
 // Wave-clock sections of the STATS build: every shader clock of a wave's
 // lifetime falls in exactly one (pt_stats.shade_clocks + trav_clocks = the
@@ -1016,16 +720,9 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   const Stack stk{(lds_int*)(s_stack + lane), P.stack_spill, n_waves * PT_BLOCK};
   // The BVH4 root, which every ray visits first: one LDS copy per wave, so
   // the root step of a fresh ray costs no vector-memory traffic (C3 +2%).
-  __shared__ int4 s_root[PT_ROOT_BYTES / 16];
+  __shared__ int4 s_root[sizeof(DNode) / 16];
   if (!BIN) {
-#if PT_NODE_WIDTH == 8
-    if (lane < 8) s_root[lane] = ((const int4*)P.nodes8)[lane];
-    else if (lane == 8) s_root[8] = P.nodes8_hi[0];
-#elif PT_NODE_COMPRESS
-    if (lane < 5) s_root[lane] = ((const int4*)P.nodesc)[lane];
-#else
     if (lane < 8) s_root[lane] = ((const int4*)P.nodes)[lane];
-#endif
   }
 
   // Material and light tables are read by every shading step: keep small
@@ -1061,17 +758,16 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   __shared__ uint32_t s_hist[STATS ? 32 : 1];
   if (STATS && lane < 32) s_hist[lane] = 0u;
   __syncthreads();
-#if PT_KARG_ROUND
   // From here on the launch parameters are read through a pointer to the
   // kernel-argument segment that an empty asm "changes" at the start of every
   // round: their scalar loads stay inside the round (scalar-cache hits)
   // instead of being hoisted to the kernel's start and held in SGPRs for the
   // whole kernel -- spilled SGPRs occupy VGPR lanes, and the constants the
-  // SGPR allocator then keeps in VGPRs cost the ENV build its spills.
+  // SGPR allocator then keeps in VGPRs cost the ENV build its spills (C5
+  // +6.8%, C3 +0.9%: profiles/r3/ab_kernarg_round.txt, r4/ab_layout.txt).
   typedef __attribute__((address_space(4))) const KParams karg_t;
   karg_t* Q = (karg_t*)__builtin_amdgcn_kernarg_segment_ptr();
 #define P (*Q)
-#endif
 #define PT_STAMP(k)                                                  \
   if constexpr (STATS) {                                             \
     const unsigned long long t_ = clock64();                         \
@@ -1096,7 +792,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // ng, which is dead between a path's last vertex and the next hit record.
   int shadow = 0;
   uint32_t oslot = 0;
-  // (PT_HELPERS) the lane tracing this lane's last shadow ray, -1 for none
+  // (drain helpers) the lane tracing this lane's last shadow ray, -1 for none
   int hl = -1;
   // the work slot (pixel, sample group) this lane renders: its index (where
   // the group's sum goes), its pixel as packed coordinates (x | y << 16;
@@ -1133,10 +829,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   uint32_t chunk_next = 0, chunk_end = 0;  // the wave's private range of work slots
   uint32_t seen = 0;                       // queue head after this wave's last claim
   bool first_claim = true;                 // the first chunk is the wave's own (no atomic)
-#if PT_QUEUE_HEADS > 1
   // the queue head this wave claims from: its XCD's (HW_REG_XCC_ID), until that one runs dry
   uint32_t qh = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) % PT_QUEUE_HEADS;
-#endif
   const unsigned long long w_start = STATS ? wall_clock64() : 0ull;
   // Residency census of the plain build (PT_CENSUS set, diagnostics): when
   // each wave started and ended, and where it ran -- which waves of the grid
@@ -1202,28 +896,21 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // light sample (or store the group's total with it) and go on with the
   // next extension ray -- or retire -- without a shading round.
   auto follow_on = [&](bool done) {
-#if PT_BALLOT_SPLIT
     {  // (the divergent branch alone skips itself when no lane takes it)
-#else
-    if (__ballot(done && shadow >= SH_FOLLOW) != 0ull) {
-#endif
       if (done && shadow >= SH_FOLLOW) {
         if (shadow == SH_FOLLOW) {
           if (!tr.found) acc = acc + pend;
         } else {  // the finished group's one store: its total with the light sample if the shadow ray is clear
-          store_sum(P.partial + PT_SUM_WORDS * (size_t)oslot, tr.found ? acc : pend);
+          store_sum(P.partial + 3 * (size_t)oslot, tr.found ? acc : pend);
           acc = ng;  // the new group's sum so far (environment seen by its camera rays that missed)
         }
-#if PT_FOLLOW_SEL
         if (shadow == SH_STORE) {
           mode = M_DONE;
         } else {
           Trav nt;
           trav_init(nt, hp, ns, 3.0e38f, false);
           tr.o = nt.o;
-#if PT_TRAV_DIR
           tr.d = nt.d;
-#endif
           tr.inv = nt.inv;
           tr.any = false;
           mode = M_TRAV;
@@ -1233,35 +920,21 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     }
     // the follow-up ray's traversal state by selects, outside the branch: the
     // loop-carried node / stack / tmax / primitive keep one register each
-    // (with the branch the compiler copied them to and fro every iteration)
+    // (with the branch the compiler copied them to and fro every iteration;
+    // C3 +0.7%: profiles/r5/ab_helpers_followsel.txt)
     const bool fo = done && mode == M_TRAV;
     tr.node = fo ? 0 : tr.node;
     tr.sp = fo ? 0 : tr.sp;
     tr.tmax = fo ? 3.0e38f : tr.tmax;
     tr.prim = fo ? -1 : tr.prim;
     tr.found = fo ? false : tr.found;
-#else
-        if (shadow == SH_STORE) {
-          mode = M_DONE;
-        } else {
-          trav_init(tr, hp, ns, 3.0e38f, false);
-          mode = M_TRAV;
-        }
-        shadow = 0;
-      }
-    }
-#endif
   };
 
   for (;;) {
-#if PT_KARG_ROUND
     asm volatile("" : "+s"(Q));
-#endif
     // the shading round issues at raised wave priority, traversal at the
     // base one (C4 +0.6%, C5 +0.4%, C3 within noise: profiles/r3/ab_build_options.txt)
     __builtin_amdgcn_s_setprio(PT_PRIO_SHADE);
-    probe_insts<PT_PROBE_SHADE_SALU, PT_PROBE_SHADE_VALU>();
-#if PT_HELPERS
     // Drain helpers (the pairing is at the end of the refill): a helper's
     // shadow ray ended -- its owner adds the light sample if the ray was
     // clear, before anything else of its path (the order of trace_ray's
@@ -1282,9 +955,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         }
       }
     }
-#endif
     // ================= shading phase: lanes whose ray finished =================
-    if (mode == M_SHADE && (!PT_HELPERS || hl < 0)) {
+    if (mode == M_SHADE && hl < 0) {
       const bool found = tr.found;
       bool finish = false;  // the sample is complete
       bool group_end = false;  // the group's last sample ended: store its sum
@@ -1402,7 +1074,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           float cos_t = fmaxf(0.0f, fr.to_local(wi).z);
           if (!(cos_t > 0.0f)) continue;
           float3 f = PT_BSDF3(bsdf, a) * 0.31830988618379067f;
-          const float3 Le = (ENV && ltype == 4) ? (PT_ENV_DIRECT_UV ? env_uv(P, etu, etv) : env_dir(P, wi))
+          const float3 Le = (ENV && ltype == 4) ? env_uv(P, etu, etv)
                                                 : PT_LIGHT3(li, rad);
           pend = mul(mul(T, Le * (cos_t * rcp(pdf))), f) * scale;
           // shadow ray (pathtracer.cpp:497-504): delta lights offset EPS_N along n
@@ -1528,7 +1200,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         }
       }
       if (group_end) {
-        store_sum(P.partial + PT_SUM_WORDS * (size_t)myslot, acc);
+        store_sum(P.partial + 3 * (size_t)myslot, acc);
         PT_SLOT_DONE();
         mode = M_FETCH;
       }
@@ -1561,7 +1233,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             // the XCDs far from its channel) stalled every round of the
             // remaining paths (C3: the XCDs' median drain 380 vs 680 us).
             nbase = total_slots;
-          } else if (PT_STATIC_FIRST && first_claim) {
+          } else if (first_claim) {
             // The wave's first chunk is dealt statically (chunk wave_id): at
             // the launch's start every wave would otherwise queue on the one
             // head at once (memory-side atomics, serialised), and the last
@@ -1575,8 +1247,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
 #if PT_CENSUS
             const unsigned long long c_t0 = census ? wall_clock64() : 0ull;
 #endif
-#if PT_QUEUE_HEADS > 1
-            const uint32_t base0 = PT_STATIC_FIRST ? n_waves * csize : 0u;  // (after the statically dealt chunks)
+            const uint32_t base0 = n_waves * csize;  // (after the statically dealt chunks)
             // PT_QUEUE_HEADS heads, one per XCD, each in its own 128-B line:
             // head h deals chunks h, h + H, h + 2H, ... -- the same interleaved
             // sweep of the frame as one head, with 1/H of the atomics on each
@@ -1605,20 +1276,6 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
               qh = (qh + 1u) % PT_QUEUE_HEADS;
             }
             if (nbase >= total_slots) csize = 0;  // every head ran dry: drained
-#else
-            if (lane == 0) nbase = atomicAdd(P.work_counter, csize);
-            // (the head counts the chunks after the statically dealt ones)
-            nbase = __builtin_amdgcn_readfirstlane(__shfl(nbase, 0)) + (PT_STATIC_FIRST ? n_waves * csize : 0u);
-#if PT_TAIL_CLAIMS
-            if (nbase >= P.tail_start) {  // (wave-uniform) the frame's tail: 64-slot claims from the tail head
-              csize = 64u;
-              uint32_t r = 0;
-              if (lane == 0) r = atomicAdd(P.work_counter + PT_QUEUE_WORDS * PT_QUEUE_HEADS, 64u);
-              nbase = __builtin_amdgcn_readfirstlane(__shfl(r, 0)) + P.tail_start;
-              if (STATS) n_atomics += lane == 0;
-            }
-#endif
-#endif
 #if PT_CENSUS
             if (census) {  // (diagnostics: how long the claim's atomics took to return)
               asm volatile("" ::"s"(nbase));
@@ -1629,12 +1286,10 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             }
 #endif
             seen = nbase + csize;
-#if PT_QUEUE_HEADS > 1
             // (several heads: the end of one head's range -- the last chunk of
             // the frame, or of a band -- is not the queue's; the wave has seen
             // the queue drained only when every head was dry, csize == 0)
             if (csize != 0u) seen = min(seen, total_slots - 1u);
-#endif
             if (STATS) n_atomics += lane == 0;
           }
         }
@@ -1755,7 +1410,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
             ng = f3(0, 0, 0);  // (the next group's sum while the store is pending)
             shadow = SH_STORE;
           } else {  // SH_STORE: this group's sum is in ng (acc holds the last group's)
-            store_sum(P.partial + PT_SUM_WORDS * (size_t)myslot, shadow ? ng : acc);
+            store_sum(P.partial + 3 * (size_t)myslot, shadow ? ng : acc);
           }
           PT_SLOT_DONE();
           mode = M_FETCH;
@@ -1764,7 +1419,6 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       PT_STAMP(S_CAMERA);
       if (__ballot(mode == M_FETCH) == 0ull) break;
     }
-#if PT_HELPERS
     // Drain helpers: once the wave's share of the queue is gone, its retired
     // lanes (M_DONE) take the shadow rays just emitted by lanes with an
     // extension ray behind them (SH_FOLLOW), and those lanes start that ray
@@ -1794,15 +1448,11 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         auto pull = [&](float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(v))); };
         const float3 so = f3(pull(tr.o.x), pull(tr.o.y), pull(tr.o.z));
         const float3 si = f3(pull(tr.inv.x), pull(tr.inv.y), pull(tr.inv.z));
-#if PT_TRAV_DIR
         const float3 sd = f3(pull(tr.d.x), pull(tr.d.y), pull(tr.d.z));
-#endif
         const float st = pull(tr.tmax);
         if (helper) {
           tr.o = so;
-#if PT_TRAV_DIR
           tr.d = sd;
-#endif
           tr.inv = si;
           tr.tmax = st;
           tr.node = 0;
@@ -1820,7 +1470,6 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         }
       }
     }
-#endif
     // ================= traversal phase =================
     __builtin_amdgcn_s_setprio(PT_PRIO_TRAV);
     // Step every in-flight ray one node at a time; leave as soon as `batch`
@@ -1831,14 +1480,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     // asm -- so the re-read parameters are not re-loaded per iteration --
     // measured C5 -2.5%, C3 -3%: the scalar loads hide behind the node
     // step's vector loads; profiles/r4/ab_layout.txt)
-#if PT_NODE_WIDTH == 8
-    const void* t_nodes = P.nodes8;
-#elif PT_NODE_COMPRESS
-    const void* t_nodes = P.nodesc;
-#else
-    const void* t_nodes = P.nodes;
-#endif
-    const int4* t_nodes_hi = P.nodes8_hi;
+    const DNode* t_nodes = P.nodes;
     const DPrim* t_prims = P.prims;
     const int t_leaf_weight = P.leaf_weight;
     // Fresh rays (node 0: references only point forward, so no ray returns
@@ -1848,7 +1490,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
     if constexpr (!BIN) {
       bool done = false;
       if (mode == M_TRAV && tr.node == 0) {
-        done = node_stepw<STATS, true>(t_nodes, t_nodes_hi, stk, tr, ct, (lds_cchar*)s_root);
+        done = node_step<STATS, true>(t_nodes, stk, tr, ct, (lds_cchar*)s_root);
         if (done) mode = M_SHADE;
       }
       follow_on(done);  // (a shadow ray leaves the root only if it misses every child box)
@@ -1876,26 +1518,17 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       // a leaf (or nothing else is left), node steps otherwise
       const bool trav = mode == M_TRAV;
       const bool at_leaf = trav && tr.node < 0;
-#if PT_BALLOT_SPLIT
       // ballots of single compares, combined in SGPRs: a ballot of a combined
       // condition is re-materialised through a VGPR (v_cndmask + v_cmp) by the
-      // compiler, twice per iteration
+      // compiler, twice per iteration (C3 +2.5%: profiles/r5/ab_order_ballot.txt)
       const unsigned long long b_trav = __ballot(mode == M_TRAV), b_leaf = __ballot(tr.node < 0);
       const int n_leaf = __popcll(b_trav & b_leaf);
       const int n_node = __popcll(b_trav & ~b_leaf);
-#else
-      const int n_leaf = __popcll(__ballot(at_leaf));
-      const int n_node = __popcll(__ballot(trav && !at_leaf));
-#endif
       bool done = false;
-#if PT_SEL_SIMPLE
       // (n_leaf > 0 and n_node == 0 need no tests of their own: some lane
       // traverses, so n_leaf * w >= n_node * 16 is false for n_leaf == 0 and
       // true for n_node == 0 -- two scalar compare-and-branches fewer)
       const bool leaf_iter = n_leaf * t_leaf_weight >= n_node * 16;
-#else
-      const bool leaf_iter = n_leaf > 0 && (n_node == 0 || n_leaf * t_leaf_weight >= n_node * 16);
-#endif
       if (STATS && trav) {
         const bool stepped = leaf_iter == at_leaf;
         r_steps += stepped;
@@ -1917,11 +1550,10 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         if (STATS) n_leafit += lane == 0;
       } else if (trav && !at_leaf) {
         if constexpr (BIN) done = node_step2<STATS>(P.nodes2, stk, tr, ct);
-        else done = node_stepw<STATS>(t_nodes, t_nodes_hi, stk, tr, ct);
+        else done = node_step<STATS>(t_nodes, stk, tr, ct);
       }
       if (done) mode = M_SHADE;
       follow_on(done);
-      probe_insts<PT_PROBE_TRAV_SALU, PT_PROBE_TRAV_VALU>();
       if (STATS && done) {
         ray_steps_max = max(ray_steps_max, r_steps);
         ray_idle_max = max(ray_idle_max, r_idle);
@@ -2028,13 +1660,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   }
 }
 
-#if PT_KARG_ROUND
 #undef P
-#endif
 
-#ifndef PT_RESOLVE_WIDE
-#define PT_RESOLVE_WIDE 1
-#endif
 #if !PT_ENV_TU  // (pt_kernels_env.hip emits only the ENV render kernels)
 // Sums each pixel's sample groups in group order, so the sum is a fixed
 // function of the pixel, independent of scheduling and of the tile -> GPU
@@ -2047,12 +1674,10 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
   const int ti = (int)blockIdx.x;
   const int4 tile = P.tiles[ti];
   const int tid = (int)threadIdx.x;
-#if PT_RESOLVE_RESETS
   // the render that wrote these sums is complete, so are its queue claims:
   // zero the heads for the render slot's next launch (pt_api.cpp launch)
   if (ti == 0)
-    for (int i = tid; i < PT_QUEUE_WORDS * (PT_QUEUE_HEADS + 1); i += 256) P.work_counter[i] = 0u;
-#endif
+    for (int i = tid; i < PT_QUEUE_WORDS * PT_QUEUE_HEADS; i += 256) P.work_counter[i] = 0u;
   auto out_at = [&](int x, int y) -> float* {
     const size_t o = P.packed ? (size_t)ti * 1024u + (size_t)(y - tile.y) * 32u + (size_t)(x - tile.x)
                               : (size_t)x + (size_t)y * (size_t)P.W;
@@ -2069,8 +1694,7 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
     const int4 b = P.blocks[k];
     if (qx >= b.z || qy >= b.w) continue;
     float3 acc = f3(0, 0, 0);
-    const float* pa = P.partial + PT_SUM_WORDS * ((size_t)k * 64u + (size_t)q) * (size_t)P.n_groups;
-#if PT_RESOLVE_WIDE && PT_SUM_WORDS == 3
+    const float* pa = P.partial + 3 * ((size_t)k * 64u + (size_t)q) * (size_t)P.n_groups;
     if ((P.n_groups & 3) == 0) {
       // The pixel's run of n_groups 12-B sums (16-B aligned: 48 B per four
       // groups) read as 16-B vectors, four groups (three loads) per step: a
@@ -2091,19 +1715,16 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) acc = acc + f3(f[3 * g], f[3 * g + 1], f[3 * g + 2]);
       }
-    } else
-#endif
-    {
+    } else {
 #pragma unroll 2
-      for (int j = 0; j < P.n_groups; ++j) acc = acc + ld3(pa + PT_SUM_WORDS * (size_t)j);
+      for (int j = 0; j < P.n_groups; ++j) acc = acc + ld3(pa + 3 * (size_t)j);
     }
     store3(out_at(b.x + qx, b.y + qy), acc * inv_spp);
   }
 }
 
 // Batched BVHAccel::intersect queries, one lane per ray.
-__global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const void* __restrict__ nodes,
-                                                           const int4* __restrict__ nodes_hi,
+__global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const DNode* __restrict__ nodes,
                                                            const DPrim* __restrict__ prims, const float* __restrict__ o,
                                                            const float* __restrict__ d, const float* __restrict__ maxt,
                                                            int64_t n, int32_t* hit, float* t, int32_t* prim,
@@ -2118,12 +1739,12 @@ __global__ __launch_bounds__(PT_BLOCK) void intersect_kernel(const void* __restr
   h.t = 0;
   h.prim = -1;
   Counters ct = {0, 0, 0};
-  bool f = traverse<false>(nodes, nodes_hi, prims, stk, O, D, 3.0e38f, false, h, ct);
+  bool f = traverse<false>(nodes, prims, stk, O, D, 3.0e38f, false, h, ct);
   hit[i] = f ? 1 : 0;
   t[i] = f ? h.t : -1.0f;
   prim[i] = f ? (prim_map ? prim_map[h.prim] : h.prim) : -1;
   Hit h2;
-  bool a = traverse<false>(nodes, nodes_hi, prims, stk, O, D, maxt[i], true, h2, ct);
+  bool a = traverse<false>(nodes, prims, stk, O, D, maxt[i], true, h2, ct);
   anyhit[i] = a ? 1 : 0;
 }
 
@@ -2188,13 +1809,13 @@ extern "C" hipError_t ptk_launch_resolve(const KParams* P, hipStream_t s) {
   return hipGetLastError();
 }
 
-extern "C" hipError_t ptk_launch_intersect(const void* nodes, const int4* nodes_hi, const DPrim* prims, const float* o,
+extern "C" hipError_t ptk_launch_intersect(const DNode* nodes, const DPrim* prims, const float* o,
                                            const float* d, const float* maxt, int64_t n, int32_t* hit, float* t,
                                            int32_t* prim, int32_t* anyhit, int* spill, const int* prim_map,
                                            hipStream_t s) {
   int grid = (int)((n + PT_BLOCK - 1) / PT_BLOCK);
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL(ptk::intersect_kernel, dim3(grid), dim3(PT_BLOCK), 0, s, nodes, nodes_hi, prims, o, d, maxt, n,
+  hipLaunchKernelGGL(ptk::intersect_kernel, dim3(grid), dim3(PT_BLOCK), 0, s, nodes, prims, o, d, maxt, n,
                      hit, t, prim, anyhit, spill, prim_map);
   return hipGetLastError();
 }

@@ -19,6 +19,10 @@ collective:
     then rank 0 scatters the tiles into the frame.  The counter RNG keys
     every sample by (seed, pixel, sample), not by rank or schedule, so the
     assembled image is bit-identical to the 1-GPU image.
+  * back-to-back frames (PipelinedExchange): the packed buffer is double-
+    buffered and frame k's gather + scatter run on a side stream behind an
+    event, so they overlap frame k+1's render; frame k+2's render waits only
+    for frame k's gather to have read its buffer.
 """
 from __future__ import annotations
 
@@ -80,7 +84,7 @@ class TileExchange:
     current stream's work, not after the pt_ctx's own stream."""
 
     def __init__(self, tiles: Sequence[Tile], width: int, height: int, rank: int, world: int, device,
-                 dst: int = 0, group=None, deal: str = "diag"):
+                 dst: int = 0, group=None, deal: str = "diag", buffers: int = 1):
         import torch
 
         self.rank, self.world, self.dst, self.group = rank, world, dst, group
@@ -91,7 +95,10 @@ class TileExchange:
         self.deal = deal
         self.mine = shard_tiles(tiles, rank, world, deal)
         self.slots = max(len(shard_tiles(tiles, r, world, deal)) for r in range(world))
-        self.packed = torch.zeros((max(self.slots, 1), TILE * TILE, 3), dtype=torch.float32, device=device)
+        # `buffers` packed buffers (PipelinedExchange: 2); `packed` is the current one
+        self.bufs = [torch.zeros((max(self.slots, 1), TILE * TILE, 3), dtype=torch.float32, device=device)
+                     for _ in range(max(1, buffers))]
+        self.packed = self.bufs[0]
         self.recv = None
         if rank == dst:
             self.recv = torch.zeros((world, max(self.slots, 1), TILE * TILE, 3), dtype=torch.float32, device=device)
@@ -103,23 +110,28 @@ class TileExchange:
             self.src = torch.from_numpy(np.concatenate(src)).to(device)
             self.dstix = torch.from_numpy(np.concatenate(dstix)).to(device)
 
-    def gather(self):
-        """Every rank's packed tiles into `recv[rank]` on `dst` (one collective)."""
+    def gather(self, packed=None):
+        """Every rank's packed tiles (`packed`, default the current buffer)
+        into `recv[rank]` on `dst` (one collective; with an initialised process
+        group also at world size 1, so the RCCL path is the one a 1-GPU test
+        exercises)."""
         import torch
         import torch.distributed as dist
 
-        if self.world > 1 and self.packed.is_cuda and dist.get_backend(self.group) == "gloo":
+        packed = self.packed if packed is None else packed
+        coll = dist.is_available() and dist.is_initialized()
+        if coll and packed.is_cuda and dist.get_backend(self.group) == "gloo":
             # gloo gathers host tensors only (tests / one-GPU rehearsals)
-            src = self.packed.cpu()
+            src = packed.cpu()
             gl = [torch.empty_like(src) for _ in range(self.world)] if self.rank == self.dst else None
             dist.gather(src, gather_list=gl, dst=self.dst, group=self.group)
             if self.rank == self.dst:
                 self.recv.copy_(torch.stack(gl))
-        elif self.world > 1:
+        elif coll:
             gl = list(self.recv.unbind(0)) if self.rank == self.dst else None
-            dist.gather(self.packed, gather_list=gl, dst=self.dst, group=self.group)
+            dist.gather(packed, gather_list=gl, dst=self.dst, group=self.group)
         else:
-            self.recv[0].copy_(self.packed)
+            self.recv[0].copy_(packed)
 
     def scatter(self, frame):
         """On `dst`: the gathered tiles into their frame pixels."""
@@ -130,6 +142,75 @@ class TileExchange:
     def exchange(self, frame):
         self.gather()
         return self.scatter(frame)
+
+
+class PipelinedExchange:
+    """Back-to-back sharded frames with the exchange off the render's path.
+
+    Frame k renders into packed buffer k % 2 (`packed_for(k)`, called BEFORE
+    the render is queued: the current stream first waits until frame k-2's
+    gather has read that buffer); `exchange(k, frame)` then records an event
+    on the current stream (the render is done) and, on a side stream behind
+    it, gathers frame k's buffer onto `dst` and scatters it into `frame` --
+    while the current stream goes on with frame k+1's render.  `xev` collects
+    (start, end) events around each side-stream exchange.  Everything the side
+    stream does is ordered: gathers, the shared receive buffer and scatters
+    follow frame order.  On CPU tensors (tests) the same calls run
+    synchronously.  The images are those of TileExchange, bit for bit."""
+
+    def __init__(self, tiles: Sequence[Tile], width: int, height: int, rank: int, world: int, device,
+                 dst: int = 0, group=None, deal: str = "diag"):
+        import torch
+
+        self.ex = TileExchange(tiles, width, height, rank, world, device, dst=dst, group=group, deal=deal, buffers=2)
+        self.mine = self.ex.mine
+        self.cuda = self.ex.bufs[0].is_cuda
+        self.side = torch.cuda.Stream(device=self.ex.bufs[0].device) if self.cuda else None
+        self.free = [None, None]  # per buffer: event after the gather that last read it
+        self.xev = []
+
+    def packed_for(self, k: int):
+        import torch
+
+        b = k % 2
+        if self.cuda and self.free[b] is not None:
+            torch.cuda.current_stream().wait_event(self.free[b])
+        self.ex.packed = self.ex.bufs[b]
+        return self.ex.bufs[b]
+
+    def exchange(self, k: int, frame, timed: bool = False):
+        import torch
+
+        buf = self.ex.bufs[k % 2]
+        if not self.cuda:
+            self.ex.gather(buf)
+            return self.ex.scatter(frame)
+        done = torch.cuda.Event()
+        done.record()  # on the current (render) stream
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(done)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self.ex.gather(buf)
+            self.ex.scatter(frame)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            free = torch.cuda.Event()
+            free.record()
+        self.free[k % 2] = free
+        if timed:
+            self.xev.append((e0, e1))
+        return frame
+
+    def drain(self):
+        """The current stream waits for every exchange issued so far."""
+        import torch
+
+        if self.cuda:
+            torch.cuda.current_stream().wait_stream(self.side)
+
+    def exchange_ms(self) -> float:
+        return float(np.mean([a.elapsed_time(b) for a, b in self.xev])) if self.xev else 0.0
 
 
 def render_sharded(render_packed: Callable[[List[Tile], object], None], frame, tiles: Sequence[Tile], rank: int,

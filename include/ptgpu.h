@@ -198,7 +198,7 @@ typedef struct pt_stats {
   int64_t hitshade_clocks; /* of shade_clocks: hit records, NEE and bounces = section_clocks[0..2] */
   double resolve_ms;       /* device time of the sample-group resolve kernel */
   int32_t bvh_stack;       /* worst-case traversal stack entries of the uploaded BVH */
-  int64_t bvh_nodes;       /* render-tree nodes uploaded (8-wide; 4-wide in a PT_NODE_WIDTH=4 build) */
+  int64_t bvh_nodes;       /* render-tree (BVH4) nodes uploaded */
   int64_t section_clocks[4]; /* of shade_clocks: hit record, light sampling, BSDF sampling + sample
                                 completion, queue fetch (the rest of shade_clocks: camera rays and loop
                                 overhead) */

@@ -101,5 +101,49 @@ def golden(name: str) -> str:
     return os.path.join(GOLDEN, name)
 
 
+def box_downsample(img: np.ndarray, k: int = 8) -> np.ndarray:
+    """k x k box average of an (H, W, 3) image (H, W multiples of k)."""
+    h, w, c = img.shape
+    return img.astype(np.float64).reshape(h // k, k, w // k, k, c).mean(axis=(1, 3))
+
+
+def downsampled_rel_l2(img: np.ndarray, ref: np.ndarray, k: int = 8) -> float:
+    """SURVEY.md §8(c) criterion 3, last clause: ||D(img) - D(ref)|| / ||D(ref)||
+    over every channel of the k x k box-downsampled images."""
+    a, b = box_downsample(img, k), box_downsample(ref, k)
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+def statistical_report(img: np.ndarray, r1: np.ndarray, r2: np.ndarray) -> dict:
+    """img against the reference's two independent renders r1, r2 of the same
+    spp (SURVEY.md §8(c) criterion 3): mean per-pixel RGB-L2 distance and the
+    reference's own seed-to-seed floor, image-mean bias against 3 sigma of the
+    mean estimator, and the 8x8-box-downsampled relative L2 against each
+    reference render and its seed-to-seed value."""
+    img, r1, r2 = (x.astype(np.float64) for x in (img, r1, r2))
+    n = r1.shape[0] * r1.shape[1]
+    return {
+        "l2": float(np.linalg.norm(img - r1, axis=2).mean()),
+        "l2_floor": float(np.linalg.norm(r1 - r2, axis=2).mean()),
+        "bias": float(abs(img.mean() - r1.mean())),
+        "sigma": float((r1 - r2).mean(axis=2).std() / np.sqrt(n)),
+        "down_rel": [downsampled_rel_l2(img, r1), downsampled_rel_l2(img, r2)],
+        "down_rel_floor": downsampled_rel_l2(r1, r2),
+    }
+
+
+# SURVEY.md §8(c) criterion 3 at >= 256 spp: 8x8-box-downsampled relative L2 <= 2%
+DOWN_REL_MAX = 0.02
+
+
+def assert_statistical(rep: dict, high_spp: bool = False) -> None:
+    assert rep["l2"] <= 1.10 * rep["l2_floor"], rep
+    assert rep["bias"] <= 3 * rep["sigma"], rep
+    if high_spp:
+        assert max(rep["down_rel"]) <= DOWN_REL_MAX, rep
+        # and no further from the reference than its own other seed, within 10%
+        assert np.mean(rep["down_rel"]) <= 1.10 * rep["down_rel_floor"], rep
+
+
 def have_ref() -> bool:
     return os.path.exists(REF_DRIVER) and os.path.isdir("/root/reference")

@@ -61,6 +61,51 @@ def test_sharded_render_bit_identical(tmp_path, restate, world):
     assert np.array_equal(got, ref)
 
 
+def _pipe_worker(rank, world, port, out_path, seeds):
+    """Back-to-back frames through PipelinedExchange (the bench's N > 1 path):
+    frame k (seed seeds[k]) renders into packed buffer k % 2 and is gathered
+    into its own frame tensor."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dsgpuraytracing_amd.dist import PipelinedExchange
+    from tests.oracle_helpers import Restatement, golden
+    rs = Restatement()
+    scene = golden("c1_default_64x64.scene.ptd")
+    ntx = (W + 31) // 32
+    pex = PipelinedExchange(tile_fifo(W, H), W, H, rank, world, torch.device("cpu"))
+    frames = [torch.zeros((H, W, 3), dtype=torch.float32) for _ in seeds]
+    for k, seed in enumerate(seeds):
+        packed = pex.packed_for(k)
+        assert packed.data_ptr() == pex.ex.bufs[k % 2].data_ptr()
+        for i, (x, y, tw, th) in enumerate(pex.mine):
+            idx = (y // 32) * ntx + x // 32
+            img, _ = rs.render(scene, W, H, SPP, seed=seed, rng_mode=1, tile_begin=idx, tile_end=idx + 1)
+            packed[i].view(32, 32, 3)[:th, :tw] = torch.from_numpy(img[y:y + th, x:x + tw])
+        pex.exchange(k, frames[k], timed=True)
+    pex.drain()
+    if rank == 0:
+        np.save(out_path, torch.stack(frames).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pipelined_exchange_bit_identical_over_frames(tmp_path, restate, world):
+    """Double-buffered packed tiles, frame after frame: every assembled frame
+    equals the single-process render of its own seed bit for bit (a frame
+    gathered from the wrong buffer would carry another seed's pixels)."""
+    from tests.oracle_helpers import golden
+    seeds = [3, 5, 8]
+    out = str(tmp_path / "frames.npy")
+    mp.spawn(_pipe_worker, args=(world, _free_port(), out, seeds), nprocs=world, join=True)
+    got = np.load(out)
+    for k, seed in enumerate(seeds):
+        ref, _ = restate.render(golden("c1_default_64x64.scene.ptd"), W, H, SPP, seed=seed, rng_mode=1, threads=2)
+        assert np.array_equal(got[k], ref), k
+    assert not np.array_equal(got[0], got[1])
+
+
 @pytest.mark.parametrize("deal", ["mod", "diag", "diag3"])
 def test_shard_tiles_partition(deal):
     tiles = tile_fifo(1920, 1080)

@@ -72,3 +72,58 @@ def test_rccl_collectives_after_device_render():
     finally:
         dist.destroy_process_group()
         torch.cuda.set_stream(torch.cuda.default_stream(0))
+
+
+def test_pipelined_exchange_on_device_keeps_every_frame():
+    """bench.py's N > 1 default in its exact stream pattern on the box: frames
+    rendered back to back into double-buffered packed tiles, each frame's
+    RCCL gather + scatter on a side stream behind an event while the next
+    frame renders.  Every frame (its own seed) must equal its direct whole-
+    frame render bit for bit: a gather reading a buffer the next-but-one
+    render already overwrote, or a scatter racing the gather, would not."""
+    import torch
+    import torch.distributed as dist
+
+    from dsgpuraytracing_amd.dist import PipelinedExchange
+    from dsgpuraytracing_amd.pathtracer import Device, Scene, tile_fifo
+    from tests.oracle_helpers import golden
+
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream(device=0)
+    torch.cuda.set_stream(stream)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        w = h = 128
+        spp = 8
+        sc = Scene.from_dump(golden("c1_default_128x128.scene.ptd"))
+        dev = Device(0)
+        dev.upload_scene(sc)
+        dev.set_camera(sc.camera)
+        tiles = tile_fifo(w, h)
+        pex = PipelinedExchange(tiles, w, h, 0, 1, torch.device("cuda", 0))
+        mine = np.asarray(pex.mine, dtype=np.int32).reshape(-1, 4)
+        seeds = [11, 12, 13, 14, 15]
+        frames = [torch.zeros((h, w, 3), dtype=torch.float32, device="cuda:0") for _ in seeds]
+        for k, seed in enumerate(seeds):  # nothing waits on the host between frames
+            dev.set_params(w, h, spp, 4, 1, seed)
+            buf = pex.packed_for(k)
+            dev.render_tiles_device(mine, buf.data_ptr(), stream.cuda_stream, packed=True, out_floats=buf.numel())
+            pex.exchange(k, frames[k], timed=True)
+        pex.drain()
+        torch.cuda.synchronize()
+        assert pex.exchange_ms() > 0
+        whole = np.asarray(tiles, np.int32).reshape(-1, 4)
+        for k, seed in enumerate(seeds):
+            ref = torch.zeros_like(frames[k])
+            dev.set_params(w, h, spp, 4, 1, seed)
+            dev.render_tiles_device(whole, ref.data_ptr(), stream.cuda_stream)
+            torch.cuda.synchronize()
+            assert torch.equal(frames[k], ref), k
+            assert float(ref.mean()) > 0
+        assert not torch.equal(frames[0], frames[1])
+        dev.close()
+    finally:
+        dist.destroy_process_group()
+        torch.cuda.set_stream(torch.cuda.default_stream(0))
