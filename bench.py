@@ -610,7 +610,8 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
                                                         "leaf_steps", "wave_rounds", "queue_atomics", "shade_clocks",
                                                         "hitshade_clocks", "trav_clocks", "max_wave_clocks",
                                                         "wave_wall_sum", "wave_wall_max", "section_clocks", "wave_span",
-                                                        "lane_iters", "partial_bytes", "deep_stack_steps")},
+                                                        "lane_iters", "partial_bytes", "deep_stack_steps",
+                                                        "node_census")},
             "launch": {"grid_blocks": s_get(dev, "grid_blocks"), "block": 64,
                        "blocks_per_cu_query": s_get(dev, "blocks_per_cu"),
                        "bvh_nodes": s_get(dev, "bvh_nodes"), "bvh_stack": s_get(dev, "bvh_stack"),

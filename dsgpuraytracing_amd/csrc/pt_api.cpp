@@ -190,10 +190,14 @@ struct pt_ctx {
   // the next frame's waves fill the CUs the previous frame's drain leaves
   // idle.  Each resolve runs on the caller's stream after its own render, so
   // the caller's stream order is kept for everything it can observe.
-#ifndef PT_RENDER_SLOTS
-#define PT_RENDER_SLOTS 2
-#endif
-  static constexpr int kSlots = PT_RENDER_SLOTS;
+  // Small launches (a strong split's share of a frame: few work slots per
+  // resident lane) rotate over all kSlots slots, so up to four frames are in
+  // flight; larger ones over the first two (three slots measured C3 -6%, four
+  // -10%: profiles/r6/ab_render_slots.txt).  See launch(): small launches.
+  static constexpr int kSlots = 4;
+  static constexpr int kSlotsLarge = 2;
+  uint64_t slot_rr = 0;      // launches issued on the pipeline (slot rotation)
+  bool small_last = false;   // the previous launch was small: rotate over every slot
   hipStream_t rstream[kSlots] = {};
   hipEvent_t ev_free[kSlots] = {};
   DevBuf<int4> tiles[kSlots];
@@ -1129,7 +1133,8 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   // trace area, so it never overlaps another launch: it runs unpipelined too.
   static const bool pipeline = (!std::getenv("PT_PIPELINE") || std::atoi(std::getenv("PT_PIPELINE")) != 0);
   const bool census_launch = std::getenv("PT_CENSUS") && !stats;
-  const int slot = pipeline && !census_launch ? (int)(c->n_launches % pt_ctx::kSlots) : 0;
+  const int depth = c->small_last ? pt_ctx::kSlots : pt_ctx::kSlotsLarge;
+  const int slot = pipeline && !census_launch ? (int)(c->slot_rr++ % (uint64_t)depth) : 0;
   // A launch that finds every slot's last resolve complete has no frame to
   // overlap with: it runs on the caller's stream, with no cross-stream waits
   // in front of the render or between the render and the resolve (a lone
@@ -1311,6 +1316,23 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   const int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
   // (slot indices reach past the end by up to a static chunk plus a claimed one per wave)
   if (slots + 2 * want * PT_CHUNK_MAX >= (int64_t)INT32_MAX) return fail(PT_E_INVALID, "frame too large for one launch");
+  // Small launches: at most PT_SMALL_SLOTS work slots per lane of the whole
+  // resident grid (a strong split's share of the C3 frame: 12.8 at N = 2,
+  // 3.2 at N = 8; the whole C3 frame has 25.6).  Each lane then renders only
+  // a few slots, so a wave's slowest lane -- not the work -- sets the launch's
+  // time.  They claim 64 slots at a time (one per lane: no wave holds two
+  // while others have none), and when queued behind other frames they run on
+  // half the resident grid with up to kSlots frames in flight (more slots per
+  // lane per launch, the next frames filling each launch's tail).  Measured
+  // on the split's share (one-GPU emulation, profiles/r6/ab_small_launch*.txt):
+  // N = 8 0.38 -> 0.22 ms per frame, N = 4 0.51 -> 0.39, N = 2 0.75 -> 0.66.
+  // Neither the grid nor the claim changes a value (the sample grouping is
+  // a function of the frame).  PT_SMALL_LAUNCH=0 turns it off.
+  static const bool small_on = !std::getenv("PT_SMALL_LAUNCH") || std::atoi(std::getenv("PT_SMALL_LAUNCH")) != 0;
+  const bool small = small_on && pipeline && !census_launch && !stats &&
+                     slots <= (int64_t)PT_SMALL_SLOTS * c->grid_plain * PT_BLOCK;
+  if (!stats) c->small_last = small;
+  if (small && !gpu_idle && !std::getenv("PT_WAVES_PER_CU")) want = std::max<int64_t>(c->n_cu, want / 2);
   pt_fastdiv_init((uint32_t)P.n_groups, &P.grp_m, &P.grp_sh);
   // queue claims: bigger for frames with many slots per lane (fewer atomics
   // on the heads; a lone small frame's drain prefers the smaller claim)
@@ -1322,9 +1344,9 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   // (C3: 256-slot claims +2.9% pipelined, lone launch +9%:
   // profiles/r5/ab_chunk_heads.txt).  A claim size never changes a value.
   const bool big_frame = slots >= (int64_t)PT_CHUNK_BIG_SLOTS * want_plain * PT_BLOCK;
-  P.chunk = big_frame || (pipeline && !census_launch && !gpu_idle)
-                ? PT_CHUNK_MAX
-                : PT_CHUNK;
+  P.chunk = small ? PT_BLOCK
+          : big_frame || (pipeline && !census_launch && !gpu_idle) ? PT_CHUNK_MAX
+                                                                   : PT_CHUNK;
   // large frames claim PT_CHUNK_BIG (512) where the slot indices and the
   // one-block-per-chunk rule allow it: half the atomics again (C5 +1.0%, C4
   // +0.7%; C3's queued frames lose 7% at 512: profiles/r5/ab_chunk512.txt)
@@ -1443,6 +1465,7 @@ static int finish_stats(pt_ctx* c, hipStream_t s, uint32_t flags, bool sync) {
     for (int k = 0; k < 4; ++k) c->last.lane_iters[k] = (int64_t)v[27 + k];
     c->last.deep_stack_steps = (int64_t)v[31];
     for (int k = 0; k < 32; ++k) c->last.slot_latency_hist[k] = (int64_t)v[32 + k];
+    for (int k = 0; k < 8; ++k) c->last.node_census[k] = (int64_t)v[64 + k];
     for (int k = 0; k < 3; ++k) c->last.wave_span[k] = (int64_t)(v[22 + k] - v[21]);
     for (int k = 0; k < 2; ++k) c->last.wave_span[3 + k] = v[25 + k] ? (int64_t)(v[25 + k] - v[21]) : -1;
     c->last.counters_valid = 1;

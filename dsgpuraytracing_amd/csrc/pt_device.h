@@ -19,6 +19,9 @@
 #ifndef PT_BANDS_TREE_MIB
 #define PT_BANDS_TREE_MIB 8  // queue bands for large frames over render trees above this size (pt_api.cpp launch)
 #endif
+#ifndef PT_SMALL_SLOTS
+#define PT_SMALL_SLOTS 16  // launches with at most this many work slots per resident lane are small (pt_api.cpp launch)
+#endif
 #ifndef PT_CHUNK_BIG_SLOTS
 #define PT_CHUNK_BIG_SLOTS 128  // C4 (184 slots per lane) +1.5%, C5 (1,620) +6.6%; C3 (26), framed C3 (51): their lone launches lose
 #endif
@@ -165,7 +168,7 @@ __host__ __device__ inline int record_lower_bound(const float* __restrict__ a, f
 #ifndef PT_ENV_GUIDE
 #define PT_ENV_GUIDE 1024  // buckets of the environment-CDF guide tables (with the window compare: C5 +10% over 64, profiles/r3/ab_env_window_search.txt)
 #endif
-#define PT_STATS_SLOTS 64  // launch counters (32..63: slot-latency histograms); per-wave trace records (PT_WAVE_TRACE u64 each) follow
+#define PT_STATS_SLOTS 72  // launch counters (32..63: slot-latency histogram, 64..71: node-step census); per-wave trace records (PT_WAVE_TRACE u64 each) follow
 #define PT_WAVE_TRACE 11
 #ifndef PT_STACK
 #define PT_STACK 24  // traversal stack entries per lane in LDS (lane-contiguous)

@@ -824,6 +824,12 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // for the shading round, retired, stepping a leaf
   uint32_t l_other = 0, l_ready = 0, l_dead = 0, l_leaf = 0;
   uint32_t l_deep = 0;  // traversal lane-steps taken with stack entries in the global spill area
+  // node-step census (STATS, wave-uniform): main-loop wave node steps, of them
+  // with every stepping lane at ONE node, lanes at the first lane's node,
+  // stepping lanes, steps / lanes inside the top two / three BVH4 levels
+  // below the root (breadth-first node order: indices < 21 / < 85)
+  uint32_t c_wsteps = 0, c_uniform = 0, c_cover = 0, c_lanes = 0, c_top2w = 0, c_top2l = 0, c_top3w = 0,
+           c_top3l = 0;
   uint32_t n_atomics = 0;              // work-queue atomics (lane 0)
   uint32_t n_titer_drain = 0, n_rounds_drain = 0;  // of them: after this wave found the queue empty
   uint32_t chunk_next = 0, chunk_end = 0;  // the wave's private range of work slots
@@ -1534,6 +1540,24 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
         r_steps += stepped;
         r_idle += !stepped;
       }
+      if (STATS && !BIN) {  // node-step census (wave-uniform values)
+        const bool ns = trav && !at_leaf && !leaf_iter;
+        const unsigned long long nm = __ballot(ns);
+        if (nm != 0ull) {
+          const int fnode = __shfl(tr.node, __ffsll((long long)nm) - 1);
+          const unsigned long long same = __ballot(ns && tr.node == fnode);
+          const unsigned long long t2 = __ballot(ns && (uint32_t)tr.node < 21u);
+          const unsigned long long t3 = __ballot(ns && (uint32_t)tr.node < 85u);
+          ++c_wsteps;
+          c_uniform += same == nm;
+          c_cover += (uint32_t)__popcll(same);
+          c_lanes += (uint32_t)__popcll(nm);
+          c_top2w += t2 == nm;
+          c_top2l += (uint32_t)__popcll(t2);
+          c_top3w += t3 == nm;
+          c_top3l += (uint32_t)__popcll(t3);
+        }
+      }
       if (STATS) {  // what each lane does in this iteration (SIMD efficiency)
         l_other += trav && leaf_iter != at_leaf;
         l_ready += mode == M_SHADE;
@@ -1641,6 +1665,8 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
       }
       atomicAdd(P.stats + 14, w);
       atomicMax(P.stats + 15, w);
+      const uint32_t cn[8] = {c_wsteps, c_uniform, c_cover, c_lanes, c_top2w, c_top2l, c_top3w, c_top3l};
+      for (int k = 0; k < 8; ++k) atomicAdd(P.stats + 64 + k, (unsigned long long)cn[k]);
       // per-wave trace (pt_get_wave_trace): start, first empty queue, end,
       // (XCC id << 32 | HW_ID), camera samples
       unsigned long long* tw = P.stats + PT_STATS_SLOTS + PT_WAVE_TRACE * (size_t)wave_id;

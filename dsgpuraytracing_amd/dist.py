@@ -107,8 +107,18 @@ class TileExchange:
                 s, d = packed_index(shard_tiles(tiles, r, world, deal), width, slot0=r * max(self.slots, 1))
                 src.append(s)
                 dstix.append(d)
-            self.src = torch.from_numpy(np.concatenate(src)).to(device)
-            self.dstix = torch.from_numpy(np.concatenate(dstix)).to(device)
+            src, dstix = np.concatenate(src), np.concatenate(dstix)
+            self.src = torch.from_numpy(src).to(device)
+            self.dstix = torch.from_numpy(dstix).to(device)
+            # tiles covering the whole frame (every split of the FIFO): each
+            # frame pixel reads its one packed pixel -- ONE gather kernel
+            # straight into the frame, no temporary
+            self.perm = None
+            if len(dstix) == width * height:
+                perm = np.full(width * height, -1, np.int64)
+                perm[dstix] = src
+                if (perm >= 0).all():
+                    self.perm = torch.from_numpy(perm).to(device)
 
     def gather(self, packed=None):
         """Every rank's packed tiles (`packed`, default the current buffer)
@@ -135,8 +145,13 @@ class TileExchange:
 
     def scatter(self, frame):
         """On `dst`: the gathered tiles into their frame pixels."""
+        import torch
+
         if self.rank == self.dst:
-            frame.view(-1, 3).index_copy_(0, self.dstix, self.recv.view(-1, 3).index_select(0, self.src))
+            if self.perm is not None and frame.is_contiguous():
+                torch.index_select(self.recv.view(-1, 3), 0, self.perm, out=frame.view(-1, 3))
+            else:
+                frame.view(-1, 3).index_copy_(0, self.dstix, self.recv.view(-1, 3).index_select(0, self.src))
         return frame
 
     def exchange(self, frame):

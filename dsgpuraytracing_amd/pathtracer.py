@@ -164,6 +164,7 @@ class Device:
         out["wave_span"] = list(s.wave_span)
         out["lane_iters"] = list(s.lane_iters)
         out["footprint"] = list(s.footprint)
+        out["node_census"] = list(s.node_census)
         return out
 
     def launch_times(self, n: int = 256):

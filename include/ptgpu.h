@@ -223,6 +223,11 @@ typedef struct pt_stats {
   int64_t slot_latency_hist[32]; /* PT_FLAG_STATS: work slots by wall-clock latency (first camera ray to the
                               group's store), bucket b = [2^(b-1), 2^b) microseconds (0: < 1 us, 31: the
                               rest) */
+  int64_t node_census[8];  /* PT_FLAG_STATS: wave node steps of the traversal loop (root steps of fresh rays
+                              apart); of them with every stepping lane at one node (a scalar-load
+                              candidate); lanes at the first stepping lane's node; stepping lanes; steps and
+                              lanes inside the top two BVH4 levels below the root (node index < 21 in the
+                              breadth-first order); the same for three levels (< 85) */
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */

@@ -117,3 +117,27 @@ def test_kernel_sha_reads_the_device_code_section():
     assert elfsha.kernel_sha256(lib) != elfsha.file_sha256(lib)
     with pytest.raises(KeyError):
         elfsha.section_bytes(lib, ".no_such_section")
+
+
+def test_round6_line_reports_the_honest_rates():
+    """beside `value`, the line carries the rate of samples
+    actually traced (the footprint cull's samples excluded), one frame alone's
+    rate (W*H*spp / single_frame_ms) and the isolated launch's VALU-issue
+    fraction as roofline.frac_kernel."""
+    path = os.path.join(ROOT, "profiles", "r6", "bench_c3_default.jsonl")
+    with open(path) as f:
+        d = json.loads(f.read().strip().splitlines()[-1])
+    c, r = d["config"], d["roofline"]
+    whs = c["width"] * c["height"] * c["spp"]
+    culled = d["counters"]["culled_samples"]
+    assert 0 < culled < whs
+    assert d["traced_samples_per_s_M"] == pytest.approx((whs - culled) / (d["ms_per_step"] * 1e3), rel=0.01)
+    assert d["traced_samples_per_s_M"] < d["value"]
+    assert d["single_frame_Mrays"] == pytest.approx(whs / (c["single_frame_ms"] * 1e3), rel=0.01)
+    assert d["single_frame_Mrays"] < d["value"]  # one frame alone does not overlap a neighbour's drain
+    assert r["frac_kernel"] == r["views"]["valu"]["frac_isolated"]
+    assert 0.0 < r["frac_kernel"] <= 1.0
+    assert r["pmc_stale"] is False
+    # the node-step census of the STATS launch is on the line (VERDICT r5 item 3)
+    n = d["launch_counters"]["node_census"]
+    assert len(n) == 8 and n[0] > 0 and 0 <= n[1] <= n[0] and n[2] <= n[3]

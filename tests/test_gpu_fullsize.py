@@ -140,10 +140,19 @@ def test_fullframe_near_exact_vs_oracle(tmp_path, restate, name):
 
 
 # (name, lit tiles, mixed tiles, per-pixel near-exact fraction: SURVEY's 99.5% pooled
-# per kind, and at least TILE_FLOOR in every single tile).  C5 has an environment
-# light: no pixel is black, so its mixed tiles are those of the scene without the
-# environment light -- the silhouettes of the box and bunny against the sky.
-TILE_FLOOR = 0.985
+# per kind, and SURVEY's 99.5% in every single tile too -- TILE_FLOOR -- except the
+# tiles named in TILE_EXCEPTIONS).  C5 has an environment light: no pixel is black,
+# so its mixed tiles are those of the scene without the environment light -- the
+# silhouettes of the box and bunny against the sky.
+TILE_FLOOR = 0.995
+# Sampled tiles below 99.5%, each with its sample-by-sample census
+# (tools/silhouette_samples.py): every off pixel differs by ONE sample whose path
+# took another turn at a silhouette (fp32 vs fp64 hit decisions at grazing
+# incidence), and that sample's difference / spp is the pixel's.
+TILE_EXCEPTIONS = {
+    ("c4", (1088, 192)): 0.985,  # 0.9883 on the box: profiles/r4/silhouette_c4_1088_192.txt
+    ("c5", (800, 416)): 0.99,    # 0.9932 on the box: profiles/r6/silhouette_c5_800_416.txt
+}
 
 
 @pytest.mark.parametrize("name,k,k_mixed,min_close", [
@@ -186,7 +195,8 @@ def test_fullsize_sampled_tiles_match_oracle(tmp_path, restate, name, k, k_mixed
               f"  {close * 100:.3f}% pixels within 1e-3, sampled-tile mean rel diff {rel_mean:.2e}, "
               f"{int(black.sum())} black reference pixels")
         assert close >= min_close, (kind, closes)
-        assert min(closes) >= TILE_FLOOR, (kind, sel, closes)
+        for (x, y), c in zip(sel, closes):
+            assert c >= TILE_EXCEPTIONS.get((name, (x, y)), TILE_FLOOR), (kind, (x, y), c)
         assert rel_mean <= 1e-3, (kind, rel_mean)
         if black.any():
             assert (gflat[black] == 0).mean() >= min_close, kind
@@ -267,3 +277,37 @@ def test_c4_fullsize_eight_way_split_bit_identical():
         parts += p
     assert np.array_equal(parts, full)
     assert full.mean() > 0
+
+
+def test_c3_small_launch_shape_never_changes_values(monkeypatch):
+    """The small-launch shape (pt_api.cpp launch: a strong split's share has
+    few work slots per lane, so it claims 64 slots at a time and, queued
+    behind other frames, runs on half the resident grid with up to four
+    frames in flight) changes only which wave renders which slot: the C3
+    frame's 8-way diagonal shares, queued back to back on one stream (the
+    bench's N > 1 pattern), reassemble the whole frame -- a large launch --
+    bit for bit, and equal the shares rendered with the shape turned off."""
+    import torch
+    dae, envmap, w, h, spp = _workload("c3")
+    dev = _device(dae, envmap, w, h, spp, seed=6)
+    stream = torch.cuda.Stream(device=0)
+    whole = np.asarray(tile_fifo(w, h), np.int32).reshape(-1, 4)
+    full = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda:0")
+    dev.render_tiles_device(whole, full.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize()
+
+    def split(n_rounds=2):
+        parts = [torch.zeros_like(full) for _ in range(8)]
+        for _ in range(n_rounds):  # queued: every launch after the first finds the GPU busy
+            for r in range(8):
+                share = np.asarray(shard_tiles(tile_fifo(w, h), r, 8, "diag"), np.int32).reshape(-1, 4)
+                dev.render_tiles_device(share, parts[r].data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        return torch.stack(parts).sum(0)
+
+    monkeypatch.delenv("PT_SMALL_LAUNCH", raising=False)
+    small = split()
+    assert torch.equal(small, full)
+    monkeypatch.setenv("PT_SMALL_LAUNCH", "0")
+    assert torch.equal(split(), full)
+    assert float(full.mean()) > 0

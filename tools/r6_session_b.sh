@@ -13,3 +13,5 @@ timeout -k 10 900 bash tools/rehearse_dist.sh > gpurun_out/r6b_rehearse.txt 2>&1
 cat gpurun_out/r6b_rehearse.txt
 timeout -k 10 900 bash tools/profile_session.sh c3 5 gpurun_out/prof_c3 > gpurun_out/r6b_prof.log 2>&1 || { tail -30 gpurun_out/r6b_prof.log; exit 1; }
 tail -5 gpurun_out/r6b_prof.log
+timeout -k 10 600 python tools/silhouette_samples.py --workload c5 --tile 800,416 > gpurun_out/r6b_silhouette_c5.txt 2>&1 || { tail -20 gpurun_out/r6b_silhouette_c5.txt; exit 1; }
+tail -15 gpurun_out/r6b_silhouette_c5.txt
