@@ -280,9 +280,15 @@ int pt_create(int device, pt_ctx** out) {
   c->device = device;
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   for (int k = 0; k < pt_ctx::kSlots; ++k) {
-    HIPCHK(hipStreamCreateWithFlags(&c->rstream[k], hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
-    HIPCHK(hipEventRecord(c->ev_free[k], c->stream));
+    // (slots past the first two get their stream when a small launch first
+    // uses them: HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues, 4 by
+    // default, and two more streams per context put the render streams of
+    // large frames on shared queues -- C3 pipelined -12%)
+    if (k < pt_ctx::kSlotsLarge) {
+      HIPCHK(hipStreamCreateWithFlags(&c->rstream[k], hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
+      HIPCHK(hipEventRecord(c->ev_free[k], c->stream));
+    }
     HIPCHK(c->counter[k].reserve(PT_QUEUE_WORDS * PT_QUEUE_HEADS));  // work-queue heads, one 128-B line each
   }
   for (auto& tri : c->ev)
@@ -1143,6 +1149,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   // here instead of being absorbed into the choice.
   bool gpu_idle = true;  // no earlier render of this context still running or queued
   for (int k = 0; k < pt_ctx::kSlots && gpu_idle; ++k) {
+    if (!c->ev_free[k]) continue;  // (a slot never used)
     const hipError_t q = hipEventQuery(c->ev_free[k]);
     if (q == hipErrorNotReady) {
       (void)hipGetLastError();  // (a not-ready query is no error of this launch)
@@ -1152,6 +1159,11 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
     }
   }
   const bool idle = pipeline && !census_launch && gpu_idle;
+  if (!c->rstream[slot]) {  // a small launch's first use of slots 2 and 3
+    HIPCHK(hipStreamCreateWithFlags(&c->rstream[slot], hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_free[slot], hipEventDisableTiming));
+    HIPCHK(hipEventRecord(c->ev_free[slot], c->stream));
+  }
   hipStream_t rs = pipeline && !census_launch && !idle ? c->rstream[slot] : s;
   // the slot's device state is free once the previous resolve that read it ran
   if (!idle) HIPCHK(hipStreamWaitEvent(rs, c->ev_free[slot], 0));

@@ -4,7 +4,7 @@
 # (efficiency is null here: the ranks share one device); companions c4_strong and c3_weak.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
-for n in 2 4; do
+for n in ${REHEARSE_N:-2 4}; do
   PT_DIST_BACKEND=gloo PT_BENCH_DEVICE=0 timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
     --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py --gpus $n --steps 5 --warmup 2 > gpurun_out/rehearse_$n.log 2>&1 || { tail -30 gpurun_out/rehearse_$n.log; exit 1; }
   tail -n 1 gpurun_out/rehearse_$n.log | python3 -c "
