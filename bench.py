@@ -560,7 +560,9 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
             value = float(np.sum(mine_arr[:, 2] * mine_arr[:, 3])) * SPP * frames / elapsed / 1e6
         avg_ms = float(np.mean(kernel_ms))
         img = frame.float().cpu().numpy()
-        scaling = ("weak" if weak else "strong") if world > 1 else "weak"
+        # at N = 1 the line names the curve it starts (the driver's N > 1 runs
+        # use the same default, the C3 frame split)
+        scaling = "weak" if weak else "strong" if world > 1 else args.scaling
         out = {
             "metric": HEADLINE_METRIC if workload == "c3" else f"Mrays/sec + wall-clock render time, {wl['desc']}",
             "value": round(value, 3),
