@@ -360,11 +360,18 @@ def main():
         print(f"[bench rank {rank}] aborted: {e}", file=sys.stderr, flush=True)
         if rank == 0:
             print(json.dumps({"metric": HEADLINE_METRIC, "value": None, "error": str(e), "n_gpus": world}), flush=True)
-        if world > 1:
+        if dist.is_initialized():
             dist.destroy_process_group()
         sys.exit(3)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def xchg_opts():
+    """The strong split's exchange: on the current stream behind the resolve
+    (default), or on a side stream with PT_XCHG_SIDE=1 (A/Bs:
+    profiles/r6/ab_stream_queues.txt)."""
+    return {"side": os.environ.get("PT_XCHG_SIDE", "0") == "1"}
 
 
 def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, check_value_knobs, shard_tiles):
@@ -407,12 +414,13 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
         mine_arr = np.asarray(shard_tiles(tiles, args.emulate_rank, args.emulate_shard, "diag"),
                               dtype=np.int32).reshape(-1, 4)
     # strong: double-buffered packed tiles, the gather on a side stream
-    pex = PipelinedExchange(tiles, W, H, rank, world, frame.device) if world > 1 and not weak else None
+    pex = PipelinedExchange(tiles, W, H, rank, world, frame.device, **xchg_opts()) if world > 1 and not weak else None
     if args.emulate_shard > 1:
         # one rank's share through the same packed render + side-stream
         # exchange (here a device copy of the share's packed tiles and their
         # scatter: the gather's link time is not in it), host overheads included
-        pex = PipelinedExchange([tuple(int(v) for v in t) for t in mine_arr], W, H, 0, 1, frame.device)
+        pex = PipelinedExchange([tuple(int(v) for v in t) for t in mine_arr], W, H, 0, 1, frame.device,
+                                **xchg_opts())
     if pex is not None:
         mine_arr = np.asarray(pex.mine, dtype=np.int32).reshape(-1, 4)
 
@@ -762,7 +770,7 @@ def multi_gpu_companions(local, rank, world, backend, StepGuard, PipelinedExchan
     dev.set_params(w, h, spp, DEPTH, NSL, SEED)
     frame = torch.zeros((h, w, 3), dtype=torch.float32, device=f"cuda:{local}")
     tiles = tile_fifo(w, h)
-    pex = PipelinedExchange(tiles, w, h, rank, world, frame.device)
+    pex = PipelinedExchange(tiles, w, h, rank, world, frame.device, **xchg_opts())
     mine = np.asarray(pex.mine, dtype=np.int32).reshape(-1, 4)
     guard = StepGuard()
     kf = [0]

@@ -152,6 +152,17 @@ void build_env_tables(const float* rgb, int w, int h, EnvTables& t) {
   for (int y = 0; y < h; y++)
     build_records(&t.p_phi[(size_t)y * w], &t.g_phi[(size_t)y * (PT_ENV_GUIDE + 1)], &t.r_phi[(size_t)y * PT_ENV_GUIDE]);
 }
+
+// Render-slot streams: plain non-blocking streams at normal priority.  HIP
+// keeps one pool of GPU_MAX_HW_QUEUES (= 4) hardware queues per stream
+// priority and gives a new stream the least-used queue of its pool; kernel
+// traces and A/Bs of the C3 split's shares (profiles/r6/ab_stream_queues.txt)
+// put render slots at high priority, on CU-masked queues of their own, or
+// the caller's stream at high priority: every arm that keeps more than four
+// hardware queues busy -- counting torch's collective stream on a rank of an
+// N-GPU run -- was slower (N = 8 share 0.22 -> 0.29-0.38 ms per frame).
+static hipError_t make_render_stream(hipStream_t* s) { return hipStreamCreateWithFlags(s, hipStreamNonBlocking); }
+
 #pragma clang fp contract(on)
 
 }  // namespace
@@ -285,7 +296,7 @@ int pt_create(int device, pt_ctx** out) {
     // default, and two more streams per context put the render streams of
     // large frames on shared queues -- C3 pipelined -12%)
     if (k < pt_ctx::kSlotsLarge) {
-      HIPCHK(hipStreamCreateWithFlags(&c->rstream[k], hipStreamNonBlocking));
+      HIPCHK(make_render_stream(&c->rstream[k]));
       HIPCHK(hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
       HIPCHK(hipEventRecord(c->ev_free[k], c->stream));
     }
@@ -1160,7 +1171,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   }
   const bool idle = pipeline && !census_launch && gpu_idle;
   if (!c->rstream[slot]) {  // a small launch's first use of slots 2 and 3
-    HIPCHK(hipStreamCreateWithFlags(&c->rstream[slot], hipStreamNonBlocking));
+    HIPCHK(make_render_stream(&c->rstream[slot]));
     HIPCHK(hipEventCreateWithFlags(&c->ev_free[slot], hipEventDisableTiming));
     HIPCHK(hipEventRecord(c->ev_free[slot], c->stream));
   }

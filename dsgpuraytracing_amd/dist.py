@@ -163,24 +163,32 @@ class PipelinedExchange:
     """Back-to-back sharded frames with the exchange off the render's path.
 
     Frame k renders into packed buffer k % 2 (`packed_for(k)`, called BEFORE
-    the render is queued: the current stream first waits until frame k-2's
-    gather has read that buffer); `exchange(k, frame)` then records an event
-    on the current stream (the render is done) and, on a side stream behind
-    it, gathers frame k's buffer onto `dst` and scatters it into `frame` --
-    while the current stream goes on with frame k+1's render.  `xev` collects
-    (start, end) events around each side-stream exchange.  Everything the side
-    stream does is ordered: gathers, the shared receive buffer and scatters
-    follow frame order.  On CPU tensors (tests) the same calls run
-    synchronously.  The images are those of TileExchange, bit for bit."""
+    the render is queued); `exchange(k, frame)` gathers frame k's buffer onto
+    `dst` and scatters it into `frame`.  The renders themselves run on the
+    library's render-slot streams (pt_api.cpp), so frame k+1's render overlaps
+    frame k's resolve and exchange whichever stream the exchange is queued on.
+    Default: on the current stream, right behind frame k's resolve (ordered,
+    no cross-stream hop; one packed buffer would do).  side=True: on a side
+    stream behind an event (the current stream first waits, in
+    `packed_for(k)`, until frame k-2's gather has read that buffer) -- kept
+    for A/Bs.  `xev` collects (start, end) events around each exchange.
+    Gathers, the shared receive buffer and scatters follow frame order.  On
+    CPU tensors (tests) the same calls run synchronously.  The images are
+    those of TileExchange, bit for bit."""
 
     def __init__(self, tiles: Sequence[Tile], width: int, height: int, rank: int, world: int, device,
-                 dst: int = 0, group=None, deal: str = "diag"):
+                 dst: int = 0, group=None, deal: str = "diag", side: bool = False):
         import torch
 
         self.ex = TileExchange(tiles, width, height, rank, world, device, dst=dst, group=group, deal=deal, buffers=2)
         self.mine = self.ex.mine
         self.cuda = self.ex.bufs[0].is_cuda
-        self.side = torch.cuda.Stream(device=self.ex.bufs[0].device) if self.cuda else None
+        # side=False (default): the exchange is queued on the current stream
+        # right behind the resolve -- no cross-stream hop between them: the
+        # C4 split's N = 8 share 2.13 -> 1.86 ms per frame, the C3 shares
+        # even (profiles/r6/ab_stream_queues.txt, sessions v and w)
+        self.side = torch.cuda.Stream(device=self.ex.bufs[0].device) if self.cuda and side else None
+        self.on_current = self.cuda and not side
         self.free = [None, None]  # per buffer: event after the gather that last read it
         self.xev = []
 
@@ -200,6 +208,16 @@ class PipelinedExchange:
         if not self.cuda:
             self.ex.gather(buf)
             return self.ex.scatter(frame)
+        if self.on_current:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self.ex.gather(buf)
+            self.ex.scatter(frame)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            if timed:
+                self.xev.append((e0, e1))
+            return frame
         done = torch.cuda.Event()
         done.record()  # on the current (render) stream
         with torch.cuda.stream(self.side):
@@ -221,7 +239,7 @@ class PipelinedExchange:
         """The current stream waits for every exchange issued so far."""
         import torch
 
-        if self.cuda:
+        if self.side is not None:
             torch.cuda.current_stream().wait_stream(self.side)
 
     def exchange_ms(self) -> float:
@@ -357,8 +375,16 @@ def init_from_env(backend: str, timeout_s: float | None = None):
     if timeout_s is None:
         timeout_s = float(os.environ.get("PT_DIST_TIMEOUT", DEFAULT_TIMEOUT_S))
     timeout = datetime.timedelta(seconds=timeout_s)
-    if world > 1 and not dist.is_initialized():
+    # PT_DIST_FORCE=1 (experiments): a one-rank group, so that a one-GPU run
+    # (bench.py --emulate-shard) issues its exchange through RCCL and torch's
+    # collective stream, as every rank of an N-GPU run does
+    force = os.environ.get("PT_DIST_FORCE") == "1"
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:
+            os.environ.setdefault("MASTER_PORT", "29531")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":  # RCCL: bind the group to this rank's GPU (eager communicator init)
             import torch
             dist.init_process_group(backend, timeout=timeout,

@@ -74,11 +74,13 @@ def test_rccl_collectives_after_device_render():
         torch.cuda.set_stream(torch.cuda.default_stream(0))
 
 
-def test_pipelined_exchange_on_device_keeps_every_frame():
+@pytest.mark.parametrize("side", [False, True])
+def test_pipelined_exchange_on_device_keeps_every_frame(side):
     """bench.py's N > 1 default in its exact stream pattern on the box: frames
-    rendered back to back into double-buffered packed tiles, each frame's
-    RCCL gather + scatter on a side stream behind an event while the next
-    frame renders.  Every frame (its own seed) must equal its direct whole-
+    rendered back to back (on the library's render-slot streams) into
+    double-buffered packed tiles, each frame's RCCL gather + scatter queued
+    behind its resolve on the current stream (side=False, the default) or on
+    a side stream behind an event (side=True) while the next frame renders.  Every frame (its own seed) must equal its direct whole-
     frame render bit for bit: a gather reading a buffer the next-but-one
     render already overwrote, or a scatter racing the gather, would not."""
     import torch
@@ -102,7 +104,7 @@ def test_pipelined_exchange_on_device_keeps_every_frame():
         dev.upload_scene(sc)
         dev.set_camera(sc.camera)
         tiles = tile_fifo(w, h)
-        pex = PipelinedExchange(tiles, w, h, 0, 1, torch.device("cuda", 0))
+        pex = PipelinedExchange(tiles, w, h, 0, 1, torch.device("cuda", 0), side=side)
         mine = np.asarray(pex.mine, dtype=np.int32).reshape(-1, 4)
         seeds = [11, 12, 13, 14, 15]
         frames = [torch.zeros((h, w, 3), dtype=torch.float32, device="cuda:0") for _ in seeds]
