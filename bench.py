@@ -18,9 +18,9 @@ the scene.
     over the GPUs ("scaling": "strong", north_star's "near-linear tile
     scaling"): the frame's 32x32 tiles dealt diagonally, each rank rendering
     its tiles into a packed buffer, then ONE RCCL gather of the packed tiles
-    onto rank 0, pipelined: frame k's gather + scatter run
-    on a side stream behind an event while frame k+1 renders (double-
-    buffered packed tiles, dist.PipelinedExchange); value = W*H*64 *
+    onto rank 0, pipelined: frame k's gather + scatter are
+    queued behind its resolve on the current stream while frame k+1 renders
+    on the library's render-slot streams (dist.PipelinedExchange); value = W*H*64 *
     frames / max-rank time, the image bit-identical to the 1-GPU image.
     `efficiency` = value / (N * rate_1), rate_1 measured by rank 0 rendering
     the whole frame alone behind a barrier (null when ranks share a device).
@@ -413,12 +413,13 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
     if args.emulate_shard > 1:
         mine_arr = np.asarray(shard_tiles(tiles, args.emulate_rank, args.emulate_shard, "diag"),
                               dtype=np.int32).reshape(-1, 4)
-    # strong: double-buffered packed tiles, the gather on a side stream
+    # strong: packed tiles, the gather queued behind each frame's resolve
     pex = PipelinedExchange(tiles, W, H, rank, world, frame.device, **xchg_opts()) if world > 1 and not weak else None
     if args.emulate_shard > 1:
-        # one rank's share through the same packed render + side-stream
-        # exchange (here a device copy of the share's packed tiles and their
-        # scatter: the gather's link time is not in it), host overheads included
+        # one rank's share through the same packed render + exchange (here a
+        # device copy of the share's packed tiles and their scatter -- through
+        # a one-rank RCCL group with PT_DIST_FORCE=1 -- the gather's link time
+        # is not in it), host overheads included
         pex = PipelinedExchange([tuple(int(v) for v in t) for t in mine_arr], W, H, 0, 1, frame.device,
                                 **xchg_opts())
     if pex is not None:
@@ -495,7 +496,7 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
     for _ in range(args.steps):  # asynchronous: nothing waits on the GPU inside a step
         step(timed=True)
     if pex is not None:
-        pex.drain()  # (the render stream waits for the last side-stream exchange)
+        pex.drain()  # (with PT_XCHG_SIDE=1: the current stream waits for the last side-stream exchange)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -653,8 +654,10 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
             out["single_gpu_value"] = None if rate1 is None else round(rate1, 1)
             out["efficiency"] = None if (rate1 is None or shared) else round(value / (world * rate1), 4)
             out["shared_device"] = shared
-            out["exchange"] = "pipelined: packed-tile gather + scatter of frame k on a side stream behind an event, " \
-                              "overlapping frame k+1's render (double-buffered packed tiles)"
+            out["exchange"] = ("pipelined: packed-tile gather + scatter of frame k queued behind its resolve, "
+                               "overlapping frame k+1's render (render-slot streams)" if not pex.side else
+                               "pipelined: packed-tile gather + scatter of frame k on a side stream behind an event, "
+                               "overlapping frame k+1's render (double-buffered packed tiles)")
             if per_rank:
                 kms = [r[0] for r in per_rank]
                 out["kernel_ms_slowest_over_mean"] = round(max(kms) / max(1e-9, float(np.mean(kms))), 4)
@@ -746,7 +749,7 @@ def multi_gpu_companions(local, rank, world, backend, StepGuard, PipelinedExchan
     ranks):
       * c4_strong: BASELINE C4 (1080p, 256 spp, the multi-GPU config), its
         32x32 tiles dealt diagonally over the N GPUs, packed tiles gathered
-        onto rank 0 on a side stream while the next frame renders (SURVEY.md
+        onto rank 0 behind each frame's resolve while the next frame renders (SURVEY.md
         §8(e)); efficiency against rank 0 rendering the whole frame alone;
         images bit-identical to 1 GPU (tests/test_dist.py,
         test_c4_fullsize_eight_way_split_bit_identical);

@@ -19,10 +19,10 @@ collective:
     then rank 0 scatters the tiles into the frame.  The counter RNG keys
     every sample by (seed, pixel, sample), not by rank or schedule, so the
     assembled image is bit-identical to the 1-GPU image.
-  * back-to-back frames (PipelinedExchange): the packed buffer is double-
-    buffered and frame k's gather + scatter run on a side stream behind an
-    event, so they overlap frame k+1's render; frame k+2's render waits only
-    for frame k's gather to have read its buffer.
+  * back-to-back frames (PipelinedExchange): frame k's gather + scatter are
+    queued behind its resolve on the current stream; the renders run on the
+    library's render-slot streams, so they overlap frame k+1's render (a
+    side-stream variant behind events is kept for A/Bs).
 """
 from __future__ import annotations
 
