@@ -327,6 +327,11 @@ def main():
     ap.add_argument("--emulate-shard", type=int, default=0,
                     help="diagnostic: render only one rank's share of an N-GPU split on this one GPU")
     ap.add_argument("--emulate-rank", type=int, default=0, help="the rank --emulate-shard renders")
+    ap.add_argument("--frames-per-launch", type=int, default=0,
+                    help="frames rendered per launch (pt_render_frames_device, 1..8; the library renders frames "
+                         "of more than 32 work slots per lane one per launch): a frame batch shares one "
+                         "persistent launch, so a small frame's drain is filled with the next frame's work. "
+                         "Default: 8 for the strong split's shares (N > 1, --emulate-shard), 1 for N = 1")
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
                     help="N > 1: strong = one frame's tiles split across the GPUs + one pipelined RCCL gather "
                          "(default; BASELINE C4: --workload c4); weak = one pass of the whole frame per GPU over "
@@ -414,14 +419,17 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
         mine_arr = np.asarray(shard_tiles(tiles, args.emulate_rank, args.emulate_shard, "diag"),
                               dtype=np.int32).reshape(-1, 4)
     # strong: packed tiles, the gather queued behind each frame's resolve
-    pex = PipelinedExchange(tiles, W, H, rank, world, frame.device, **xchg_opts()) if world > 1 and not weak else None
+    fpl = args.frames_per_launch or (8 if (world > 1 and not weak) or args.emulate_shard > 1 else 1)
+    fpl = max(1, min(8, fpl))
+    pex = (PipelinedExchange(tiles, W, H, rank, world, frame.device, buffers=max(2, fpl), **xchg_opts())
+           if world > 1 and not weak else None)
     if args.emulate_shard > 1:
         # one rank's share through the same packed render + exchange (here a
         # device copy of the share's packed tiles and their scatter -- through
         # a one-rank RCCL group with PT_DIST_FORCE=1 -- the gather's link time
         # is not in it), host overheads included
         pex = PipelinedExchange([tuple(int(v) for v in t) for t in mine_arr], W, H, 0, 1, frame.device,
-                                **xchg_opts())
+                                buffers=max(2, fpl), **xchg_opts())
     if pex is not None:
         mine_arr = np.asarray(pex.mine, dtype=np.int32).reshape(-1, 4)
 
@@ -468,6 +476,29 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
             pex.exchange(k, frame, timed=timed)
         return guard.run(dev.stats) if stats else None
 
+    def steps(n, timed=False):
+        """n frames: with --frames-per-launch F > 1 in frame batches of up to F
+        frames per launch (pt_render_frames_device; the same images), each
+        frame then exchanged as step() does."""
+        if fpl <= 1 or weak:
+            for _ in range(n):
+                step(timed=timed)
+            return
+        done = 0
+        while done < n:
+            m = min(fpl, n - done)
+            if pex is None:
+                guard.run(dev.render_frames_device, mine_arr, [frame.data_ptr()] * m, [SEED] * m, stream)
+            else:
+                ks = list(range(kframe[0], kframe[0] + m))
+                kframe[0] += m
+                bufs = [pex.packed_for(k) for k in ks]
+                guard.run(dev.render_frames_device, mine_arr, [b.data_ptr() for b in bufs], [SEED] * m, stream,
+                          packed=True, out_floats=bufs[0].numel())
+                for k in ks:
+                    pex.exchange(k, frame, timed=timed)
+            done += m
+
     # counters for the roofline's algorithmic bytes: the reference's binary BVH
     # (SURVEY.md §8(d) cost model); and the launch's own counters (4-wide BVH)
     st_counts = step(stats="ref")
@@ -486,15 +517,13 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
         frame[y1 + 1:].zero_()
     # the ranks must group each pixel's samples alike (bit-identical frame)
     knobs = check_value_knobs({"group_spp": st_perf["group_spp"]})
-    for _ in range(args.warmup):
-        step()
+    steps(args.warmup)
     guard.check()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):  # asynchronous: nothing waits on the GPU inside a step
-        step(timed=True)
+    steps(args.steps, timed=True)  # asynchronous: nothing waits on the GPU inside a step
     if pex is not None:
         pex.drain()  # (with PT_XCHG_SIDE=1: the current stream waits for the last side-stream exchange)
     if world > 1:
@@ -503,7 +532,10 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
     elapsed = time.perf_counter() - t0
     guard.check()
     # HIP events recorded around every launch on its stream (the timed ones)
-    kernel_ms, resolve_ms = dev.launch_times(args.steps)
+    n_launch = args.steps if fpl <= 1 or weak else -(-args.steps // fpl)
+    kernel_ms, resolve_ms = dev.launch_times(n_launch)
+    if n_launch != args.steps:  # (a frame batch's launch and resolves: per frame)
+        kernel_ms, resolve_ms = kernel_ms * n_launch / args.steps, resolve_ms * n_launch / args.steps
     xchg_ms = float(np.mean([a.elapsed_time(b) for a, b in xev])) if xev else 0.0
     if pex is not None:
         xchg_ms = pex.exchange_ms()
@@ -511,7 +543,7 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
     # frame alone behind a barrier (the other ranks idle), same clock and frames
     rate1, shared = None, False
     if world > 1 and not weak:
-        rate1, shared = single_gpu_rate(dev, tiles, W, H, SPP, frame, stream, rank, backend, args.steps)
+        rate1, shared = single_gpu_rate(dev, tiles, W, H, SPP, frame, stream, rank, backend, args.steps, fpl=fpl)
     per_rank = None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else f"cuda:{local}")
@@ -533,6 +565,7 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
 
     host_ms = None
     single_ms = None
+    frame_batch = None
     iso_ms = 0.0
     if world == 1:
         # one frame alone, synchronised on both sides (no overlap with a
@@ -562,6 +595,20 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
         for _ in range(2):
             dev.render_tiles(mine_arr, host)
         host_ms = (time.perf_counter() - t0h) / 2 * 1e3
+        # the same frame in batches of 8 per launch (pt_render_frames_device),
+        # as the N > 1 line renders its shares: the like-for-like 1-GPU point
+        # of that curve (its own single_gpu_value measures the same)
+        if args.emulate_shard <= 1:
+            nb = 64
+            dev.render_frames_device(mine_arr, [frame.data_ptr()] * 8, [SEED] * 8, stream)  # (warm-up)
+            torch.cuda.synchronize()
+            t0b = time.perf_counter()
+            for _ in range(nb // 8):
+                dev.render_frames_device(mine_arr, [frame.data_ptr()] * 8, [SEED] * 8, stream)
+            torch.cuda.synchronize()
+            elb = time.perf_counter() - t0b
+            frame_batch = {"frames_per_launch": 8, "frames": nb, "ms_per_step": round(elb / nb * 1e3, 4),
+                           "value": round(W * H * SPP * nb / elb / 1e6, 1)}
     if rank == 0:
         frames = args.steps
         value = W * H * SPP * frames * (world if weak else 1) / elapsed / 1e6
@@ -595,6 +642,7 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
                        "width": W, "height": H, "spp": SPP, "max_ray_depth": DEPTH, "ns_area_light": NSL,
                        "spp_total": SPP * world if weak else SPP,
                        "parallelism": (f"samples{world}" if weak else f"tiles{world}") if world > 1 else "single",
+                       "frames_per_launch": 1 if weak else fpl,
                        "exchange_bytes_per_rank": (int(band[0].numel() * 4) if weak else
                                                    (int(pex.ex.packed.numel() * 4) if pex is not None else 0)),
                        # BASELINE's "wall-clock render time": ONE frame start to image,
@@ -639,6 +687,8 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
                   st_counts["culled_samples"] * (world if weak else 1))
         out["traced_samples_per_s_M"] = round((W * H * SPP * (world if weak else 1) - culled) * frames / elapsed / 1e6, 1)
         out["single_frame_Mrays"] = None if single_ms is None else round(W * H * SPP / (single_ms * 1e-3) / 1e6, 1)
+        if frame_batch is not None:
+            out["frame_batch"] = frame_batch
         # the graded kernel fraction: the isolated launch's VALU-issue fraction
         vv = out["roofline"]["views"].get("valu")
         out["roofline"]["frac_kernel"] = vv.get("frac_isolated") if vv else None
@@ -702,12 +752,13 @@ def device_fingerprint(local: int) -> str:
     return f"{socket.gethostname()}:{dev_id}"
 
 
-def single_gpu_rate(dev, tiles, w, h, spp, frame, stream, rank, backend, frames, warmup=2):
+def single_gpu_rate(dev, tiles, w, h, spp, frame, stream, rank, backend, frames, warmup=2, fpl=1):
     """Collective.  The 1-GPU point of the strong-split curve: rank 0 renders
     the WHOLE frame `frames` times alone, back to back, behind a barrier (the
     other ranks wait in it, their GPUs idle), synchronised on both sides ->
-    M samples/s, broadcast to every rank.  Also whether two ranks share a
-    device (then the N-rank value is no scaling point: efficiency null)."""
+    M samples/s, broadcast to every rank; with `fpl` frames per launch, as the
+    N-GPU line renders its shares.  Also whether two ranks share a device
+    (then the N-rank value is no scaling point: efficiency null)."""
     import torch
     import torch.distributed as dist
 
@@ -719,12 +770,20 @@ def single_gpu_rate(dev, tiles, w, h, spp, frame, stream, rank, backend, frames,
     if rank == 0:
         whole = np.asarray(tiles, dtype=np.int32).reshape(-1, 4)
         scratch = torch.empty_like(frame)
-        for _ in range(warmup):
-            dev.render_tiles_device(whole, scratch.data_ptr(), stream)
+        def render(n):
+            k = 0
+            while k < n:
+                m = min(max(1, fpl), n - k)
+                if m == 1:
+                    dev.render_tiles_device(whole, scratch.data_ptr(), stream)
+                else:
+                    dev.render_frames_device(whole, [scratch.data_ptr()] * m, [SEED] * m, stream)
+                k += m
+
+        render(warmup)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(frames):
-            dev.render_tiles_device(whole, scratch.data_ptr(), stream)
+        render(frames)
         torch.cuda.synchronize()
         rate.fill_(w * h * spp * frames / (time.perf_counter() - t0) / 1e6)
         del scratch

@@ -1136,11 +1136,17 @@ static int group_size(int64_t traced, bool env, int spp, int64_t lanes, int64_t 
   return gs;
 }
 
+static int frames_that_fit(const pt_ctx* c, const std::vector<int4>& tl, int nf);
+
 // One render: the render kernel on the slot's render stream, then the resolve
 // on the caller's stream `s`, ordered after the render (see pt_ctx: the render
 // pipeline).  (The resolve on the render stream instead measured one frame
-// +0.03 ms: profiles/r5/ab_resolve_reset_stream.txt.)
-static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStream_t s, uint32_t flags) {
+// +0.03 ms: profiles/r5/ab_resolve_reset_stream.txt.)  `nf` > 1: a frame batch
+// (pt_render_frames_device) -- nf frames of these tiles, frame f keyed by
+// seeds[f] into outs[f], in ONE render launch (the MF kernel) and nf resolves;
+// `seeds` null: the parameters' seed.
+static int launch(pt_ctx* c, const std::vector<int4>& tl, float* const* outs, int nf, const uint32_t* seeds,
+                  hipStream_t s, uint32_t flags) {
   const bool stats = (flags & (PT_FLAG_STATS | PT_FLAG_REF_COUNTS)) != 0;
   std::memset(&c->last, 0, sizeof(c->last));
   c->times_pending = false;
@@ -1215,8 +1221,10 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.max_depth = c->params.max_depth;
   P.ns_area = c->params.ns_area_light;
   P.nls_scale = (float)(1.0 / (double)P.ns_area);
-  P.seed = c->params.seed;
+  P.seed = seeds ? seeds[0] : c->params.seed;
   P.sample_base = c->params.sample_base;
+  P.n_frames = nf;
+  for (int f = 0; f < PT_MAX_FRAMES; ++f) P.seeds[f] = seeds && f < nf ? seeds[f] : P.seed;
   P.n_lights = c->n_lights;
   P.n_bsdfs = c->n_bsdfs;
   P.n_tiles = (int)tl.size();
@@ -1239,7 +1247,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.env_rtheta = c->env_rtheta.p;
   P.env_rphi = c->env_rphi.p;
   P.tiles = c->tiles[slot].p;
-  P.out = out_dev;
+  P.out = outs[0];
   P.packed = (flags & PT_FLAG_PACKED) ? 1 : 0;
   P.work_counter = c->counter[slot].p;
   P.stats = c->stats.p;
@@ -1336,7 +1344,10 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.group_spp = group_size(traced_px(c, P.W, P.H), c->env_w > 0, P.spp, (int64_t)PT_GROUP_REF_LANES, frame_blocks,
                            budget_waves);
   P.n_groups = (P.spp + P.group_spp - 1) / P.group_spp;
-  const int64_t slots = (int64_t)bl.size() * 64 * P.n_groups;
+  const int64_t frame_slots = (int64_t)bl.size() * 64 * P.n_groups;
+  const int64_t slots = frame_slots * nf;  // (a frame batch: every frame's slots, frame after frame)
+  P.frame_slots = (uint32_t)frame_slots;
+  pt_fastdiv_init((uint32_t)std::max<int64_t>(frame_slots, 1), &P.frm_m, &P.frm_sh);
   // (slot indices reach past the end by up to a static chunk plus a claimed one per wave)
   if (slots + 2 * want * PT_CHUNK_MAX >= (int64_t)INT32_MAX) return fail(PT_E_INVALID, "frame too large for one launch");
   // Small launches: at most PT_SMALL_SLOTS work slots per lane of the whole
@@ -1391,6 +1402,19 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   P.sblocks = (64 * P.n_groups) % P.chunk == 0 ? 1 : 0;  // every (aligned) chunk inside one block
   // group sums: 12 B per work slot of THIS launch (a rank's share of a split
   // frame holds only its own blocks' sums)
+  if (nf > 1) {
+    // a frame batch: every render slot's group sums sized at once for the
+    // largest batch of this tile set, and its spill area for the whole grid
+    // (growing a buffer later synchronises the device -- inside the caller's
+    // back-to-back frames)
+    const size_t cap = (size_t)std::max<int64_t>(frame_slots, 1) * 3 *
+                       (size_t)std::max(nf, frames_that_fit(c, tl, PT_MAX_FRAMES));
+    for (int k = 0; k < pt_ctx::kSlots; ++k) {
+      HIPCHK(c->partial[k].reserve(cap));
+      if (c->bvh_stack > PT_STACK)
+        HIPCHK(c->spill[k].reserve((size_t)(c->bvh_stack - PT_STACK) * std::max<int64_t>(want, c->grid_plain) * PT_BLOCK));
+    }
+  }
   HIPCHK(c->partial[slot].reserve((size_t)std::max<int64_t>(slots, 1) * 3));
   P.partial = c->partial[slot].p;
   c->last.partial_bytes = slots * PT_SUM_BYTES;
@@ -1423,7 +1447,12 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* out_dev, hipStr
   HIPCHK(ptk_launch_render(&P, grid, stats, (flags & PT_FLAG_REF_COUNTS) != 0, rs));
   HIPCHK(hipEventRecord(c->ev1, rs));
   if (rs != s) HIPCHK(hipStreamWaitEvent(s, c->ev1, 0));  // the resolve reads the finished group sums
-  HIPCHK(ptk_launch_resolve(&P, s));
+  for (int f = 0; f < nf; ++f) {  // (a frame batch: frame f's sums follow frame f - 1's)
+    KParams Pf = P;
+    Pf.partial = P.partial + 3 * (size_t)f * (size_t)frame_slots;
+    Pf.out = outs[f];
+    HIPCHK(ptk_launch_resolve(&Pf, s));
+  }
   c->counter_clean[slot] = true;  // (the resolve zeroed the slot's queue heads)
   HIPCHK(hipEventRecord(c->ev2, s));
   HIPCHK(hipEventRecord(c->ev_free[slot], s));
@@ -1527,7 +1556,8 @@ int pt_render_tiles(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, float* hdr
   if ((rc = build_tiles(c, tiles, n_tiles, tl))) return rc;
   const size_t W = (size_t)c->params.width, H = (size_t)c->params.height;
   HIPCHK(c->frame.reserve(W * H * 3));
-  if ((rc = launch(c, tl, c->frame.p, c->stream, flags))) return rc;
+  float* fr = c->frame.p;
+  if ((rc = launch(c, tl, &fr, 1, nullptr, c->stream, flags))) return rc;
   // Copy back only the tiles' pixels (the caller's buffer is theirs outside
   // them); a call whose (clipped, disjoint) tiles cover the whole frame - the
   // whole-frame batch - is one contiguous copy.
@@ -1564,7 +1594,85 @@ int pt_render_tiles_device(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, flo
     }
   }
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  if ((rc = launch(c, tl, hdr_out_dev, s, flags))) return rc;
+  if ((rc = launch(c, tl, &hdr_out_dev, 1, nullptr, s, flags))) return rc;
+  return finish_stats(c, s, flags, false);
+}
+
+// Frames of the tile set `tl` one launch of a frame batch takes.  A frame
+// with more than PT_BATCH_SLOTS work slots per lane of a whole MI355X renders
+// alone: it fills the GPU by itself, and batching measured slower there (C4
+// -4.7%; C3's 25.6 slots per lane +2%, its strong split's shares +15..+45%:
+// profiles/r6/ab_frame_batch.txt).  Otherwise as many as keep the work-slot
+// indices (with the claims' overshoot, a grid of up to 40 waves per CU) 32-bit
+// and the group sums within PT_GROUP_SUM_GIB.  The blocks are the launch's
+// own (the tiles' 8x8 blocks inside the scene's screen footprint).
+static int frames_that_fit(const pt_ctx* c, const std::vector<int4>& tl, int nf) {
+  const int W = c->params.width, H = c->params.height;
+  KParams fp;
+  std::memset(&fp, 0, sizeof(fp));
+  fp.W = W;
+  fp.H = H;
+  screen_footprint(c, fp);
+  int64_t blocks = 0;
+  for (const int4& t : tl) {
+    const int x0 = std::max(t.x, fp.cull_x0), x1 = std::min(t.x + t.z - 1, fp.cull_x1);
+    const int y0 = std::max(t.y, fp.cull_y0), y1 = std::min(t.y + t.w - 1, fp.cull_y1);
+    if (x1 >= x0 && y1 >= y0) blocks += (int64_t)((x1 - x0 + 8) / 8) * ((y1 - y0 + 8) / 8);
+  }
+  const int64_t frame_blocks = (int64_t)((W + 7) / 8) * ((H + 7) / 8);
+  const int64_t waves = std::max<int64_t>({(int64_t)c->grid_plain, (int64_t)c->grid_stats, (int64_t)40 * c->n_cu});
+  const int gs = group_size(traced_px(c, W, H), c->env_w > 0, c->params.spp, (int64_t)PT_GROUP_REF_LANES,
+                            frame_blocks, waves);
+  const int64_t per = blocks * 64 * ((c->params.spp + gs - 1) / gs);
+  if (per > (int64_t)PT_BATCH_SLOTS * PT_GROUP_REF_LANES) return 1;
+  while (nf > 1 && (per * nf + 2 * waves * PT_CHUNK_BIG >= (int64_t)INT32_MAX ||
+                    per * nf * PT_SUM_BYTES > ((int64_t)PT_GROUP_SUM_GIB << 30)))
+    --nf;
+  return nf;
+}
+
+int pt_render_frames_device(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, int32_t n_frames, const uint32_t* seeds,
+                            float* const* hdr_outs_dev, void* stream, uint32_t flags) {
+  int rc = check_ready(c);
+  if (rc) return rc;
+  if ((rc = tile_launch(c))) return rc;
+  if (n_frames < 1 || n_frames > PT_MAX_FRAMES || !seeds || !hdr_outs_dev || n_tiles < 0 || (n_tiles > 0 && !tiles))
+    return fail(PT_E_INVALID, "pt_render_frames_device: bad args (1 <= n_frames <= PT_MAX_FRAMES, seeds and outputs)");
+  for (int32_t f = 0; f < n_frames; ++f)
+    if (n_tiles > 0 && !hdr_outs_dev[f]) return fail(PT_E_INVALID, "pt_render_frames_device: NULL output");
+  if (flags & (PT_FLAG_STATS | PT_FLAG_REF_COUNTS))
+    return fail(PT_E_INVALID, "pt_render_frames_device: counters are per frame (pt_render_tiles_device)");
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<int4> tl;
+  if ((rc = build_tiles(c, tiles, n_tiles, tl))) return rc;
+  if (flags & PT_FLAG_PACKED) {
+    const int W = c->params.width, H = c->params.height;
+    for (int32_t i = 0; i < n_tiles; ++i) {
+      const pt_tile& t = tiles[i];
+      if (t.w < 1 || t.h < 1 || t.w > 32 || t.h > 32 || t.x < 0 || t.y < 0 || t.x + t.w > W || t.y + t.h > H)
+        return fail(PT_E_INVALID, "pt_render_frames_device: PT_FLAG_PACKED needs tiles of 1..32 x 1..32 inside the frame");
+    }
+  }
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  // One launch for the batch in the plain common build; the environment-light
+  // and global-table builds, diagnostics and PT_FRAME_BATCH=0 render the
+  // frames one launch each (the same images)
+  static const bool batch_on = !std::getenv("PT_FRAME_BATCH") || std::atoi(std::getenv("PT_FRAME_BATCH")) != 0;
+  const bool gtab = c->n_bsdfs > PT_LDS_BSDFS || c->n_lights > PT_LDS_LIGHTS || std::getenv("PT_FORCE_GLOBAL_TABLES");
+  const bool one = !batch_on || n_frames == 1 || c->env_w > 0 || gtab || std::getenv("PT_CENSUS") ||
+                   std::getenv("PT_DEBUG_PIXEL");
+  if (one) {
+    for (int32_t f = 0; f < n_frames; ++f)
+      if ((rc = launch(c, tl, &hdr_outs_dev[f], 1, &seeds[f], s, flags))) return rc;
+  } else {
+    // (frames beyond what one launch's slot indices and group sums hold go
+    // into further batches)
+    for (int32_t f = 0; f < n_frames;) {
+      const int nf = frames_that_fit(c, tl, n_frames - f);
+      if ((rc = launch(c, tl, hdr_outs_dev + f, nf, seeds + f, s, flags))) return rc;
+      f += nf;
+    }
+  }
   return finish_stats(c, s, flags, false);
 }
 
@@ -1709,7 +1817,8 @@ static int tile_launch_impl(pt_ctx* c) {
     give_back();
     return fail(PT_E_HIP, std::string("pt_tile_submit: ") + hipGetErrorString(e));
   }
-  if (int rc = launch(c, tl, c->frame.p, c->stream, 0)) {
+  float* fr = c->frame.p;
+  if (int rc = launch(c, tl, &fr, 1, nullptr, c->stream, 0)) {
     give_back();
     return rc;
   }

@@ -19,6 +19,13 @@
 #ifndef PT_BANDS_TREE_MIB
 #define PT_BANDS_TREE_MIB 8  // queue bands for large frames over render trees above this size (pt_api.cpp launch)
 #endif
+// Frames per launch of pt_render_frames_device (KParams.seeds; include/ptgpu.h)
+#ifndef PT_MAX_FRAMES
+#define PT_MAX_FRAMES 8
+#endif
+#ifndef PT_BATCH_SLOTS
+#define PT_BATCH_SLOTS 32  // a frame with more work slots per lane (of a whole MI355X) renders alone (pt_api.cpp)
+#endif
 #ifndef PT_SMALL_SLOTS
 #define PT_SMALL_SLOTS 16  // launches with at most this many work slots per resident lane are small (pt_api.cpp launch)
 #endif
@@ -286,6 +293,14 @@ struct KParams {
   int census;                 // plain build: record each wave's start / end / CU / drain in the trace area (PT_CENSUS)
   float root_lo[3], root_hi[3];  // scene bounds (root box, rounded outward)
   int cull_x0, cull_y0, cull_x1, cull_y1;  // pixels outside [x0,x1]x[y0,y1] see no geometry
+  // Frame batch (pt_render_frames_device, the MF kernel): n_frames frames of
+  // the same tiles in one launch.  Work slot g is slot g - f * frame_slots of
+  // frame f = g / frame_slots; frame f keys its samples with seeds[f] and its
+  // group sums follow frame f - 1's (partial + 3 * g).  One frame: unused.
+  int n_frames;
+  uint32_t frame_slots;
+  uint32_t frm_m, frm_sh;  // fastdiv by frame_slots
+  uint32_t seeds[PT_MAX_FRAMES];
 };
 
 // q = u / d for u < 2^31 and a runtime divisor d >= 1, without a division:

@@ -710,7 +710,10 @@ enum : int { S_HIT = 0, S_NEE = 1, S_BSDF = 2, S_FETCH = 3, S_CAMERA = 4, S_TRAV
 // memory; the common build reads them from LDS through address-space-typed
 // pointers, never through FLAT accesses).
 // TRI: every primitive is a triangle (branch-free leaf steps, no sphere test).
-template <bool STATS, bool DBG, bool BIN, bool ENV, bool GTAB, bool TRI = false>
+// MF: a frame batch (KParams.n_frames frames of one tile set in one launch,
+// plain common build only): the queue runs over every frame's work slots, so
+// a small frame's drain is filled by the next frame's slots.
+template <bool STATS, bool DBG, bool BIN, bool ENV, bool GTAB, bool TRI = false, bool MF = false>
 __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel(KParams P) {
   // the wave's PT_STACK x 64 LDS stack (lane-contiguous rows)
   __shared__ int s_stack[PT_STACK * PT_BLOCK];
@@ -874,7 +877,7 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // the pixel index from the packed coordinates: one multiply-add, no
   // division per camera ray
   auto pix_index = [&](int p) -> int { return (p & 0xffff) + (int)((uint32_t)p >> 16) * P.W; };
-  const uint32_t total_slots = (uint32_t)P.n_blocks * 64u * (uint32_t)P.n_groups;
+  const uint32_t total_slots = (uint32_t)P.n_blocks * 64u * (uint32_t)P.n_groups * (MF ? (uint32_t)P.n_frames : 1u);
   const int batch = P.shade_batch;
   // Camera::generate_ray (camera.cpp:113-129) for the lane's pixel and
   // current sample, at the jittered position of raytrace_pixel
@@ -883,7 +886,14 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
   // nothing but the environment: pathtracer.cpp:421-426).
   auto camera_ray = [&](Trav& t, float3& d) -> bool {
     const int px = pix & 0xffff, py = (int)((uint32_t)pix >> 16);
-    rbase = ptrng::stream_base(P.seed, (uint32_t)(px + py * P.W), (uint32_t)sample + P.sample_base);
+    uint32_t seed = P.seed;
+    if constexpr (MF) {  // the lane's frame of the batch keys its samples
+      const uint32_t f = pt_fastdiv(myslot, P.frm_m, P.frm_sh);
+      seed = P.seeds[0];
+#pragma unroll
+      for (int i = 1; i < PT_MAX_FRAMES; ++i) seed = f == (uint32_t)i ? P.seeds[i] : seed;
+    }
+    rbase = ptrng::stream_base(seed, (uint32_t)(px + py * P.W), (uint32_t)sample + P.sample_base);
     rdim = ptrng::kDrawInit;
     float ry = PT_DRAW();  // UniformGridSampler2D draws y first
     float rx = PT_DRAW();
@@ -1300,13 +1310,20 @@ __global__ __launch_bounds__(PT_BLOCK, PT_MIN_WAVES_PER_SIMD) void render_kernel
           }
         }
         // Work slots -> (block k, pixel q, group j): see KParams (a fastdiv)
+        // (MF: the slot within its frame; a frame's slots are a multiple of
+        // 64 * n_groups, so no chunk of a block-aligned claim straddles two)
+        auto local_slot = [&](uint32_t slot) -> uint32_t {
+          if constexpr (MF) return slot - pt_fastdiv(slot, P.frm_m, P.frm_sh) * P.frame_slots;
+          else return slot;
+        };
         auto decode = [&](uint32_t slot, uint32_t& k, uint32_t& j, uint32_t& q) {
+          slot = local_slot(slot);
           const uint32_t px = pt_fastdiv(slot, P.grp_m, P.grp_sh);
           j = slot - px * (uint32_t)P.n_groups;
           k = px >> 6;
           q = px & 63u;
         };
-        auto block_of = [&](uint32_t slot) -> uint32_t { return pt_fastdiv(slot, P.grp_m, P.grp_sh) >> 6; };
+        auto block_of = [&](uint32_t slot) -> uint32_t { return pt_fastdiv(local_slot(slot), P.grp_m, P.grp_sh) >> 6; };
         // A chunk of 128 slots (128-aligned) lies inside one block when a
         // pixel has an even number of groups, and the lanes are
         // served from at most two chunks -- the rest of the old one and the
@@ -1791,7 +1808,14 @@ static void launch_render(const KParams* P, int waves, bool stats, bool ref_coun
     hipLaunchKernelGGL((ptk::render_kernel<true, false, false, ENV, GTAB, true>), dim3(grid), blk, 0, s, *P);
   else if (stats)
     hipLaunchKernelGGL((ptk::render_kernel<true, false, false, ENV, GTAB>), dim3(grid), blk, 0, s, *P);
-  else if (P->tri_only && !GTAB)
+  else if (P->n_frames > 1) {  // a frame batch (host: the plain common build only)
+    if constexpr (!ENV && !GTAB) {
+      if (P->tri_only)
+        hipLaunchKernelGGL((ptk::render_kernel<false, false, false, false, false, true, true>), dim3(grid), blk, 0, s, *P);
+      else
+        hipLaunchKernelGGL((ptk::render_kernel<false, false, false, false, false, false, true>), dim3(grid), blk, 0, s, *P);
+    }
+  } else if (P->tri_only && !GTAB)
     hipLaunchKernelGGL((ptk::render_kernel<false, false, false, ENV, GTAB, true>), dim3(grid), blk, 0, s, *P);
   else
     hipLaunchKernelGGL((ptk::render_kernel<false, false, false, ENV, GTAB>), dim3(grid), blk, 0, s, *P);

@@ -162,7 +162,7 @@ class TileExchange:
 class PipelinedExchange:
     """Back-to-back sharded frames with the exchange off the render's path.
 
-    Frame k renders into packed buffer k % 2 (`packed_for(k)`, called BEFORE
+    Frame k renders into packed buffer k % buffers (`packed_for(k)`, called BEFORE
     the render is queued); `exchange(k, frame)` gathers frame k's buffer onto
     `dst` and scatters it into `frame`.  The renders themselves run on the
     library's render-slot streams (pt_api.cpp), so frame k+1's render overlaps
@@ -177,10 +177,14 @@ class PipelinedExchange:
     those of TileExchange, bit for bit."""
 
     def __init__(self, tiles: Sequence[Tile], width: int, height: int, rank: int, world: int, device,
-                 dst: int = 0, group=None, deal: str = "diag", side: bool = False):
+                 dst: int = 0, group=None, deal: str = "diag", side: bool = False, buffers: int = 2):
         import torch
 
-        self.ex = TileExchange(tiles, width, height, rank, world, device, dst=dst, group=group, deal=deal, buffers=2)
+        # `buffers` packed buffers, frame k in buffer k % buffers: at least the
+        # frames of one frame batch (bench.py --frames-per-launch), whose
+        # resolves all run before the batch's exchanges
+        self.ex = TileExchange(tiles, width, height, rank, world, device, dst=dst, group=group, deal=deal,
+                               buffers=max(2, buffers))
         self.mine = self.ex.mine
         self.cuda = self.ex.bufs[0].is_cuda
         # side=False (default): the exchange is queued on the current stream
@@ -189,13 +193,13 @@ class PipelinedExchange:
         # even (profiles/r6/ab_stream_queues.txt, sessions v and w)
         self.side = torch.cuda.Stream(device=self.ex.bufs[0].device) if self.cuda and side else None
         self.on_current = self.cuda and not side
-        self.free = [None, None]  # per buffer: event after the gather that last read it
+        self.free = [None] * len(self.ex.bufs)  # per buffer: event after the gather that last read it
         self.xev = []
 
     def packed_for(self, k: int):
         import torch
 
-        b = k % 2
+        b = k % len(self.ex.bufs)
         if self.cuda and self.free[b] is not None:
             torch.cuda.current_stream().wait_event(self.free[b])
         self.ex.packed = self.ex.bufs[b]
@@ -204,7 +208,7 @@ class PipelinedExchange:
     def exchange(self, k: int, frame, timed: bool = False):
         import torch
 
-        buf = self.ex.bufs[k % 2]
+        buf = self.ex.bufs[k % len(self.ex.bufs)]
         if not self.cuda:
             self.ex.gather(buf)
             return self.ex.scatter(frame)
@@ -230,7 +234,7 @@ class PipelinedExchange:
             e1.record()
             free = torch.cuda.Event()
             free.record()
-        self.free[k % 2] = free
+        self.free[k % len(self.ex.bufs)] = free
         if timed:
             self.xev.append((e0, e1))
         return frame

@@ -25,6 +25,7 @@ PT_LIGHT_ENVIRONMENT = 4
 PT_FLAG_STATS = 1
 PT_FLAG_REF_COUNTS = 2
 PT_FLAG_PACKED = 4
+PT_MAX_FRAMES = 8  # frames per pt_render_frames_device launch (include/ptgpu.h)
 
 PRIM_SPHERE, PRIM_TRIANGLE = 0, 1
 BSDF_DIFFUSE, BSDF_MIRROR, BSDF_REFRACTION, BSDF_GLASS, BSDF_EMISSION = range(5)
@@ -106,6 +107,8 @@ _SIGS = {
     "pt_set_params": (c_int32, [c_void_p, POINTER(pt_params)]),
     "pt_render_tiles": (c_int32, [c_void_p, POINTER(pt_tile), c_int32, c_void_p, c_uint32]),
     "pt_render_tiles_device": (c_int32, [c_void_p, POINTER(pt_tile), c_int32, c_void_p, c_void_p, c_uint32]),
+    "pt_render_frames_device": (c_int32, [c_void_p, POINTER(pt_tile), c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                          c_uint32]),
     "pt_tile_submit": (c_int32, [c_void_p, POINTER(pt_tile), c_void_p, c_void_p]),
     "pt_tile_finish": (c_int32, [c_void_p]),
     "pt_intersect": (c_int32, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -124,6 +124,29 @@ class Device:
         check(self._lib.pt_render_tiles_device(self.handle, arr, len(keep), ctypes.c_void_p(out_ptr),
                                                ctypes.c_void_p(stream or None), flags))
 
+    def render_frames_device(self, tiles, out_ptrs, seeds, stream: int = 0, packed: bool = False,
+                             out_floats: Optional[int] = None):
+        """pt_render_frames_device: len(seeds) (1..4) frames of the same tiles in
+        one launch, frame f keyed by seeds[f] into out_ptrs[f] (each laid out as
+        render_tiles_device's out_ptr); every image equals its own
+        render_tiles_device call with that seed."""
+        n = len(seeds)
+        if n != len(out_ptrs) or not 1 <= n <= native.PT_MAX_FRAMES:
+            raise ValueError(f"render_frames_device: 1..{native.PT_MAX_FRAMES} frames, one output each")
+        keep, arr = self._tiles(tiles)
+        if out_floats is not None:
+            if getattr(self, "_frame", None) is None:
+                raise ValueError("render_frames_device: set_params first")
+            need = len(keep) * 1024 * 3 if packed else self._frame[0] * self._frame[1] * 3
+            if out_floats < need:
+                raise ValueError(f"render_frames_device: outputs hold {out_floats} floats, the "
+                                 f"{'packed' if packed else 'frame'} layout writes {need}")
+        sd = (ctypes.c_uint32 * n)(*[int(v) & 0xFFFFFFFF for v in seeds])
+        op = (ctypes.c_void_p * n)(*[int(v) for v in out_ptrs])
+        flags = native.PT_FLAG_PACKED if packed else 0
+        check(self._lib.pt_render_frames_device(self.handle, arr, len(keep), n, sd, op,
+                                                ctypes.c_void_p(stream or None), flags))
+
     def submit_tile(self, tile, hdr: np.ndarray, rgba: Optional[np.ndarray] = None):
         """pt_tile_submit: queue one tile; its pixels land in `hdr` ((H, W, 3)
         float32) and, toColor'd, in `rgba` ((H, W, 4) uint8) when its batch

@@ -34,6 +34,9 @@
  *                               (sampleBuffer + toColor) by a completion thread
  *   pt_render_tiles_device      same, output left in device memory on a caller stream
  *                               (used for the multi-GPU framebuffer reduction)
+ *   pt_render_frames_device     several frames of one tile set (one seed each) in one
+ *                               launch: CUDAPathTracer::startRayTracingPT called back to
+ *                               back (setup.cu:147-179), without a drain between frames
  *   pt_intersect                BVHAccel::intersect(ray, isect) and BVHAccel::intersect(ray)
  *                               (src/bvh.cpp:331-362) as a batched query
  *   pt_get_stats                timers/counters (pathtracer.cpp:615-632, setup.cu:546-685)
@@ -264,6 +267,17 @@ int pt_render_tiles(pt_ctx* ctx, const pt_tile* tiles, int32_t n_tiles, float* h
  * minus its host copy-back. */
 int pt_render_tiles_device(pt_ctx* ctx, const pt_tile* tiles, int32_t n_tiles, float* hdr_out_dev,
                            void* stream, uint32_t flags);
+/* A frame batch: n_frames (1..PT_MAX_FRAMES = 8) renders of the same tiles, frame
+ * f with pt_params.seed replaced by seeds[f], into hdr_outs_dev[f] (each as
+ * pt_render_tiles_device's hdr_out_dev, PT_FLAG_PACKED allowed; counters are
+ * not: PT_FLAG_STATS / PT_FLAG_REF_COUNTS return PT_E_INVALID).  Every image
+ * is bit-identical to its own pt_render_tiles_device call with that seed;
+ * the frames share ONE persistent launch, so a small frame's drain (a rank's
+ * share of a split frame) is filled with the next frame's work.  Stream
+ * semantics as pt_render_tiles_device. */
+#define PT_MAX_FRAMES 8
+int pt_render_frames_device(pt_ctx* ctx, const pt_tile* tiles, int32_t n_tiles, int32_t n_frames,
+                            const uint32_t* seeds, float* const* hdr_outs_dev, void* stream, uint32_t flags);
 /* Asynchronous one-tile seam: PathTracer::raytrace_tile(tile_x, tile_y, tile_w, tile_h)
  * (src/pathtracer.cpp:585-611) as the reference's worker threads call it
  * (worker_thread, pathtracer.cpp:613-621), without one launch and one host

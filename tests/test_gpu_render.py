@@ -1014,3 +1014,55 @@ def test_gpu_tree_build_is_deterministic(monkeypatch):
     assert out[0][0].mean() > 0
     for img, nv, nn in out[1:]:
         assert np.array_equal(img, out[0][0]) and nv == out[0][1] and nn == out[0][2]
+
+
+@pytest.mark.parametrize("name,w,h,packed", [("c1_default_128x128", 128, 128, False), ("c3proxy", 128, 128, False),
+                                             ("c3proxy", 128, 128, True), ("c1env_64x64", 64, 64, False)])
+def test_frame_batch_is_bit_identical_to_single_frames(name, w, h, packed):
+    """pt_render_frames_device: n frames of one tile set in ONE launch (the MF
+    kernel: the queue runs over every frame's work slots; environment-light
+    scenes take one launch per frame), frame f keyed by seeds[f].  Every image
+    equals its own pt_render_tiles_device call with that seed -- 8, 3 and 1
+    frames, whole frames, and (packed) a rank's share of a 4-way strong split,
+    with spheres (the mixed kernel) and triangle-only scenes (TRI)."""
+    import torch
+
+    from dsgpuraytracing_amd import scenes
+    from dsgpuraytracing_amd.dist import shard_tiles
+    from dsgpuraytracing_amd.pathtracer import Device
+
+    if name == "c3proxy":
+        sc = Scene.from_dae(scenes.proxy_path(1), w, h)
+    else:
+        sc = Scene.from_dump(golden(f"{name}.scene.ptd"))
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream(device=0)
+    dev = Device(0)
+    try:
+        dev.upload_scene(sc)
+        dev.set_camera(sc.camera)
+        spp = 8
+        dev.set_params(w, h, spp, 4, 1, 1)
+        tiles = [(x, y, min(tw, w - x), min(th, h - y)) for (x, y, tw, th) in tile_fifo(w, h)]
+        mine = shard_tiles(tiles, 1, 4, "diag") if packed else tiles
+        arr = np.asarray(mine, np.int32).reshape(-1, 4)
+        size = len(mine) * 1024 * 3 if packed else w * h * 3
+        for seeds in ([5, 6, 7, 8, 9, 10, 11, 12], [21, 22, 23], [9]):
+            outs = [torch.full((size,), -1.0, dtype=torch.float32, device="cuda:0") for _ in seeds]
+            dev.render_frames_device(arr, [o.data_ptr() for o in outs], seeds, stream.cuda_stream, packed=packed,
+                                     out_floats=size)
+            torch.cuda.synchronize()
+            for s, o in zip(seeds, outs):
+                ref = torch.full((size,), -1.0, dtype=torch.float32, device="cuda:0")
+                dev.set_params(w, h, spp, 4, 1, s)
+                dev.render_tiles_device(arr, ref.data_ptr(), stream.cuda_stream, packed=packed, out_floats=size)
+                torch.cuda.synchronize()
+                assert torch.equal(o, ref), (name, seeds, s)
+                assert float(o.abs().sum()) > 0
+            dev.set_params(w, h, spp, 4, 1, 1)
+            if len(seeds) > 1:
+                assert not torch.equal(outs[0], outs[1])
+        with pytest.raises(ValueError):
+            dev.render_frames_device(arr, [0] * 9, list(range(9)), stream.cuda_stream)
+    finally:
+        dev.close()

@@ -8,7 +8,7 @@ import collections
 import re
 import sys
 
-DEFAULT = "_ZN3ptk13render_kernelILb0ELb0ELb0ELb0ELb0ELb0EEEv7KParams"
+DEFAULT = "_ZN3ptk13render_kernelILb0ELb0ELb0ELb0ELb0ELb0ELb0EEEv7KParams"
 
 
 def census(path, name=DEFAULT):

@@ -7,7 +7,7 @@ import re
 import sys
 
 path = sys.argv[1]
-name = sys.argv[2] if len(sys.argv) > 2 else "_ZN3ptk13render_kernelILb0ELb0ELb0ELb0ELb0ELb1EEEv7KParams"
+name = sys.argv[2] if len(sys.argv) > 2 else "_ZN3ptk13render_kernelILb0ELb0ELb0ELb0ELb0ELb1ELb0EEEv7KParams"
 s = open(path).read()
 a = s.index(name + ":")
 b = s.index(".Lfunc_end", a)
