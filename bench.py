@@ -598,7 +598,7 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
         # the same frame in batches of 8 per launch (pt_render_frames_device),
         # as the N > 1 line renders its shares: the like-for-like 1-GPU point
         # of that curve (its own single_gpu_value measures the same)
-        if args.emulate_shard <= 1:
+        if args.emulate_shard <= 1 and workload == "c3":  # (larger frames render one per launch anyway)
             nb = 64
             dev.render_frames_device(mine_arr, [frame.data_ptr()] * 8, [SEED] * 8, stream)  # (warm-up)
             torch.cuda.synchronize()

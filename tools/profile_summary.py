@@ -32,12 +32,19 @@ KERNELS = {"c5": "render_kernel<false, false, false, true, false", "c5big": "ren
 KERNEL = "render_kernel<false, false, false, false, false"
 
 
+def timed(name):
+    """The workload's timed render launch: the kernel prefix, and not the
+    frame-batch instantiation (last template argument MF = true), which the
+    N = 1 line's frame_batch field also launches in the profiled process."""
+    return KERNEL in name and ", true>(" not in name
+
+
 def _pmc(path):
     agg = collections.defaultdict(list)
     if not os.path.exists(path):
         return {}
     for r in csv.DictReader(open(path)):
-        if KERNEL in r["Kernel_Name"]:
+        if timed(r["Kernel_Name"]):
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
@@ -53,13 +60,13 @@ def main():
     ks = os.path.join(prof, "kt", "kt_kernel_stats.csv")
     shutil.copy(ks, os.path.join(out, f"{workload}_kernel_stats.csv"))
     stats = {r["Name"]: r for r in csv.DictReader(open(ks))}
-    render = next(v for k, v in stats.items() if KERNEL in k)
+    render = next(v for k, v in stats.items() if timed(k))
     resolve = next((v for k, v in stats.items() if "resolve_kernel" in k), None)
     iso = None
     ksi = os.path.join(prof, "kt_iso", "kt_iso_kernel_stats.csv")
     if os.path.exists(ksi):
         shutil.copy(ksi, os.path.join(out, f"{workload}_kernel_stats_isolated.csv"))
-        iso = next(v for k, v in {r["Name"]: r for r in csv.DictReader(open(ksi))}.items() if KERNEL in k)
+        iso = next(v for k, v in {r["Name"]: r for r in csv.DictReader(open(ksi))}.items() if timed(k))
     fetch = _pmc(os.path.join(prof, "fetch", "fetch_counter_collection.csv"))
     write = _pmc(os.path.join(prof, "write", "write_counter_collection.csv"))
     sq = _pmc(os.path.join(prof, "sq", "sq_counter_collection.csv"))
@@ -67,7 +74,7 @@ def main():
     for name, d in (("fetch", fetch), ("write", write), ("sq", sq), ("tcc", tcc)):
         src = os.path.join(prof, name, f"{name}_counter_collection.csv")
         if os.path.exists(src):
-            rows = [r for r in csv.DictReader(open(src)) if KERNEL in r["Kernel_Name"]]
+            rows = [r for r in csv.DictReader(open(src)) if timed(r["Kernel_Name"])]
             with open(os.path.join(out, f"{workload}_pmc_{name}.csv"), "w", newline="") as f:
                 w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
                 w.writeheader()
