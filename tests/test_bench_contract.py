@@ -63,8 +63,11 @@ def test_pmc_summary_agrees_with_committed_kernel_trace():
     with open(stats) as f:
         rows = {r["Name"]: r for r in csv.DictReader(f)}
     # the plain render kernel of the summary's round (rounds 1-4: five template
-    # arguments; round 5 adds the triangle-only flag)
-    names = [n for n in rows if pm.get("kernel", "render_kernel<false, false, false, false, false") in n]
+    # arguments; round 5 adds the triangle-only flag; round 6 the frame-batch
+    # flag, whose instantiation -- the N = 1 line's frame_batch field -- is not
+    # the timed kernel: tools/profile_summary.py timed())
+    names = [n for n in rows if pm.get("kernel", "render_kernel<false, false, false, false, false") in n
+             and ", true>(" not in n]
     assert len(names) == 1, names
     avg_ms = float(rows[names[0]]["AverageNs"]) * 1e-6
     assert avg_ms == pytest.approx(pm["avg_ms"], rel=0.02)
@@ -141,3 +144,18 @@ def test_round6_line_reports_the_honest_rates():
     # the node-step census of the STATS launch is on the line
     n = d["launch_counters"]["node_census"]
     assert len(n) == 8 and n[0] > 0 and 0 <= n[1] <= n[0] and n[2] <= n[3]
+
+
+def test_round6_line_reports_its_frames_per_launch():
+    """The N = 1 headline renders one frame per launch and says so; beside it
+    the same frame in batches of eight (pt_render_frames_device), the
+    like-for-like 1-GPU point of the N > 1 strong split, whose shares render
+    eight frames per launch (bench.py --frames-per-launch)."""
+    path = os.path.join(ROOT, "profiles", "r6", "bench_c3_default.jsonl")
+    with open(path) as f:
+        d = json.loads(f.read().strip().splitlines()[-1])
+    assert d["config"]["frames_per_launch"] == 1
+    fb = d["frame_batch"]
+    assert fb["frames_per_launch"] == 8 and fb["frames"] % 8 == 0
+    whs = d["config"]["width"] * d["config"]["height"] * d["config"]["spp"]
+    assert fb["value"] == pytest.approx(whs / (fb["ms_per_step"] * 1e3), rel=0.01)
