@@ -331,7 +331,7 @@ def main():
                     help="frames rendered per launch (pt_render_frames_device, 1..8; the library renders frames "
                          "of more than 32 work slots per lane one per launch): a frame batch shares one "
                          "persistent launch, so a small frame's drain is filled with the next frame's work. "
-                         "Default: 8 for the strong split's shares (N > 1, --emulate-shard), 1 for N = 1")
+                         "Default 8 (the weak pass: 1)")
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
                     help="N > 1: strong = one frame's tiles split across the GPUs + one pipelined RCCL gather "
                          "(default; BASELINE C4: --workload c4); weak = one pass of the whole frame per GPU over "
@@ -419,8 +419,7 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
         mine_arr = np.asarray(shard_tiles(tiles, args.emulate_rank, args.emulate_shard, "diag"),
                               dtype=np.int32).reshape(-1, 4)
     # strong: packed tiles, the gather queued behind each frame's resolve
-    fpl = args.frames_per_launch or (8 if (world > 1 and not weak) or args.emulate_shard > 1 else 1)
-    fpl = max(1, min(8, fpl))
+    fpl = 1 if weak else max(1, min(8, args.frames_per_launch or 8))
     pex = (PipelinedExchange(tiles, W, H, rank, world, frame.device, buffers=max(2, fpl), **xchg_opts())
            if world > 1 and not weak else None)
     if args.emulate_shard > 1:
@@ -595,19 +594,19 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
         for _ in range(2):
             dev.render_tiles(mine_arr, host)
         host_ms = (time.perf_counter() - t0h) / 2 * 1e3
-        # the same frame in batches of 8 per launch (pt_render_frames_device),
-        # as the N > 1 line renders its shares: the like-for-like 1-GPU point
-        # of that curve (its own single_gpu_value measures the same)
-        if args.emulate_shard <= 1 and workload == "c3":  # (larger frames render one per launch anyway)
-            nb = 64
-            dev.render_frames_device(mine_arr, [frame.data_ptr()] * 8, [SEED] * 8, stream)  # (warm-up)
+        # beside a batched line: the same frames one per launch
+        # (pt_render_tiles_device per frame, the reference's one-frame call)
+        if args.emulate_shard <= 1 and fpl > 1 and workload == "c3":  # (larger frames render one per launch anyway)
+            nb = 32
+            for _ in range(2):
+                dev.render_tiles_device(mine_arr, frame.data_ptr(), stream)
             torch.cuda.synchronize()
             t0b = time.perf_counter()
-            for _ in range(nb // 8):
-                dev.render_frames_device(mine_arr, [frame.data_ptr()] * 8, [SEED] * 8, stream)
+            for _ in range(nb):
+                dev.render_tiles_device(mine_arr, frame.data_ptr(), stream)
             torch.cuda.synchronize()
             elb = time.perf_counter() - t0b
-            frame_batch = {"frames_per_launch": 8, "frames": nb, "ms_per_step": round(elb / nb * 1e3, 4),
+            frame_batch = {"frames_per_launch": 1, "frames": nb, "ms_per_step": round(elb / nb * 1e3, 4),
                            "value": round(W * H * SPP * nb / elb / 1e6, 1)}
     if rank == 0:
         frames = args.steps
@@ -671,7 +670,11 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
                                                         "wave_wall_sum", "wave_wall_max", "section_clocks", "wave_span",
                                                         "lane_iters", "partial_bytes", "deep_stack_steps",
                                                         "node_census")},
-            "launch": {"grid_blocks": s_get(dev, "grid_blocks"), "block": 64,
+            # frames per timed launch: the roofline's counts and durations are per
+            # frame; one launch of the kernel trace = launch_ms, frames_per_launch frames
+            "launch": {"frames_per_launch": fpl, "launch_ms": round(avg_ms * (args.steps / n_launch), 4),
+                       "timed_launches": n_launch,
+                       "grid_blocks": s_get(dev, "grid_blocks"), "block": 64,
                        "blocks_per_cu_query": s_get(dev, "blocks_per_cu"),
                        "bvh_nodes": s_get(dev, "bvh_nodes"), "bvh_stack": s_get(dev, "bvh_stack"),
                        "group_spp": s_get(dev, "group_spp")},
@@ -688,7 +691,7 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
         out["traced_samples_per_s_M"] = round((W * H * SPP * (world if weak else 1) - culled) * frames / elapsed / 1e6, 1)
         out["single_frame_Mrays"] = None if single_ms is None else round(W * H * SPP / (single_ms * 1e-3) / 1e6, 1)
         if frame_batch is not None:
-            out["frame_batch"] = frame_batch
+            out["one_frame_per_launch"] = frame_batch
         # the graded kernel fraction: the isolated launch's VALU-issue fraction
         vv = out["roofline"]["views"].get("valu")
         out["roofline"]["frac_kernel"] = vv.get("frac_isolated") if vv else None

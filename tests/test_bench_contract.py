@@ -66,8 +66,10 @@ def test_pmc_summary_agrees_with_committed_kernel_trace():
     # arguments; round 5 adds the triangle-only flag; round 6 the frame-batch
     # flag, whose instantiation -- the N = 1 line's frame_batch field -- is not
     # the timed kernel: tools/profile_summary.py timed())
-    names = [n for n in rows if pm.get("kernel", "render_kernel<false, false, false, false, false") in n
-             and ", true>(" not in n]
+    if pm.get("kernel_name"):  # round 6: the exact timed instantiation (frame batches: the MF one)
+        names = [n for n in rows if n == pm["kernel_name"]]
+    else:
+        names = [n for n in rows if pm.get("kernel", "render_kernel<false, false, false, false, false") in n]
     assert len(names) == 1, names
     avg_ms = float(rows[names[0]]["AverageNs"]) * 1e-6
     assert avg_ms == pytest.approx(pm["avg_ms"], rel=0.02)
@@ -147,15 +149,19 @@ def test_round6_line_reports_the_honest_rates():
 
 
 def test_round6_line_reports_its_frames_per_launch():
-    """The N = 1 headline renders one frame per launch and says so; beside it
-    the same frame in batches of eight (pt_render_frames_device), the
-    like-for-like 1-GPU point of the N > 1 strong split, whose shares render
-    eight frames per launch (bench.py --frames-per-launch)."""
+    """The C3 line renders its frames eight per launch (frame batches,
+    pt_render_frames_device; bit-identical images) and says so -- config and
+    launch -- with the launch duration beside the per-frame one; beside it the
+    same frames one per launch (the reference's one-frame call)."""
     path = os.path.join(ROOT, "profiles", "r6", "bench_c3_default.jsonl")
     with open(path) as f:
         d = json.loads(f.read().strip().splitlines()[-1])
-    assert d["config"]["frames_per_launch"] == 1
-    fb = d["frame_batch"]
-    assert fb["frames_per_launch"] == 8 and fb["frames"] % 8 == 0
+    assert d["config"]["frames_per_launch"] == 8 == d["launch"]["frames_per_launch"]
+    assert d["launch"]["timed_launches"] == -(-d["steps"] // 8)
+    one = d["one_frame_per_launch"]
+    assert one["frames_per_launch"] == 1 and one["frames"] > 0
     whs = d["config"]["width"] * d["config"]["height"] * d["config"]["spp"]
-    assert fb["value"] == pytest.approx(whs / (fb["ms_per_step"] * 1e3), rel=0.01)
+    assert one["value"] == pytest.approx(whs / (one["ms_per_step"] * 1e3), rel=0.01)
+    # the PMC summary counts per frame of the 8-frame launches
+    pm = bench.profile_summary("c3")
+    assert pm["frames_per_launch"] == 8 and pm["counts_per"] == "frame"

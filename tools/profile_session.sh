@@ -10,7 +10,10 @@ export TMPDIR=/tmp
 WL=${1:-c3}
 STEPS=${2:-5}
 OUT=${3:-gpurun_out/prof}
-B="python3 bench.py --workload $WL --steps $STEPS --warmup 2 --no-cpu-baseline --no-extras"
+# (C3 renders 8 frames per launch: whole batches only, so every timed launch
+# the passes count is an 8-frame one -- tools/profile_summary.py <wl> <out> <prof> "" 8)
+WARM=2; [ "$WL" = c3 ] && WARM=8
+B="python3 bench.py --workload $WL --steps $STEPS --warmup $WARM --no-cpu-baseline --no-extras"
 P="rocprofv3 --output-format csv"
 I="PT_PIPELINE=0"
 rm -rf "$OUT"

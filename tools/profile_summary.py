@@ -13,7 +13,14 @@ and writes <out>/<workload>_kernel_stats.csv and <out>/<workload>_summary.json
 (bench.py's roofline reads the newest round's summary of its workload), stamped
 with the sha256 of the libptgpu.so the passes ran (bench.py reports pmc_stale
 when it loads a different one).  The PMC passes run with PT_PIPELINE=0.
-Usage: python tools/profile_summary.py <workload> <out_dir> [prof_dir] [lib]
+Frame batches (round 6): when bench.py's timed launches render F frames each
+(--frames-per-launch; the C3 line renders 8), pass F: the timed kernel is then
+the frame-batch instantiation (MF), and every count of the summary -- HBM
+bytes, SQ / TCC counters, the durations' per-frame fields -- is per FRAME (the
+per-launch count / F), which is what bench.py's roofline divides by its
+per-frame interval; `avg_ms` / `isolated_avg_ms` stay per launch (they must
+agree with the kernel-trace files beside them).
+Usage: python tools/profile_summary.py <workload> <out_dir> [prof_dir] [lib] [frames_per_launch]
 """
 import collections
 import csv
@@ -32,11 +39,15 @@ KERNELS = {"c5": "render_kernel<false, false, false, true, false", "c5big": "ren
 KERNEL = "render_kernel<false, false, false, false, false"
 
 
+FPL = 1  # frames per timed launch
+
+
 def timed(name):
-    """The workload's timed render launch: the kernel prefix, and not the
-    frame-batch instantiation (last template argument MF = true), which the
-    N = 1 line's frame_batch field also launches in the profiled process."""
-    return KERNEL in name and ", true>(" not in name
+    """The workload's timed render launch: the kernel prefix, and the
+    frame-batch instantiation (last template argument MF = true) exactly when
+    the timed launches render several frames each (the profiled process also
+    launches the other one: single frames, per-launch companions)."""
+    return KERNEL in name and ((", true>(" in name) == (FPL > 1))
 
 
 def _pmc(path):
@@ -50,11 +61,12 @@ def _pmc(path):
 
 
 def main():
-    global KERNEL
+    global KERNEL, FPL
     workload, out = sys.argv[1], sys.argv[2]
+    FPL = int(sys.argv[5]) if len(sys.argv) > 5 else 1
     KERNEL = KERNELS.get(workload, KERNEL)
     prof = sys.argv[3] if len(sys.argv) > 3 else "gpurun_out/prof"
-    lib = sys.argv[4] if len(sys.argv) > 4 else os.path.join(os.path.dirname(os.path.dirname(
+    lib = sys.argv[4] if len(sys.argv) > 4 and sys.argv[4] else os.path.join(os.path.dirname(os.path.dirname(
         os.path.abspath(__file__))), "dsgpuraytracing_amd", "libptgpu.so")
     os.makedirs(out, exist_ok=True)
     ks = os.path.join(prof, "kt", "kt_kernel_stats.csv")
@@ -67,10 +79,13 @@ def main():
     if os.path.exists(ksi):
         shutil.copy(ksi, os.path.join(out, f"{workload}_kernel_stats_isolated.csv"))
         iso = next(v for k, v in {r["Name"]: r for r in csv.DictReader(open(ksi))}.items() if timed(k))
-    fetch = _pmc(os.path.join(prof, "fetch", "fetch_counter_collection.csv"))
-    write = _pmc(os.path.join(prof, "write", "write_counter_collection.csv"))
-    sq = _pmc(os.path.join(prof, "sq", "sq_counter_collection.csv"))
-    tcc = _pmc(os.path.join(prof, "tcc", "tcc_counter_collection.csv"))
+    def per_frame(d):  # a batch launch's counts per frame
+        return {k: v / FPL for k, v in d.items()}
+
+    fetch = per_frame(_pmc(os.path.join(prof, "fetch", "fetch_counter_collection.csv")))
+    write = per_frame(_pmc(os.path.join(prof, "write", "write_counter_collection.csv")))
+    sq = per_frame(_pmc(os.path.join(prof, "sq", "sq_counter_collection.csv")))
+    tcc = per_frame(_pmc(os.path.join(prof, "tcc", "tcc_counter_collection.csv")))
     for name, d in (("fetch", fetch), ("write", write), ("sq", sq), ("tcc", tcc)):
         src = os.path.join(prof, name, f"{name}_counter_collection.csv")
         if os.path.exists(src):
@@ -83,6 +98,9 @@ def main():
     s = {
         "workload": workload,
         "kernel": KERNEL,
+        "kernel_name": next(k for k in stats if timed(k)),
+        "frames_per_launch": FPL,
+        "counts_per": "frame",
         "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
         "kernel_sha256": kernel_sha256(lib),
         "calls": int(render["Calls"]),
@@ -90,8 +108,12 @@ def main():
         "isolated_avg_ms": float(iso["AverageNs"]) / 1e6 if iso else None,
         "resolve_avg_ms": float(resolve["AverageNs"]) / 1e6 if resolve else None,
     }
+    if FPL > 1:
+        s["avg_ms_per_frame"] = s["avg_ms"] / FPL
+        s["isolated_avg_ms_per_frame"] = s["isolated_avg_ms"] / FPL if iso else None
     if iso:  # utilisation over the kernel's own duration, not an overlapped span
         avg_ns = float(iso["AverageNs"])
+    avg_ns /= FPL  # (per frame, as the counts)
     if "FETCH_SIZE" in fetch and "WRITE_SIZE" in write:
         s["fetch_size_kb"] = fetch["FETCH_SIZE"]
         s["write_size_kb"] = write["WRITE_SIZE"]
