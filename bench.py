@@ -566,6 +566,7 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
     single_ms = None
     frame_batch = None
     iso_ms = 0.0
+    iso_single_ms = None
     if world == 1:
         # one frame alone, synchronised on both sides (no overlap with a
         # neighbouring frame): the wall-clock render time of ONE frame, and
@@ -587,6 +588,20 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
         single_api_ms = float(np.median(api)) * 1e3
         sync_floor_ms = float(np.median(idle)) * 1e3
         iso_ms = float(np.median(dev.launch_times(5)[0]))
+        iso_single_ms = iso_ms
+        if fpl > 1 and args.emulate_shard <= 1:
+            # the timed kernel is the frame batch's: its own duration alone on
+            # the GPU (a lone launch of fpl frames, synchronised on both sides),
+            # per frame -- the roofline's isolated fraction divides the per-frame
+            # counts of the same 8-frame launches (profiles/<round>/c3_summary.json)
+            isb = []
+            for _ in range(3):
+                torch.cuda.synchronize()
+                dev.render_frames_device(mine_arr, [frame.data_ptr()] * fpl, [SEED] * fpl, stream)
+                torch.cuda.synchronize()
+                # (frames the launch held: larger frames render one per launch)
+                isb.append(dev.launch_times(1)[0][0] / max(1, dev.stats()["frames_per_launch"]))
+            iso_ms = float(np.median(isb))
         # the drop-in pt_render_tiles path: output copied to a host buffer (PCIe-inclusive)
         host = np.zeros((H, W, 3), np.float32)
         dev.render_tiles(mine_arr, host)
@@ -655,6 +670,9 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
                        "single_frame_ms": None if single_ms is None else round(single_ms, 3),
                        # host time inside the render call (launch preparation) and an idle synchronize
                        "single_frame_api_ms": None if single_ms is None else round(single_api_ms, 4),
+                       # the render kernel of ONE frame alone (one frame per launch, HIP events);
+                       # roofline.isolated_kernel_ms is the timed launch's own: per frame of a lone batch
+                       "single_frame_kernel_ms": None if iso_single_ms is None else round(iso_single_ms, 4),
                        "sync_floor_ms": None if single_ms is None else round(sync_floor_ms, 4),
                        "bvh": bvh_desc(args.lbvh),
                        "upload_s": round(t_up, 4),

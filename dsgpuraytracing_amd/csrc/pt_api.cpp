@@ -1466,6 +1466,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* const* outs, in
   c->last.bvh_stack = c->bvh_stack;
   c->last.bvh_nodes = (int64_t)c->n_render_nodes;
   c->last.samples = px * c->params.spp;
+  c->last.frames_per_launch = nf;
   return PT_OK;
 }
 

@@ -188,6 +188,7 @@ class Device:
         out["lane_iters"] = list(s.lane_iters)
         out["footprint"] = list(s.footprint)
         out["node_census"] = list(s.node_census)
+        out["frames_per_launch"] = int(s.frames_per_launch)
         return out
 
     def launch_times(self, n: int = 256):

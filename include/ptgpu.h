@@ -231,6 +231,9 @@ typedef struct pt_stats {
                               candidate); lanes at the first stepping lane's node; stepping lanes; steps and
                               lanes inside the top two BVH4 levels below the root (node index < 21 in the
                               breadth-first order); the same for three levels (< 85) */
+  int32_t frames_per_launch; /* frames the last render launch held (pt_render_frames_device batches: up to
+                                PT_MAX_FRAMES; 1 otherwise) */
+  int32_t reserved0;
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */
