@@ -599,9 +599,12 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
                 torch.cuda.synchronize()
                 dev.render_frames_device(mine_arr, [frame.data_ptr()] * fpl, [SEED] * fpl, stream)
                 torch.cuda.synchronize()
-                # (frames the launch held: larger frames render one per launch)
-                isb.append(dev.launch_times(1)[0][0] / max(1, dev.stats()["frames_per_launch"]))
-            iso_ms = float(np.median(isb))
+                nfl = dev.stats()["frames_per_launch"]
+                if nfl <= 1:  # larger frames render one per launch: the lone single frame above
+                    break
+                isb.append(dev.launch_times(1)[0][0] / nfl)
+            if isb:
+                iso_ms = float(np.median(isb))
         # the drop-in pt_render_tiles path: output copied to a host buffer (PCIe-inclusive)
         host = np.zeros((H, W, 3), np.float32)
         dev.render_tiles(mine_arr, host)
