@@ -1066,3 +1066,45 @@ def test_frame_batch_is_bit_identical_to_single_frames(name, w, h, packed):
             dev.render_frames_device(arr, [0] * 9, list(range(9)), stream.cuda_stream)
     finally:
         dev.close()
+
+
+def test_frame_batch_of_large_frames_renders_one_per_launch():
+    """Frames of more than PT_BATCH_SLOTS (32) work slots per lane render one
+    per launch inside pt_render_frames_device (they fill the GPU alone; C4
+    batched measured slower): the call still renders every frame, each equal
+    to its own pt_render_tiles_device call, and reports one frame per launch."""
+    import torch
+
+    from dsgpuraytracing_amd import scenes
+    from dsgpuraytracing_amd.pathtracer import Device
+
+    w, h, spp = 1920, 1080, 64
+    sc = Scene.from_dae(scenes.proxy_path(1), w, h)
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream(device=0)
+    dev = Device(0)
+    try:
+        dev.upload_scene(sc)
+        dev.set_camera(sc.camera)
+        dev.set_params(w, h, spp, 4, 1, 1)
+        arr = np.asarray(tile_fifo(w, h), np.int32).reshape(-1, 4)
+        seeds = [31, 32]
+        outs = [torch.zeros((h * w * 3,), dtype=torch.float32, device="cuda:0") for _ in seeds]
+        dev.render_frames_device(arr, [o.data_ptr() for o in outs], seeds, stream.cuda_stream, out_floats=h * w * 3)
+        torch.cuda.synchronize()
+        assert dev.stats()["frames_per_launch"] == 1
+        for s, o in zip(seeds, outs):
+            ref = torch.zeros_like(o)
+            dev.set_params(w, h, spp, 4, 1, s)
+            dev.render_tiles_device(arr, ref.data_ptr(), stream.cuda_stream)
+            torch.cuda.synchronize()
+            assert torch.equal(o, ref), s
+        # a small frame of the same scene is batched
+        dev.set_params(128, 128, 8, 4, 1, 1)
+        small = np.asarray(tile_fifo(128, 128), np.int32).reshape(-1, 4)
+        so = [torch.zeros((128 * 128 * 3,), dtype=torch.float32, device="cuda:0") for _ in range(3)]
+        dev.render_frames_device(small, [o.data_ptr() for o in so], [1, 2, 3], stream.cuda_stream)
+        torch.cuda.synchronize()
+        assert dev.stats()["frames_per_launch"] == 3
+    finally:
+        dev.close()
