@@ -327,6 +327,20 @@ def main():
     ap.add_argument("--emulate-shard", type=int, default=0,
                     help="diagnostic: render only one rank's share of an N-GPU split on this one GPU")
     ap.add_argument("--emulate-rank", type=int, default=0, help="the rank --emulate-shard renders")
+    ap.add_argument("--split-tile", type=int, default=32,
+                    help="tile edge of the strong split's deal (16 or 32; the reference's FIFO is 32x32): "
+                         "smaller tiles spread each rank's share more evenly over the frame")
+    ap.add_argument("--tile", type=int, default=32,
+                    help="diagnostic: tile edge of the one-GPU (and weak) tile FIFO (8, 16 or 32)")
+    ap.add_argument("--tile-order", default="rows", choices=["rows", "morton"],
+                    help="diagnostic: order of the tile FIFO (rows: the reference's row-major queue; morton: "
+                         "Z-order of the tiles) -- the same image in any order")
+    ap.add_argument("--deal-block", type=int, default=0,
+                    help="edge of the blocks the strong split deals (default: --split-tile); 16x16 tiles dealt "
+                         "by 32x32 blocks keep each block's four tiles on one rank")
+    ap.add_argument("--split-deal", default="auto",
+                    help="the strong split's tile deal (dist.tile_owner: auto = diag3 at N >= 8, diag below; diag, "
+                         "diagK, mod)")
     ap.add_argument("--frames-per-launch", type=int, default=0,
                     help="frames rendered per launch (pt_render_frames_device, 1..8; the library renders frames "
                          "of more than 32 work slots per lane one per launch): a frame batch shares one "
@@ -372,6 +386,24 @@ def main():
         dist.destroy_process_group()
 
 
+def ordered_tiles(tiles, order="rows"):
+    """The tile FIFO in `order`: "rows" keeps the reference's row-major queue
+    (pathtracer.cpp:209-214); "morton" sorts the tiles by the Z-order of their
+    (column, row) -- a launch's blocks follow its tile list, so the order sets
+    which pixels the waves in flight share.  Images are per pixel and sample:
+    identical in any order."""
+    if order == "rows" or not tiles:
+        return list(tiles)
+    t = min(min(w, h) for (_, _, w, h) in tiles)
+
+    def z(tile):
+        c, r, k = tile[0] // t, tile[1] // t, 0
+        for b in range(16):
+            k |= ((c >> b) & 1) << (2 * b) | ((r >> b) & 1) << (2 * b + 1)
+        return k
+    return sorted(tiles, key=z)
+
+
 def xchg_opts():
     """The strong split's exchange: on the current stream behind the resolve
     (default), or on a side stream with PT_XCHG_SIDE=1 (A/Bs:
@@ -409,18 +441,23 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
     dev.set_params(W, H, SPP, DEPTH, NSL, SEED, sample_base=SPP * rank if weak else 0)
     t_load = time.perf_counter() - t_load
 
-    tiles = tile_fifo(W, H)
+    # the strong split deals tiles of --split-tile pixels (the same image for
+    # any tiling: values are per pixel and sample)
+    split = world > 1 and not weak or args.emulate_shard > 1
+    tiles = ordered_tiles(tile_fifo(W, H, args.split_tile if split else args.tile), args.tile_order)
     frame = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{local}")
     stream = torch.cuda.current_stream().cuda_stream
 
     # strong: this rank's share of the tiles; weak (and one GPU): every tile
     mine_arr = np.asarray(tiles, dtype=np.int32).reshape(-1, 4)
     if args.emulate_shard > 1:
-        mine_arr = np.asarray(shard_tiles(tiles, args.emulate_rank, args.emulate_shard, "diag"),
+        mine_arr = np.asarray(shard_tiles(tiles, args.emulate_rank, args.emulate_shard, args.split_deal,
+                                          args.deal_block or args.split_tile),
                               dtype=np.int32).reshape(-1, 4)
     # strong: packed tiles, the gather queued behind each frame's resolve
     fpl = 1 if weak else max(1, min(8, args.frames_per_launch or 8))
-    pex = (PipelinedExchange(tiles, W, H, rank, world, frame.device, buffers=max(2, fpl), **xchg_opts())
+    pex = (PipelinedExchange(tiles, W, H, rank, world, frame.device, buffers=max(2, fpl), deal=args.split_deal,
+                             tile_size=args.split_tile, deal_block=args.deal_block, **xchg_opts())
            if world > 1 and not weak else None)
     if args.emulate_shard > 1:
         # one rank's share through the same packed render + exchange (here a
@@ -428,7 +465,7 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
         # a one-rank RCCL group with PT_DIST_FORCE=1 -- the gather's link time
         # is not in it), host overheads included
         pex = PipelinedExchange([tuple(int(v) for v in t) for t in mine_arr], W, H, 0, 1, frame.device,
-                                buffers=max(2, fpl), **xchg_opts())
+                                buffers=max(2, fpl), tile_size=args.split_tile, **xchg_opts())
     if pex is not None:
         mine_arr = np.asarray(pex.mine, dtype=np.int32).reshape(-1, 4)
 
@@ -470,7 +507,7 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
             k = kframe[0]
             kframe[0] += 1
             buf = pex.packed_for(k)
-            guard.run(dev.render_tiles_device, mine_arr, buf.data_ptr(), stream, stats=stats, packed=True,
+            guard.run(dev.render_tiles_device, mine_arr, buf.data_ptr(), stream, stats=stats, packed=pex.ex.slot,
                       out_floats=buf.numel())
             pex.exchange(k, frame, timed=timed)
         return guard.run(dev.stats) if stats else None
@@ -493,7 +530,7 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
                 kframe[0] += m
                 bufs = [pex.packed_for(k) for k in ks]
                 guard.run(dev.render_frames_device, mine_arr, [b.data_ptr() for b in bufs], [SEED] * m, stream,
-                          packed=True, out_floats=bufs[0].numel())
+                          packed=pex.ex.slot, out_floats=bufs[0].numel())
                 for k in ks:
                     pex.exchange(k, frame, timed=timed)
             done += m
@@ -560,7 +597,9 @@ def bench_run(args, backend, local, rank, world, StepGuard, PipelinedExchange, c
     if world > 1 and not args.no_extras:
         # every rank takes part (collectives inside)
         multi = multi_gpu_companions(local, rank, world, backend, StepGuard, PipelinedExchange,
-                                     frames=max(3, min(args.steps, 10)), with_weak=not weak)
+                                     frames=max(3, min(args.steps, 10)), with_weak=not weak,
+                                     split_tile=args.split_tile, split_deal=args.split_deal,
+                                     deal_block=args.deal_block)
 
     host_ms = None
     single_ms = None
@@ -826,7 +865,7 @@ def timed_max(el, backend, local):
 
 
 def multi_gpu_companions(local, rank, world, backend, StepGuard, PipelinedExchange, frames=5, warmup=2,
-                         with_weak=True):
+                         with_weak=True, split_tile=32, split_deal="diag", deal_block=0):
     """N > 1 companions (never `value`), same clock as the headline (barrier +
     synchronise on both sides of `frames` back-to-back frames, max over
     ranks):
@@ -855,8 +894,9 @@ def multi_gpu_companions(local, rank, world, backend, StepGuard, PipelinedExchan
     dev.set_camera(sc.camera)
     dev.set_params(w, h, spp, DEPTH, NSL, SEED)
     frame = torch.zeros((h, w, 3), dtype=torch.float32, device=f"cuda:{local}")
-    tiles = tile_fifo(w, h)
-    pex = PipelinedExchange(tiles, w, h, rank, world, frame.device, **xchg_opts())
+    tiles = tile_fifo(w, h, split_tile)
+    pex = PipelinedExchange(tiles, w, h, rank, world, frame.device, deal=split_deal, tile_size=split_tile,
+                            deal_block=deal_block, **xchg_opts())
     mine = np.asarray(pex.mine, dtype=np.int32).reshape(-1, 4)
     guard = StepGuard()
     kf = [0]
@@ -865,7 +905,7 @@ def multi_gpu_companions(local, rank, world, backend, StepGuard, PipelinedExchan
         k = kf[0]
         kf[0] += 1
         buf = pex.packed_for(k)
-        guard.run(dev.render_tiles_device, mine, buf.data_ptr(), stream, packed=True, out_floats=buf.numel(),
+        guard.run(dev.render_tiles_device, mine, buf.data_ptr(), stream, packed=pex.ex.slot, out_floats=buf.numel(),
                   stats=stats)
         pex.exchange(k, frame, timed=timed)
 

@@ -1248,7 +1248,7 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* const* outs, in
   P.env_rphi = c->env_rphi.p;
   P.tiles = c->tiles[slot].p;
   P.out = outs[0];
-  P.packed = (flags & PT_FLAG_PACKED) ? 1 : 0;
+  P.packed = (flags & PT_FLAG_PACKED16) ? 16 : (flags & PT_FLAG_PACKED) ? 32 : 0;
   P.work_counter = c->counter[slot].p;
   P.stats = c->stats.p;
   P.dbg_pix = -1;
@@ -1551,7 +1551,8 @@ int pt_render_tiles(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, float* hdr
   if (rc) return rc;
   if ((rc = tile_launch(c))) return rc;  // earlier asynchronous tiles first (call order)
   if (n_tiles < 0 || (n_tiles > 0 && (!tiles || !hdr_out_host))) return fail(PT_E_INVALID, "pt_render_tiles: bad args");
-  if (flags & PT_FLAG_PACKED) return fail(PT_E_INVALID, "pt_render_tiles: PT_FLAG_PACKED is for pt_render_tiles_device");
+  if (flags & (PT_FLAG_PACKED | PT_FLAG_PACKED16))
+    return fail(PT_E_INVALID, "pt_render_tiles: packed output is for pt_render_tiles_device");
   HIPCHK(hipSetDevice(c->device));
   std::vector<int4> tl;
   if ((rc = build_tiles(c, tiles, n_tiles, tl))) return rc;
@@ -1576,6 +1577,21 @@ int pt_render_tiles(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, float* hdr
   return finish_stats(c, c->stream, flags, true);
 }
 
+// PT_FLAG_PACKED / PT_FLAG_PACKED16: tile i -> packed slot i, so no clipping
+// or splitting may renumber tiles: every tile 1..S x 1..S and inside the frame
+static int check_packed(const pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, uint32_t flags, const char* fn) {
+  if (!(flags & (PT_FLAG_PACKED | PT_FLAG_PACKED16))) return PT_OK;
+  const int S = (flags & PT_FLAG_PACKED16) ? 16 : 32;
+  const int W = c->params.width, H = c->params.height;
+  for (int32_t i = 0; i < n_tiles; ++i) {
+    const pt_tile& t = tiles[i];
+    if (t.w < 1 || t.h < 1 || t.w > S || t.h > S || t.x < 0 || t.y < 0 || t.x + t.w > W || t.y + t.h > H)
+      return fail(PT_E_INVALID, std::string(fn) + ": packed output needs tiles of 1.." + std::to_string(S) + " x 1.." +
+                                    std::to_string(S) + " inside the frame");
+  }
+  return PT_OK;
+}
+
 int pt_render_tiles_device(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, float* hdr_out_dev, void* stream,
                            uint32_t flags) {
   int rc = check_ready(c);
@@ -1586,14 +1602,7 @@ int pt_render_tiles_device(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, flo
   HIPCHK(hipSetDevice(c->device));
   std::vector<int4> tl;
   if ((rc = build_tiles(c, tiles, n_tiles, tl))) return rc;
-  if (flags & PT_FLAG_PACKED) {  // tile i -> packed slot i: no clipping or splitting may renumber tiles
-    const int W = c->params.width, H = c->params.height;
-    for (int32_t i = 0; i < n_tiles; ++i) {
-      const pt_tile& t = tiles[i];
-      if (t.w < 1 || t.h < 1 || t.w > 32 || t.h > 32 || t.x < 0 || t.y < 0 || t.x + t.w > W || t.y + t.h > H)
-        return fail(PT_E_INVALID, "pt_render_tiles_device: PT_FLAG_PACKED needs tiles of 1..32 x 1..32 inside the frame");
-    }
-  }
+  if (int rc2 = check_packed(c, tiles, n_tiles, flags, "pt_render_tiles_device")) return rc2;
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   if ((rc = launch(c, tl, &hdr_out_dev, 1, nullptr, s, flags))) return rc;
   return finish_stats(c, s, flags, false);
@@ -1646,14 +1655,7 @@ int pt_render_frames_device(pt_ctx* c, const pt_tile* tiles, int32_t n_tiles, in
   HIPCHK(hipSetDevice(c->device));
   std::vector<int4> tl;
   if ((rc = build_tiles(c, tiles, n_tiles, tl))) return rc;
-  if (flags & PT_FLAG_PACKED) {
-    const int W = c->params.width, H = c->params.height;
-    for (int32_t i = 0; i < n_tiles; ++i) {
-      const pt_tile& t = tiles[i];
-      if (t.w < 1 || t.h < 1 || t.w > 32 || t.h > 32 || t.x < 0 || t.y < 0 || t.x + t.w > W || t.y + t.h > H)
-        return fail(PT_E_INVALID, "pt_render_frames_device: PT_FLAG_PACKED needs tiles of 1..32 x 1..32 inside the frame");
-    }
-  }
+  if (int rc2 = check_packed(c, tiles, n_tiles, flags, "pt_render_frames_device")) return rc2;
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   // One launch for the batch in the plain common build; the environment-light
   // and global-table builds, diagnostics and PT_FRAME_BATCH=0 render the

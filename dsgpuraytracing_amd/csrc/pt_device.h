@@ -276,7 +276,8 @@ struct KParams {
   const struct EnvRec* env_rphi;    // bucket records of the rows of env_pphi (h x PT_ENV_GUIDE)
   const int4* tiles;  // (x, y, w, h)
   float* out;         // W*H*3, or n_tiles*1024*3 when packed
-  int packed;         // PT_FLAG_PACKED: tile i's pixel (x, y) -> out[3 * (i*1024 + (y-ty)*32 + (x-tx))]
+  int packed;         // packed slot edge S (PT_FLAG_PACKED: 32, PT_FLAG_PACKED16: 16; 0: the frame):
+                      // tile i's pixel (x, y) -> out[3 * (i*S*S + (y-ty)*S + (x-tx))]
   float* partial;     // 3 floats per work slot: each sample group's sum, resolved into `out` in group order
   const int4* blocks;  // (x, y, w<=8, h<=8): footprint-clipped pixel blocks of the tiles
   int n_blocks;

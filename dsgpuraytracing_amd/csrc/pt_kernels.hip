@@ -1722,8 +1722,9 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
   if (ti == 0)
     for (int i = tid; i < PT_QUEUE_WORDS * PT_QUEUE_HEADS; i += 256) P.work_counter[i] = 0u;
   auto out_at = [&](int x, int y) -> float* {
-    const size_t o = P.packed ? (size_t)ti * 1024u + (size_t)(y - tile.y) * 32u + (size_t)(x - tile.x)
-                              : (size_t)x + (size_t)y * (size_t)P.W;
+    const size_t ps = (size_t)P.packed;  // packed slot edge (32, or 16 with PT_FLAG_PACKED16); 0: the frame
+    const size_t o = ps ? (size_t)ti * ps * ps + (size_t)(y - tile.y) * ps + (size_t)(x - tile.x)
+                        : (size_t)x + (size_t)y * (size_t)P.W;
     return P.out + 3 * o;
   };
   for (int i = tid; i < 1024; i += 256) {

@@ -34,37 +34,45 @@ Tile = Tuple[int, int, int, int]
 TILE = 32
 
 
-def tile_owner(tile: Tile, index: int, world: int, deal: str = "mod") -> int:
+def tile_owner(tile: Tile, index: int, world: int, deal: str = "mod", tile_size: int = TILE) -> int:
     """Rank that renders `tile` (FIFO position `index`).  "mod": tile_id mod
     world; "diag": (column + row) mod world, so a rank's tiles also spread
     over every column when the row length is a multiple of world (plain mod
-    then deals whole columns); "diag3": (column + 3*row) mod world."""
-    col, row = tile[0] // TILE, tile[1] // TILE
+    then deals whole columns); "diagK": (column + K*row) mod world; "auto":
+    diag3 at 8 or more ranks, diag below.  Columns
+    and rows count tiles of `tile_size` pixels (the FIFO's tile edge)."""
+    col, row = tile[0] // tile_size, tile[1] // tile_size
     if deal == "mod":
         return index % world
-    if deal == "diag":
-        return (col + row) % world
-    if deal == "diag3":
-        return (col + 3 * row) % world
+    if deal == "auto":
+        # the measured best per world size (C3, slowest rank's share with the
+        # RCCL exchange in the loop: profiles/r6/ab_split_deal.txt): diag3 at
+        # 8 ranks (0.21 vs diag's 0.23 ms), diag below (N = 4: 0.317 vs
+        # 0.322; N = 2 the two are the same checkerboard)
+        deal = "diag3" if world >= 8 else "diag"
+    if deal.startswith("diag") and (deal[4:] == "" or deal[4:].isdigit()):
+        # "diagK": (column + K * row) mod world
+        return (col + int(deal[4:] or 1) * row) % world
     raise ValueError(f"unknown tile deal {deal!r}")
 
 
-def shard_tiles(tiles: Sequence[Tile], rank: int, world: int, deal: str = "mod") -> List[Tile]:
+def shard_tiles(tiles: Sequence[Tile], rank: int, world: int, deal: str = "mod", tile_size: int = TILE) -> List[Tile]:
     if world < 1 or not 0 <= rank < world:
         raise ValueError(f"bad rank/world {rank}/{world}")
     if deal == "mod":
         return list(tiles[rank::world])
-    return [t for i, t in enumerate(tiles) if tile_owner(t, i, world, deal) == rank]
+    return [t for i, t in enumerate(tiles) if tile_owner(t, i, world, deal, tile_size) == rank]
 
 
-def packed_index(tiles: Sequence[Tile], width: int, slot0: int = 0):
+def packed_index(tiles: Sequence[Tile], width: int, slot0: int = 0, slot: int = TILE):
     """(packed pixel index, frame pixel index) pairs of every pixel of `tiles`
-    in the PT_FLAG_PACKED layout (tile i -> slots [(slot0+i)*1024, +1024),
-    pixel (x, y) at (y-ty)*32 + (x-tx)); frame index x + y*width."""
+    in the packed layout of `slot` x `slot` slots (PT_FLAG_PACKED: 32,
+    PT_FLAG_PACKED16: 16; tile i -> [(slot0+i)*slot^2, +slot^2), pixel (x, y)
+    at (y-ty)*slot + (x-tx)); frame index x + y*width."""
     src, dst = [], []
     for i, (tx, ty, tw, th) in enumerate(tiles):
         ly, lx = np.meshgrid(np.arange(th), np.arange(tw), indexing="ij")
-        src.append(((slot0 + i) * TILE * TILE + ly * TILE + lx).ravel())
+        src.append(((slot0 + i) * slot * slot + ly * slot + lx).ravel())
         dst.append(((ty + ly) * width + tx + lx).ravel())
     if not src:
         return np.zeros(0, np.int64), np.zeros(0, np.int64)
@@ -84,7 +92,8 @@ class TileExchange:
     current stream's work, not after the pt_ctx's own stream."""
 
     def __init__(self, tiles: Sequence[Tile], width: int, height: int, rank: int, world: int, device,
-                 dst: int = 0, group=None, deal: str = "diag", buffers: int = 1):
+                 dst: int = 0, group=None, deal: str = "diag", buffers: int = 1, tile_size: int = TILE,
+                 deal_block: int = 0):
         import torch
 
         self.rank, self.world, self.dst, self.group = rank, world, dst, group
@@ -93,18 +102,26 @@ class TileExchange:
         # pathtracer.cpp:594-595); packed slots hold the clamped tiles
         tiles = [(x, y, min(w, width - x), min(h, height - y)) for (x, y, w, h) in tiles]
         self.deal = deal
-        self.mine = shard_tiles(tiles, rank, world, deal)
-        self.slots = max(len(shard_tiles(tiles, r, world, deal)) for r in range(world))
+        # the deal counts columns and rows of `deal_block` pixels (default: the
+        # tile edge); 16x16 tiles dealt by 32x32 blocks keep a block's four
+        # tiles on one rank
+        db = deal_block or tile_size
+        self.mine = shard_tiles(tiles, rank, world, deal, db)
+        self.slots = max(len(shard_tiles(tiles, r, world, deal, db)) for r in range(world))
         # `buffers` packed buffers (PipelinedExchange: 2); `packed` is the current one
-        self.bufs = [torch.zeros((max(self.slots, 1), TILE * TILE, 3), dtype=torch.float32, device=device)
+        # packed slots of the deal's tile edge (PT_FLAG_PACKED16 for 16x16 tiles)
+        self.slot = 16 if tile_size <= 16 else TILE
+        self.bufs = [torch.zeros((max(self.slots, 1), self.slot * self.slot, 3), dtype=torch.float32, device=device)
                      for _ in range(max(1, buffers))]
         self.packed = self.bufs[0]
         self.recv = None
         if rank == dst:
-            self.recv = torch.zeros((world, max(self.slots, 1), TILE * TILE, 3), dtype=torch.float32, device=device)
+            self.recv = torch.zeros((world, max(self.slots, 1), self.slot * self.slot, 3), dtype=torch.float32,
+                                    device=device)
             src, dstix = [], []
             for r in range(world):
-                s, d = packed_index(shard_tiles(tiles, r, world, deal), width, slot0=r * max(self.slots, 1))
+                s, d = packed_index(shard_tiles(tiles, r, world, deal, db), width, slot0=r * max(self.slots, 1),
+                                    slot=self.slot)
                 src.append(s)
                 dstix.append(d)
             src, dstix = np.concatenate(src), np.concatenate(dstix)
@@ -177,14 +194,15 @@ class PipelinedExchange:
     those of TileExchange, bit for bit."""
 
     def __init__(self, tiles: Sequence[Tile], width: int, height: int, rank: int, world: int, device,
-                 dst: int = 0, group=None, deal: str = "diag", side: bool = False, buffers: int = 2):
+                 dst: int = 0, group=None, deal: str = "diag", side: bool = False, buffers: int = 2,
+                 tile_size: int = TILE, deal_block: int = 0):
         import torch
 
         # `buffers` packed buffers, frame k in buffer k % buffers: at least the
         # frames of one frame batch (bench.py --frames-per-launch), whose
         # resolves all run before the batch's exchanges
         self.ex = TileExchange(tiles, width, height, rank, world, device, dst=dst, group=group, deal=deal,
-                               buffers=max(2, buffers))
+                               buffers=max(2, buffers), tile_size=tile_size, deal_block=deal_block)
         self.mine = self.ex.mine
         self.cuda = self.ex.bufs[0].is_cuda
         # side=False (default): the exchange is queued on the current stream

@@ -25,6 +25,7 @@ PT_LIGHT_ENVIRONMENT = 4
 PT_FLAG_STATS = 1
 PT_FLAG_REF_COUNTS = 2
 PT_FLAG_PACKED = 4
+PT_FLAG_PACKED16 = 8
 PT_MAX_FRAMES = 8  # frames per pt_render_frames_device launch (include/ptgpu.h)
 
 PRIM_SPHERE, PRIM_TRIANGLE = 0, 1

@@ -108,25 +108,26 @@ class Device:
 
     def render_tiles_device(self, tiles, out_ptr: int, stream: int = 0, stats: bool = False, packed: bool = False,
                             out_floats: Optional[int] = None):
-        """packed=True: out_ptr holds len(tiles)*32*32*3 floats, tile i's pixel
-        (x, y) at [(i*1024 + (y-ty)*32 + (x-tx))*3] (PT_FLAG_PACKED); else a
+        """packed=True (or 32): out_ptr holds len(tiles)*32*32*3 floats, tile
+        i's pixel (x, y) at [(i*1024 + (y-ty)*32 + (x-tx))*3] (PT_FLAG_PACKED);
+        packed=16: 16x16 slots (PT_FLAG_PACKED16, tiles <= 16x16); else a
         whole H x W x 3 frame.  out_floats: the buffer's size in floats, checked
         against what the layout writes (the library sees only a pointer)."""
         keep, arr = self._tiles(tiles)
         if out_floats is not None:
             if getattr(self, "_frame", None) is None:
                 raise ValueError("render_tiles_device: set_params first")
-            need = len(keep) * 1024 * 3 if packed else self._frame[0] * self._frame[1] * 3
+            need = len(keep) * _slot(packed) ** 2 * 3 if packed else self._frame[0] * self._frame[1] * 3
             if out_floats < need:
                 raise ValueError(f"render_tiles_device: output holds {out_floats} floats, the "
                                  f"{'packed' if packed else 'frame'} layout writes {need}")
-        flags = _flags(stats) | (native.PT_FLAG_PACKED if packed else 0)
+        flags = _flags(stats) | _packed_flag(packed)
         check(self._lib.pt_render_tiles_device(self.handle, arr, len(keep), ctypes.c_void_p(out_ptr),
                                                ctypes.c_void_p(stream or None), flags))
 
     def render_frames_device(self, tiles, out_ptrs, seeds, stream: int = 0, packed: bool = False,
                              out_floats: Optional[int] = None):
-        """pt_render_frames_device: len(seeds) (1..4) frames of the same tiles in
+        """pt_render_frames_device: len(seeds) (1..8) frames of the same tiles in
         one launch, frame f keyed by seeds[f] into out_ptrs[f] (each laid out as
         render_tiles_device's out_ptr); every image equals its own
         render_tiles_device call with that seed."""
@@ -137,13 +138,13 @@ class Device:
         if out_floats is not None:
             if getattr(self, "_frame", None) is None:
                 raise ValueError("render_frames_device: set_params first")
-            need = len(keep) * 1024 * 3 if packed else self._frame[0] * self._frame[1] * 3
+            need = len(keep) * _slot(packed) ** 2 * 3 if packed else self._frame[0] * self._frame[1] * 3
             if out_floats < need:
                 raise ValueError(f"render_frames_device: outputs hold {out_floats} floats, the "
                                  f"{'packed' if packed else 'frame'} layout writes {need}")
         sd = (ctypes.c_uint32 * n)(*[int(v) & 0xFFFFFFFF for v in seeds])
         op = (ctypes.c_void_p * n)(*[int(v) for v in out_ptrs])
-        flags = native.PT_FLAG_PACKED if packed else 0
+        flags = _packed_flag(packed)
         check(self._lib.pt_render_frames_device(self.handle, arr, len(keep), n, sd, op,
                                                 ctypes.c_void_p(stream or None), flags))
 
@@ -243,6 +244,17 @@ class State(enum.IntEnum):
     VISUALIZE = 2
     RENDERING = 3
     DONE = 4
+
+
+def _slot(packed) -> int:
+    """Packed slot edge of a `packed` argument: True / 32 -> 32, 16 -> 16."""
+    return 16 if packed == 16 else 32
+
+
+def _packed_flag(packed) -> int:
+    if not packed:
+        return 0
+    return native.PT_FLAG_PACKED16 if _slot(packed) == 16 else native.PT_FLAG_PACKED
 
 
 def tile_fifo(w: int, h: int, tile: int = TILE) -> List[Tuple[int, int, int, int]]:

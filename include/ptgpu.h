@@ -244,6 +244,9 @@ typedef struct pt_stats {
                              tile i's pixel (x, y) goes to [(i*1024 + (y-tile.y)*32 + (x-tile.x))*3]
                              (every tile 1..32 x 1..32 and inside the frame); the multi-GPU exchange
                              gathers these packed tiles instead of whole frames */
+#define PT_FLAG_PACKED16 8u /* as PT_FLAG_PACKED with 16x16 slots: n_tiles*16*16*3 floats, tile i's pixel
+                               (x, y) at [(i*256 + (y-tile.y)*16 + (x-tile.x))*3], every tile 1..16 x 1..16
+                               (the strong split dealing 16x16 tiles: a rank's share spread more evenly) */
 
 int pt_create(int device, pt_ctx** out);
 int pt_destroy(pt_ctx* ctx);

@@ -106,7 +106,7 @@ def test_pipelined_exchange_bit_identical_over_frames(tmp_path, restate, world):
     assert not np.array_equal(got[0], got[1])
 
 
-@pytest.mark.parametrize("deal", ["mod", "diag", "diag3"])
+@pytest.mark.parametrize("deal", ["mod", "diag", "diag3", "auto"])
 def test_shard_tiles_partition(deal):
     tiles = tile_fifo(1920, 1080)
     for world in (1, 2, 4, 8):
@@ -225,3 +225,67 @@ def test_value_knobs_must_agree(tmp_path, knob, value):
     assert [p.exitcode for p in ps] == [3, 3]
     for r in range(2):
         assert knob in open(tmp_path / f"knob{r}.txt").read()
+
+
+def _packed16_worker(rank, world, port, out_path, deal, deal_block=0):
+    """The strong split dealing 16x16 tiles (PT_FLAG_PACKED16 slots): each
+    rank fills its packed slots from the frame (the restatement's whole-frame
+    render, cheap at this size) and ONE gather + scatter assembles rank 0's."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dsgpuraytracing_amd.dist import TileExchange
+    from tests.oracle_helpers import Restatement, golden
+    img, _ = Restatement().render(golden("c1_default_64x64.scene.ptd"), W, H, SPP, rng_mode=1, threads=1)
+    ex = TileExchange(tile_fifo(W, H, 16), W, H, rank, world, torch.device("cpu"), deal=deal, tile_size=16,
+                      deal_block=deal_block)
+    assert ex.slot == 16 and ex.packed.shape[1] == 256
+    for i, (x, y, tw, th) in enumerate(ex.mine):
+        ex.packed[i].view(16, 16, 3)[:th, :tw] = torch.from_numpy(img[y:y + th, x:x + tw])
+    frame = torch.zeros((H, W, 3), dtype=torch.float32)
+    ex.exchange(frame)
+    if rank == 0:
+        np.save(out_path, frame.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,deal,block", [(2, "diag3", 0), (3, "diag5", 0), (2, "auto", 32)])
+def test_packed16_split_bit_identical(tmp_path, restate, world, deal, block):
+    from tests.oracle_helpers import golden
+    out = str(tmp_path / "frame16.npy")
+    mp.spawn(_packed16_worker, args=(world, _free_port(), out, deal, block), nprocs=world, join=True)
+    ref, _ = restate.render(golden("c1_default_64x64.scene.ptd"), W, H, SPP, rng_mode=1, threads=2)
+    assert np.array_equal(np.load(out), ref)
+
+
+@pytest.mark.parametrize("deal", ["diag", "diag3", "diag5"])
+def test_shard_tiles_partition_16(deal):
+    """16x16 tiles (bench.py --split-tile 16): a partition with equal counts
+    up to one tile per row, columns / rows counted in 16-px tiles."""
+    tiles = tile_fifo(1024, 1024, 16)
+    for world in (2, 4, 8):
+        shards = [shard_tiles(tiles, r, world, deal, 16) for r in range(world)]
+        assert sorted(t for s in shards for t in s) == sorted(tiles)
+        assert len({len(s) for s in shards}) == 1  # 64 x 64 tiles: exact
+    from dsgpuraytracing_amd.dist import packed_index
+    src, dst = packed_index([(0, 0, 16, 16), (16, 32, 8, 4)], 40, slot=16)
+    k = int(np.nonzero(dst == 33 * 40 + 17)[0][0])
+    assert src[k] == 256 + 1 * 16 + 1
+
+
+def test_auto_deal_and_deal_blocks():
+    """"auto" is diag3 at 8 or more ranks and diag below (the measured best:
+    profiles/r6/ab_split_deal.txt); a deal by 32-px blocks keeps the four
+    16x16 tiles of each block on one rank."""
+    from dsgpuraytracing_amd.dist import tile_owner
+    t32, t16 = tile_fifo(512, 256), tile_fifo(512, 256, 16)
+    for world, k in ((2, "diag"), (4, "diag"), (8, "diag3"), (16, "diag3")):
+        assert [tile_owner(t, i, world, "auto") for i, t in enumerate(t32)] == \
+            [tile_owner(t, i, world, k) for i, t in enumerate(t32)]
+    for world in (2, 8):
+        own32 = {(t[0], t[1]): tile_owner(t, i, world, "diag3") for i, t in enumerate(t32)}
+        for i, t in enumerate(t16):
+            assert tile_owner(t, i, world, "diag3", 32) == own32[(t[0] // 32 * 32, t[1] // 32 * 32)]
+        shards = [shard_tiles(t16, r, world, "diag3", 32) for r in range(world)]
+        assert sorted(t for s in shards for t in s) == sorted(t16)

@@ -1108,3 +1108,48 @@ def test_frame_batch_of_large_frames_renders_one_per_launch():
         assert dev.stats()["frames_per_launch"] == 3
     finally:
         dev.close()
+
+
+def test_packed16_tiles_match_frame():
+    """PT_FLAG_PACKED16 (16x16 slots: the strong split's 16x16 deal): every
+    rank's share of a diag3 deal, rendered packed -- one frame per launch and
+    as a frame batch -- and scattered back, equals the whole-frame render."""
+    import torch
+
+    from dsgpuraytracing_amd import scenes
+    from dsgpuraytracing_amd.dist import packed_index, shard_tiles
+    from dsgpuraytracing_amd.pathtracer import Device
+
+    w, h, spp = 200, 136, 8  # ragged last tile row and column
+    sc = Scene.from_dae(scenes.proxy_path(1), w, h)
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream(device=0)
+    dev = Device(0)
+    try:
+        dev.upload_scene(sc)
+        dev.set_camera(sc.camera)
+        dev.set_params(w, h, spp, 4, 1, 5)
+        whole = torch.zeros((h * w * 3,), dtype=torch.float32, device="cuda:0")
+        dev.render_tiles_device(np.asarray(tile_fifo(w, h), np.int32), whole.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        ref = whole.view(-1, 3).cpu()
+        tiles = [(x, y, min(16, w - x), min(16, h - y)) for (x, y, _, _) in tile_fifo(w, h, 16)]
+        got = torch.zeros_like(ref)
+        for r in range(3):
+            mine = shard_tiles(tiles, r, 3, "diag3", 16)
+            arr = np.asarray(mine, np.int32).reshape(-1, 4)
+            buf = torch.full((len(mine) * 256 * 3,), -1.0, dtype=torch.float32, device="cuda:0")
+            dev.render_tiles_device(arr, buf.data_ptr(), stream.cuda_stream, packed=16, out_floats=buf.numel())
+            bufs = [torch.full_like(buf, -1.0) for _ in range(2)]
+            dev.render_frames_device(arr, [b.data_ptr() for b in bufs], [5, 5], stream.cuda_stream, packed=16,
+                                     out_floats=buf.numel())
+            torch.cuda.synchronize()
+            assert torch.equal(bufs[0], buf) and torch.equal(bufs[1], buf)
+            src, dst = packed_index(mine, w, slot=16)
+            got[torch.from_numpy(dst)] = buf.view(-1, 3).cpu()[torch.from_numpy(src)]
+        assert torch.equal(got, ref)
+        with pytest.raises(RuntimeError):  # a 32x32 tile does not fit a 16x16 slot
+            dev.render_tiles_device(np.asarray([(0, 0, 32, 32)], np.int32), buf.data_ptr(), stream.cuda_stream,
+                                    packed=16)
+    finally:
+        dev.close()
