@@ -394,7 +394,7 @@ def ordered_tiles(tiles, order="rows"):
     identical in any order."""
     if order == "rows" or not tiles:
         return list(tiles)
-    t = min(min(w, h) for (_, _, w, h) in tiles)
+    t = max(max(w, h) for (_, _, w, h) in tiles)  # (the tile edge; clipped edge tiles are smaller)
 
     def z(tile):
         c, r, k = tile[0] // t, tile[1] // t, 0

@@ -217,6 +217,8 @@ struct pt_ctx {
   std::vector<int4> blocks_host[kSlots];
   DevBuf<int> tblock0[kSlots];           // first block of each tile (+ the end), for the resolve
   std::vector<int> tblock0_host[kSlots];
+  DevBuf<int> tout[kSlots];              // caller's index of each launched tile (a Z-ordered packed launch)
+  std::vector<int> tout_host[kSlots];
   DevBuf<float> partial[kSlots];   // per-slot sample-group sums
   DevBuf<int> spill[kSlots];       // traversal stack entries beyond PT_STACK
   DevBuf<uint32_t> counter[kSlots];
@@ -350,6 +352,7 @@ int pt_destroy(pt_ctx* c) {
     c->tiles[k].release();
     c->blocks[k].release();
     c->tblock0[k].release();
+    c->tout[k].release();
     c->spill[k].release();
     c->partial[k].release();
     c->counter[k].release();
@@ -1145,12 +1148,48 @@ static int frames_that_fit(const pt_ctx* c, const std::vector<int4>& tl, int nf)
 // (pt_render_frames_device) -- nf frames of these tiles, frame f keyed by
 // seeds[f] into outs[f], in ONE render launch (the MF kernel) and nf resolves;
 // `seeds` null: the parameters' seed.
-static int launch(pt_ctx* c, const std::vector<int4>& tl, float* const* outs, int nf, const uint32_t* seeds,
+static int launch(pt_ctx* c, const std::vector<int4>& tl_in, float* const* outs, int nf, const uint32_t* seeds,
                   hipStream_t s, uint32_t flags) {
   const bool stats = (flags & (PT_FLAG_STATS | PT_FLAG_REF_COUNTS)) != 0;
   std::memset(&c->last, 0, sizeof(c->last));
   c->times_pending = false;
-  if (tl.empty()) return PT_OK;
+  if (tl_in.empty()) return PT_OK;
+  // Large launches over trees larger than two XCD L2s render their tiles in
+  // Z-order (the queue bands below then deal each XCD a compact region
+  // rather than a strip of rows: C5 +2.5%, c5big +2.7%; C4's 4-MB tree,
+  // without bands, -0.5% in Z-order, keeps the rows: profiles/r6/
+  // ab_tile_zorder.txt).  Images are per
+  // pixel and sample, identical in any order; packed outputs keep the
+  // caller's tile index (tile_out).  PT_TILE_ZORDER=0/1 forces it (A/B, tests).
+  std::vector<int4> tz;
+  std::vector<int> tperm;
+  {
+    int64_t px = 0;
+    int edge = 1;  // the tile edge: the largest tile's (clipped edge tiles are smaller)
+    for (const int4& t : tl_in) {
+      px += (int64_t)t.z * t.w;
+      edge = std::max(edge, std::max(t.z, t.w));
+    }
+    bool z = tl_in.size() > 1 && px >= ((int64_t)1 << 20) &&
+             (int64_t)c->n_render_nodes * 128 > ((int64_t)PT_BANDS_TREE_MIB << 20);
+    if (const char* zo = std::getenv("PT_TILE_ZORDER")) z = tl_in.size() > 1 && std::atoi(zo) != 0;
+    if (z) {
+      std::vector<uint64_t> key(tl_in.size());
+      for (size_t i = 0; i < tl_in.size(); ++i) {
+        const uint64_t cx = (uint64_t)std::max(0, tl_in[i].x / edge), cy = (uint64_t)std::max(0, tl_in[i].y / edge);
+        uint64_t k = 0;
+        for (int b = 0; b < 21; ++b) k |= ((cx >> b) & 1ull) << (2 * b) | ((cy >> b) & 1ull) << (2 * b + 1);
+        key[i] = k;
+      }
+      tperm.resize(tl_in.size());
+      for (size_t i = 0; i < tperm.size(); ++i) tperm[i] = (int)i;
+      std::stable_sort(tperm.begin(), tperm.end(), [&](int a, int b) { return key[a] < key[b]; });
+      tz.resize(tl_in.size());
+      for (size_t i = 0; i < tz.size(); ++i) tz[i] = tl_in[tperm[i]];
+    }
+  }
+  const std::vector<int4>& tl = tperm.empty() ? tl_in : tz;
+  c->last.tile_zorder = tperm.empty() ? 0 : 1;
   // PT_PIPELINE=0: every render on the caller's stream, one slot (A/B).  A
   // census launch (PT_CENSUS) writes its per-wave records into the one shared
   // trace area, so it never overlaps another launch: it runs unpipelined too.
@@ -1247,6 +1286,16 @@ static int launch(pt_ctx* c, const std::vector<int4>& tl, float* const* outs, in
   P.env_rtheta = c->env_rtheta.p;
   P.env_rphi = c->env_rphi.p;
   P.tiles = c->tiles[slot].p;
+  P.tile_out = nullptr;
+  if (!tperm.empty() && (flags & (PT_FLAG_PACKED | PT_FLAG_PACKED16))) {
+    std::vector<int>& oh = c->tout_host[slot];
+    if (oh != tperm) {
+      oh = tperm;
+      HIPCHK(c->tout[slot].reserve(oh.size()));
+      HIPCHK(hipMemcpyAsync(c->tout[slot].p, oh.data(), oh.size() * sizeof(int), hipMemcpyHostToDevice, rs));
+    }
+    P.tile_out = c->tout[slot].p;
+  }
   P.out = outs[0];
   P.packed = (flags & PT_FLAG_PACKED16) ? 16 : (flags & PT_FLAG_PACKED) ? 32 : 0;
   P.work_counter = c->counter[slot].p;

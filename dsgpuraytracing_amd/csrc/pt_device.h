@@ -275,6 +275,7 @@ struct KParams {
   const struct EnvRec* env_rtheta;  // bucket records of env_ptheta (PT_ENV_GUIDE)
   const struct EnvRec* env_rphi;    // bucket records of the rows of env_pphi (h x PT_ENV_GUIDE)
   const int4* tiles;  // (x, y, w, h)
+  const int* tile_out;  // packed slot of launched tile i (the caller's index; null: i) -- a Z-ordered launch
   float* out;         // W*H*3, or n_tiles*1024*3 when packed
   int packed;         // packed slot edge S (PT_FLAG_PACKED: 32, PT_FLAG_PACKED16: 16; 0: the frame):
                       // tile i's pixel (x, y) -> out[3 * (i*S*S + (y-ty)*S + (x-tx))]

@@ -1723,7 +1723,8 @@ __global__ __launch_bounds__(256) void resolve_kernel(KParams P) {
     for (int i = tid; i < PT_QUEUE_WORDS * PT_QUEUE_HEADS; i += 256) P.work_counter[i] = 0u;
   auto out_at = [&](int x, int y) -> float* {
     const size_t ps = (size_t)P.packed;  // packed slot edge (32, or 16 with PT_FLAG_PACKED16); 0: the frame
-    const size_t o = ps ? (size_t)ti * ps * ps + (size_t)(y - tile.y) * ps + (size_t)(x - tile.x)
+    const size_t oi = P.tile_out ? (size_t)P.tile_out[ti] : (size_t)ti;  // (the caller's tile index)
+    const size_t o = ps ? oi * ps * ps + (size_t)(y - tile.y) * ps + (size_t)(x - tile.x)
                         : (size_t)x + (size_t)y * (size_t)P.W;
     return P.out + 3 * o;
   };

@@ -96,7 +96,7 @@ class pt_stats(ctypes.Structure):
                 ("wave_span", c_int64 * 5), ("group_spp", c_int32), ("lane_iters", c_int64 * 4),
                 ("deep_stack_steps", c_int64), ("partial_bytes", c_int64),
                 ("footprint", c_int32 * 4), ("slot_latency_hist", c_int64 * 32), ("node_census", c_int64 * 8),
-                ("frames_per_launch", c_int32), ("reserved0", c_int32)]
+                ("frames_per_launch", c_int32), ("tile_zorder", c_int32)]
 
 
 # Every symbol include/ptgpu.h and include/ptgpu_scene.h declare, with ctypes signatures.

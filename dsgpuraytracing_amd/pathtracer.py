@@ -190,6 +190,7 @@ class Device:
         out["footprint"] = list(s.footprint)
         out["node_census"] = list(s.node_census)
         out["frames_per_launch"] = int(s.frames_per_launch)
+        out["tile_zorder"] = int(s.tile_zorder)
         return out
 
     def launch_times(self, n: int = 256):

@@ -233,7 +233,8 @@ typedef struct pt_stats {
                               breadth-first order); the same for three levels (< 85) */
   int32_t frames_per_launch; /* frames the last render launch held (pt_render_frames_device batches: up to
                                 PT_MAX_FRAMES; 1 otherwise) */
-  int32_t reserved0;
+  int32_t tile_zorder; /* 1: the last launch rendered its tiles in Z-order (large frames over trees above
+                          PT_BANDS_TREE_MIB; PT_TILE_ZORDER=0/1 forces it) -- the same image */
 } pt_stats;
 
 #define PT_FLAG_STATS 1u /* count rays / node visits / primitive tests (slower build of the kernel) */

@@ -1153,3 +1153,48 @@ def test_packed16_tiles_match_frame():
                                     packed=16)
     finally:
         dev.close()
+
+
+@pytest.mark.parametrize("packed", [0, 32, 16])
+def test_zorder_launch_is_bit_identical(monkeypatch, packed):
+    """PT_TILE_ZORDER=1 (the library's Z-ordered launch of large frames over
+    large trees, forced here on a small one): the frame -- and a rank's packed
+    share, whose slots keep the caller's tile order (tile_out) -- equals the
+    row-major launch, one frame per launch and as a frame batch."""
+    import torch
+
+    from dsgpuraytracing_amd import scenes
+    from dsgpuraytracing_amd.dist import shard_tiles
+    from dsgpuraytracing_amd.pathtracer import Device
+
+    w, h, spp = 200, 136, 8  # ragged last tile row and column
+    edge = packed or 32
+    sc = Scene.from_dae(scenes.proxy_path(1), w, h)
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream(device=0)
+    dev = Device(0)
+    try:
+        dev.upload_scene(sc)
+        dev.set_camera(sc.camera)
+        dev.set_params(w, h, spp, 4, 1, 5)
+        tiles = [(x, y, min(edge, w - x), min(edge, h - y)) for (x, y, _, _) in tile_fifo(w, h, edge)]
+        mine = shard_tiles(tiles, 1, 3, "diag", edge) if packed else tiles
+        arr = np.asarray(mine, np.int32).reshape(-1, 4)
+        n = len(mine) * edge * edge * 3 if packed else w * h * 3
+        outs = {}
+        for z in ("0", "1"):
+            monkeypatch.setenv("PT_TILE_ZORDER", z)
+            one = torch.full((n,), -1.0, dtype=torch.float32, device="cuda:0")
+            dev.render_tiles_device(arr, one.data_ptr(), stream.cuda_stream, packed=packed, out_floats=n)
+            torch.cuda.synchronize()
+            assert dev.stats()["tile_zorder"] == int(z)
+            two = [torch.full_like(one, -1.0) for _ in range(2)]
+            dev.render_frames_device(arr, [b.data_ptr() for b in two], [5, 5], stream.cuda_stream, packed=packed,
+                                     out_floats=n)
+            torch.cuda.synchronize()
+            assert torch.equal(two[0], one) and torch.equal(two[1], one)
+            outs[z] = one.cpu()
+        assert torch.equal(outs["0"], outs["1"])
+        assert (outs["1"] >= 0).any()
+    finally:
+        dev.close()
