@@ -7,7 +7,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 WL=${1:-c3}
 STEPS=${2:-5}
-B="python3 bench.py --workload $WL --steps $STEPS --warmup 2 --no-cpu-baseline --no-extras"
+WARM=2; [ "$WL" = c3 ] && WARM=8  # (C3: 8 frames per launch -- whole batches only, as tools/profile_session.sh)
+B="python3 bench.py --workload $WL --steps $STEPS --warmup $WARM --no-cpu-baseline --no-extras"
 P="rocprofv3 --output-format csv"
 I="PT_PIPELINE=0"  # every render alone: counts per launch
 exec tools/gpu_session.sh \
