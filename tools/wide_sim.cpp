@@ -192,12 +192,13 @@ static int emit(Tree& t, int64_t b) {
   return me;
 }
 
-// SAH-optimal collapse of the binary tree into a 4-wide tree (dynamic
-// programming over (binary node, slots), after Ylitie et al. 2017 at width 4):
+// SAH-optimal collapse of the binary tree into a g_W-wide tree (4 or 8; dynamic
+// programming over (binary node, slots), after Ylitie et al. 2017):
 // cost(n, i) = the least expected steps of n's subtree when it fills at most
 // i slots of its parent; a node step and a leaf step of two primitives cost
 // one each, weighted by surface area.
-static std::vector<double> dpc;   // [n * 5 + i]
+static int g_W = 4;                // the collapse's width (slots per node)
+static std::vector<double> dpc;   // [n * 9 + i]
 static std::vector<int8_t> dpk;   // split of best_dist(n, i): slots for the left child; 0 = n kept whole
 static double sa(int64_t b) {
   double dx = B[b].bb_max[0] - B[b].bb_min[0], dy = B[b].bb_max[1] - B[b].bb_min[1], dz = B[b].bb_max[2] - B[b].bb_min[2];
@@ -206,9 +207,9 @@ static double sa(int64_t b) {
 static double g_cn = 1.0, g_cl = 1.0;
 static void dp_solve(int64_t b) {
   if (is_leaf(b)) {
-    for (int i = 1; i <= 4; ++i) {
-      dpc[b * 5 + i] = sa(b) * g_cl * ((B[b].range + 1) / 2);
-      dpk[b * 5 + i] = 0;
+    for (int i = 1; i <= g_W; ++i) {
+      dpc[b * 9 + i] = sa(b) * g_cl * ((B[b].range + 1) / 2);
+      dpk[b * 9 + i] = 0;
     }
     return;
   }
@@ -219,7 +220,7 @@ static void dp_solve(int64_t b) {
     double best = 1e300;
     bk = 1;
     for (int k = 1; k < j; ++k) {
-      double c = dpc[L * 5 + k] + dpc[R * 5 + (j - k)];
+      double c = dpc[L * 9 + k] + dpc[R * 9 + (j - k)];
       if (c < best) {
         best = c;
         bk = k;
@@ -228,40 +229,40 @@ static void dp_solve(int64_t b) {
     return best;
   };
   int k4;
-  const double node = sa(b) * g_cn + dist(4, k4);
-  dpc[b * 5 + 1] = node;
-  dpk[b * 5 + 1] = 0;
-  for (int i = 2; i <= 4; ++i) {
+  const double node = sa(b) * g_cn + dist(g_W, k4);
+  dpc[b * 9 + 1] = node;
+  dpk[b * 9 + 1] = 0;
+  for (int i = 2; i <= g_W; ++i) {
     int k;
     const double d = dist(i, k);
-    if (d < dpc[b * 5 + i - 1]) {
-      dpc[b * 5 + i] = d;
-      dpk[b * 5 + i] = (int8_t)k;
+    if (d < dpc[b * 9 + i - 1]) {
+      dpc[b * 9 + i] = d;
+      dpk[b * 9 + i] = (int8_t)k;
     } else {
-      dpc[b * 5 + i] = dpc[b * 5 + i - 1];
-      dpk[b * 5 + i] = -1;  // as with i - 1 slots
+      dpc[b * 9 + i] = dpc[b * 9 + i - 1];
+      dpk[b * 9 + i] = -1;  // as with i - 1 slots
     }
   }
 }
 // the subtrees that fill (at most) i slots for binary node b
 static void dp_collect(int64_t b, int i, std::vector<int64_t>& out) {
-  while (i > 1 && dpk[b * 5 + i] == -1) --i;
+  while (i > 1 && dpk[b * 9 + i] == -1) --i;
   if (i == 1 || is_leaf(b)) {
     out.push_back(b);
     return;
   }
-  const int k = dpk[b * 5 + i];
+  const int k = dpk[b * 9 + i];
   dp_collect(B[b].left, k, out);
   dp_collect(B[b].right, i - k, out);
 }
 static int emit_dp(Tree& t, int64_t b) {
-  // b is an internal node kept whole: its children distributed over 4 slots
+  // b is an internal node kept whole: its children distributed over g_W slots
   std::vector<int64_t> kids;
   int k4 = 1;
   {
     double best = 1e300;
-    for (int k = 1; k < 4; ++k) {
-      double c = dpc[B[b].left * 5 + k] + dpc[B[b].right * 5 + (4 - k)];
+    for (int k = 1; k < g_W; ++k) {
+      double c = dpc[B[b].left * 9 + k] + dpc[B[b].right * 9 + (g_W - k)];
       if (c < best) {
         best = c;
         k4 = k;
@@ -269,7 +270,7 @@ static int emit_dp(Tree& t, int64_t b) {
     }
   }
   dp_collect(B[b].left, k4, kids);
-  dp_collect(B[b].right, 4 - k4, kids);
+  dp_collect(B[b].right, g_W - k4, kids);
   std::vector<Child> ch;
   for (int64_t x : kids) ch.push_back(child_of(t, x));
   int me = (int)t.nodes.size();
@@ -463,15 +464,21 @@ int main(int argc, char** argv) {
   emit(t2, 0);
   emit(t8s, 0);
   emit(t4s, 0);
-  Tree t4d;
+  Tree t4d, t8d;
   t4d.W = 4;
-  dpc.assign(B.size() * 5, 0.0);
-  dpk.assign(B.size() * 5, 0);
+  t8d.W = 8;
+  dpc.assign(B.size() * 9, 0.0);
+  dpk.assign(B.size() * 9, 0);
   if (const char* c = std::getenv("WS_CN")) g_cn = std::atof(c);
   dp_solve(0);
   emit_dp(t4d, 0);
   std::printf("BVH4 greedy nodes %zu, BVH4 dp nodes %zu (dp expected steps %.4f per root area)\n", t4.nodes.size(),
-              t4d.nodes.size(), dpc[0 * 5 + 1] / sa(0));
+              t4d.nodes.size(), dpc[0 * 9 + 1] / sa(0));
+  g_W = 8;  // the same DP at width 8
+  dp_solve(0);
+  emit_dp(t8d, 0);
+  std::printf("BVH8 greedy nodes %zu, BVH8 dp nodes %zu (dp expected steps %.4f per root area)\n", t8.nodes.size(),
+              t8d.nodes.size(), dpc[0 * 9 + 1] / sa(0));
   auto fill = [](const Tree& t) { double c = 0; for (auto& n : t.nodes) c += n.n; return c / t.nodes.size(); };
   std::printf("children per node: BVH4 %.2f, BVH8 %.2f, BVH8 split %.2f, BVH4 split %.2f\n", fill(t4), fill(t8), fill(t8s), fill(t4s));
   std::printf("prims %lld, binary nodes %lld, BVH4 nodes %zu, BVH8 nodes %zu, leaves %zu\n", (long long)sc.n_prims,
@@ -539,7 +546,7 @@ int main(int argc, char** argv) {
   } layouts[] = {{"BVH2", &t2, SORT},        {"BVH4 sort", &t4, SORT},       {"BVH8 sort", &t8, SORT},
                  {"BVH8 octant", &t8, OCT},  {"BVH8 near+slot", &t8, NEAR_SLOT}, {"BVH8 near+oct", &t8, NEAR_OCT},
                  {"BVH8 fp16 sort", &t8q, SORT}, {"BVH8 fp16 n+slot", &t8q, NEAR_SLOT},
-                 {"BVH4 near+slot", &t4, NEAR_SLOT}, {"BVH4 dp sort", &t4d, SORT}};
+                 {"BVH4 near+slot", &t4, NEAR_SLOT}, {"BVH4 dp sort", &t4d, SORT}, {"BVH8 dp sort", &t8d, SORT}};
   for (int s = 0; s < 3; ++s) {
     std::printf("-- %s rays (%zu)\n", names[s], sets[s]->size());
     for (const L& l : layouts) {
